@@ -1,0 +1,108 @@
+/*
+ * nanotel_oracle.h -- CPU restatement of NanoTel's telomere hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This library is the *checker*: only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg may load it.  The
+ * product path (telomere-analyzer_amd/) never links or calls it.
+ *
+ * It restates, function by function, the R code of NanoTel.R (Tzfatilab/
+ * Telomere-Analyzer @ v1.1.9-beta) together with the semantics of the
+ * un-vendored Bioconductor C code it calls:
+ *   - Biostrings 2.66/2.68 matchPattern (naive-inexact / boyer-moore semantics,
+ *     including out-of-bound positions counted as mismatches),
+ *   - IRanges 2.32/2.34 trim / union(=reduce of concatenation) / intersect.
+ * It deliberately uses the *range-list* representation of the reference
+ * (views, reduce, intersect) and not the bitmask representation used by the
+ * HIP kernels, so that the two are independent.
+ *
+ * Parity pinning: reproduces Example/Example_output/summary.csv (all 40
+ * numeric cells, legacy mode = no edge extension) and all 1,974 per-window
+ * densities encoded in Example_output/single_read_plots_adj/read*.eps
+ * (see tests/test_oracle_golden.py).
+ */
+#ifndef NANOTEL_ORACLE_H
+#define NANOTEL_ORACLE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NTO_MAX_PAT 16   /* patterns per list (after unique) */
+#define NTO_MAX_M   64   /* longest pattern accepted by the parser */
+
+/* Error codes (negative). */
+#define NTO_OK             0
+#define NTO_E_EMPTY_PAT   -1   /* matchPattern(""): "empty pattern" */
+#define NTO_E_BAD_LETTER  -2   /* letter outside DNA_ALPHABET */
+#define NTO_E_PAT_LONG    -3   /* testit::assert(str_length(pattern) <= 18) NanoTel.R:589,647 */
+#define NTO_E_EMPTY_READ  -4   /* seq(1, 0, by=L) errors in split_telo NanoTel.R:216 */
+#define NTO_E_RIGHT_EMPTY -5   /* find_right_telo on a 0-row table: if(logical(0)) NanoTel.R:861 */
+#define NTO_E_NEG_WIDTH   -6   /* IRanges(start, end) with end < start-1 */
+#define NTO_E_ARG         -7
+#define NTO_E_NOMEM       -8
+
+typedef struct nto_patterns nto_patterns;
+
+/* A1: extract_patterns (NanoTel.R:2322-2334) + fixed test (NanoTel.R:334). */
+nto_patterns* nto_patterns_new(const char* patterns, const char* tvr_patterns,
+                               int* err_out);
+void nto_patterns_free(nto_patterns* p);
+int  nto_patterns_npass(const nto_patterns* p);      /* 2, or 3 with TVRs */
+int  nto_patterns_count(const nto_patterns* p, int tvr);
+
+/* Biostrings DNA letter code (A=1 C=2 G=4 T=8 ... N=15 '-'=16 '+'=32 '.'=64),
+ * case-insensitive; 0 = not a DNA letter. */
+uint8_t nto_dna_code(char c);
+
+/* Biostrings::matchPattern(pattern, subject, max.mismatch=k, fixed=fixed).
+ * Writes 1-based view starts (may be <1 or > n-m+1: out-of-bound matches).
+ * Returns the number of matches (or <0 on error).  starts may be NULL. */
+int64_t nto_match_pattern(const char* pattern, const char* subject, int64_t n,
+                          int k, int fixed, int32_t* starts, int64_t cap);
+
+/* split_telo (NanoTel.R:199-227): number of windows for a read of length n. */
+int64_t nto_window_count(int64_t n, int L);
+
+/* Reverse complement in place (Biostrings::reverseComplement, NanoTel.R:2220). */
+int nto_reverse_complement(char* seq, int64_t n);
+
+typedef struct {
+  int32_t start[3];     /* final called range per pass (P1 exact, P2 mm1, P3 mm1+TVR) */
+  int32_t end[3];
+  int64_t width[3];     /* IRanges width = end - start + 1 */
+  double  density[3];   /* get_sub_density(called range, pass ranges) */
+  int32_t na[3];        /* 1 if start == -1 (NA columns) */
+  int32_t n_pass;
+  int32_t telomeric;    /* 1 = row emitted (max width >= 30), NanoTel.R:1847-1868 */
+  int64_t n_windows;
+} nto_row;
+
+/* analyze_read (NanoTel.R:1774-1976) minus plots/IO.
+ * win_counts: optional [n_pass][n_windows] covered-base counts per window.
+ * hit_counts: optional [2*n_pat + n_tvr]: length(matchPattern) for each
+ *   pattern at k=0, each pattern at k=1, each TVR at k=0 (unique lists).
+ * legacy_no_ext: skip search_left/right_patterns (NanoTel.R:1140-1149), i.e.
+ *   the 2023 code version that produced Example/Example_output. */
+int nto_analyze_read(const char* seq, int64_t n, const nto_patterns* P, int L,
+                     double min_density, int right_edge, int legacy_no_ext,
+                     nto_row* row, uint32_t* win_counts, uint32_t* hit_counts);
+
+/* A15: serial numbers and row order for one chunk (NanoTel.R:2234-2258,
+ * 2050-2070).  is_telo[n] (chunk reads in stream order);
+ * serial_start_io: in = this chunk's serial_start (1 for the first chunk,
+ *   NanoTel.R:2208), out = next chunk's serial_start = max(all Serial)+1
+ *   (NanoTel.R:2258; -Inf while no row exists, max(numeric(0)));
+ * max_serial_io: running max over all rows so far (-Inf initially);
+ * serial_out[n]: serial of each read (NaN if not telomeric);
+ * order_out[rows]: read index of each emitted row in data-frame order
+ *   (group-major, NanoTel.R:2254).  Returns the number of rows emitted. */
+int64_t nto_assign_serials(const uint8_t* is_telo, int64_t n,
+                           double* serial_start_io, double* max_serial_io,
+                           double* serial_out, int64_t* order_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
