@@ -99,7 +99,8 @@ def test_window_split_rules():
     assert O.window_count(151, 100) == 2
     assert O.window_count(50, 100) == 0
     assert O.window_count(51, 100) == 1
-    assert O.window_count(1, 1) == 1
+    assert O.window_count(1, 1) == 0  # 1 - 1 < 0.5: the only window is dropped
+    assert O.window_count(2, 1) == 1
 
 
 def test_pattern_parsing_errors():
