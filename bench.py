@@ -1,0 +1,196 @@
+"""Throughput of the NanoTel hot path on MI355X (BASELINE.json metric).
+
+One step = one launch of the fused scan+call kernel over a device-resident
+batch of synthetic long reads (generated on the GPU by the counter-based
+generator of nt_rng.h; inputs resident in HBM before the timed region):
+  matchPattern TTAGGG exact + 1-mismatch (OOB rule), coverage, per-window
+  densities for both passes, telomere calling (A8-A12) and summary rows.
+
+N GPUs: one process per GPU (torch.distributed, RCCL), each rank scans its own
+shard of reads (first_read = rank * reads) -> weak scaling, no data-path
+collective.  value = bases of all ranks / max-over-ranks time.
+
+python bench.py --gpus N --steps K --warmup W [--config c50k|c10k]
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "telomere-analyzer_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+CONFIGS = {
+    # BASELINE.json metric: "Gbases/s scanned (TTAGGG, 50 kb reads)", configs[1]'s read count
+    "c50k": dict(reads=1_000_000, read_len=50_000, patterns="TTAGGG", tvr=None, rc=False, variant=0.0,
+                 desc="1M synthetic 50 kb reads / GPU, TTAGGG, P1 exact + P2 1-mismatch"),
+    # BASELINE.json configs[1]
+    "c10k": dict(reads=1_000_000, read_len=10_000, patterns="TTAGGG", tvr=None, rc=False, variant=0.0,
+                 desc="1M synthetic 10 kb reads / GPU, TTAGGG, P1 + P2"),
+}
+
+
+def algorithmic_bytes_per_read(read_len, n_pass, n_windows):
+    # planes (2 bits/base, 32-base blocks) + blk_off + len + win_off
+    # + window counts written (uint16 per window per pass)
+    # + row written: start/end int32 x3, density f64 x3, flags u8
+    blocks = (read_len + 31) // 32
+    return blocks * 8 + 8 + 4 + 8 + n_windows * n_pass * 2 + 3 * 4 * 2 + 3 * 8 + 1
+
+
+def cpu_baseline(cfg, budget_s=12.0, max_reads=64):
+    """CPU oracle (restatement, single core) on the first reads of the same
+    synthetic workload (host twin of the device generator)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _oracle as O
+    from nanotel_amd import synth_params, synth_read_ascii
+    sp = synth_params(read_len=cfg["read_len"], variant_rate=cfg["variant"], rc_layout=cfg["rc"])
+    P = O.Patterns(cfg["patterns"], cfg["tvr"])
+    done = bases = 0
+    t0 = time.perf_counter()
+    elapsed = 0.0
+    while done < max_reads and elapsed < budget_s:
+        s = synth_read_ascii(sp, done)
+        if cfg["rc"]:
+            s = O.reverse_complement(s)
+        t1 = time.perf_counter()
+        O.analyze_read(s, P)
+        elapsed += time.perf_counter() - t1
+        done += 1
+        bases += len(s)
+    return {"value": bases / elapsed / 1e9, "unit": "Gbases/s", "cores": 1, "kind": "port",
+            "sample": f"{done} reads x {cfg['read_len']} bases of the same synthetic workload, "
+                      f"oracle/nanotel_oracle.c (C restatement, -O2, 1 thread), {elapsed:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c50k", choices=sorted(CONFIGS))
+    ap.add_argument("--reads", type=int, default=0, help="override reads per GPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    from nanotel_amd import NanoTel, synth_params, window_count
+
+    cfg = dict(CONFIGS[args.config])
+    if args.reads:
+        cfg["reads"] = args.reads
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    n = cfg["reads"]
+    L = cfg["read_len"]
+    nt = NanoTel(patterns=cfg["patterns"], tvr_patterns=cfg["tvr"], rc=False, device=local)
+    stream = torch.cuda.current_stream(dev)
+    nt.set_stream(stream.cuda_stream)
+    npass = nt.n_pass
+    nblk = (L + 31) // 32
+    nw = window_count(L, 100)
+    planes = torch.empty(n * nblk * 2, dtype=torch.int32, device=dev)
+    blk_off = torch.empty(n, dtype=torch.int64, device=dev)
+    lens = torch.empty(n, dtype=torch.int32, device=dev)
+    win_off = torch.empty(n, dtype=torch.int64, device=dev)
+    wc = torch.empty(n * nw * npass, dtype=torch.int16, device=dev)
+    start = torch.empty(n * 3, dtype=torch.int32, device=dev)
+    end = torch.empty(n * 3, dtype=torch.int32, device=dev)
+    dens = torch.empty(n * 3, dtype=torch.float64, device=dev)
+    flags = torch.empty(n, dtype=torch.uint8, device=dev)
+    sp = synth_params(first_read=rank * n, read_len=L, variant_rate=cfg["variant"], rc_layout=cfg["rc"])
+    nt.synth_device(sp, n, planes.data_ptr())
+    nt.uniform_layout_device(n, L, blk_off.data_ptr(), lens.data_ptr(), win_off.data_ptr())
+    torch.cuda.synchronize(dev)
+
+    def step():
+        nt.scan_call_device(planes.data_ptr(), blk_off.data_ptr(), lens.data_ptr(), win_off.data_ptr(),
+                            n, L, start.data_ptr(), end.data_ptr(), dens.data_ptr(), flags.data_ptr(),
+                            win_counts=wc.data_ptr())
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+    t0 = time.perf_counter()
+    evs[0].record(stream)
+    for i in range(args.steps):
+        step()
+        evs[i + 1].record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    wall = t1 - t0
+    kern_ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)]
+    if world > 1:
+        t = torch.tensor([wall], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall = float(t.item())
+
+    telo = int(((flags & 1) != 0).sum().item())
+    total_bases = n * L * world * args.steps
+    value = total_bases / wall / 1e9
+    avg_kern_s = sum(kern_ms) / len(kern_ms) / 1e3
+    bytes_per_launch = n * algorithmic_bytes_per_read(L, npass, nw)
+    achieved = bytes_per_launch / avg_kern_s / 1e9
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            tj = json.load(open(args.traffic_json))
+            if tj.get("config") == args.config and tj.get("reads") == n:
+                traffic = tj.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    if rank == 0:
+        out = {
+            "metric": "Gbases/s scanned (TTAGGG, 50 kb reads)" if args.config == "c50k"
+            else "Gbases/s scanned (TTAGGG, 10 kb reads)",
+            "value": round(value, 3),
+            "unit": "Gbases/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(wall / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32 (2-bit planes, integer scan; fp64 densities)",
+            "data": "synthetic (device counter-based generator, seed 20260501)",
+            "config": {"workload": cfg["desc"], "reads_per_gpu": n, "read_len": L,
+                       "patterns": cfg["patterns"], "subseq_length": 100, "min_density": 0.6,
+                       "passes": npass, "telomeric_reads_rank0": telo,
+                       "parallelism": f"dp{world} (read shards)"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": traffic,
+                         "kernel": "nt_scan_call_kernel<false>",
+                         "kernel_avg_ms": round(avg_kern_s * 1e3, 4),
+                         "algorithmic_bytes_per_launch": bytes_per_launch},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(cfg)
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

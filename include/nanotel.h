@@ -1,0 +1,160 @@
+/*
+ * nanotel.h -- C-ABI of the MI355X-native NanoTel hot path.
+ *
+ * Drop-in boundary: one call per chunk replaces the per-chunk block of
+ * NanoTel.R's run_future_worker_chuncks (NanoTel.R:2234-2256: the `< 8 reads`
+ * sequential search_patterns call, or the 8 forked `%<-% search_patterns`
+ * futures and their Reduce(union_all)), i.e. everything below
+ * readDNAStringSet/reverseComplement and above write_csv:
+ *
+ *   reference interface (NanoTel.R)                  replaced by
+ *   ------------------------------------------------ ----------------------------
+ *   extract_patterns + fixed test   :2322-2334, :334 nt_compile
+ *   reverseComplement(dna_reads)    :2219-2221       nt_params.rc (nt_pack_reads)
+ *   analyze_subtelos / get_density_iranges / split_telo / get_sub_density
+ *                                   :717-766, :308-397, :199-227, :449-468
+ *                                                    nt_scan_call (window counts)
+ *   find_telo_position_wraper and callees :1080-1155, :973-1077, :1692-1764,
+ *                                   :843-959, :496-697   nt_scan_call (rows)
+ *   analyze_read row logic          :1774-1862, :1920-1976 nt_scan_call (rows)
+ *   search_patterns serials + 8-way split/union_all :2001-2078, :2234-2258
+ *                                                    nt_assign_serials
+ *
+ * Conventions: plain pointers and sizes only; 0 = NT_OK, negative = error,
+ * message via nt_last_error(ctx).  Positions are 1-based like IRanges; -1 is
+ * the reference's "no telomere" sentinel (NA in summary.csv).  A context is
+ * owned by one host thread.  HIP must not be initialised before a fork
+ * (R future::multicore): create the context in the process that calls.
+ */
+#ifndef NANOTEL_H
+#define NANOTEL_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NT_OK 0
+#define NT_E_ARG (-1)
+#define NT_E_PATTERN (-2)     /* empty pattern ("empty pattern"), letter outside DNA_ALPHABET,
+                                 or length > 18 (testit::assert NanoTel.R:589,647) */
+#define NT_E_LETTER (-3)      /* read letter outside DNA_ALPHABET (readDNAStringSet errors) */
+#define NT_E_EMPTY_READ (-4)  /* seq(1, 0, by=L) errors in split_telo (NanoTel.R:216) */
+#define NT_E_RIGHT_EMPTY (-5) /* --check_right_edge on a read with no window (NanoTel.R:861) */
+#define NT_E_NEG_WIDTH (-6)   /* IRanges(start, end) with end < start - 1 */
+#define NT_E_HIP (-7)
+#define NT_E_NOMEM (-8)
+#define NT_E_LIMIT (-9)       /* > 8 patterns, TVR > 32 letters, subseq_length > 43690 */
+#define NT_E_STATE (-10)      /* nt_compile() not called */
+
+/* summary flags per read */
+#define NT_ROW_TELOMERIC 0x01 /* row emitted: max telomere width >= 30 (NanoTel.R:1847) */
+#define NT_ROW_NA(p) (0x02 << (p)) /* pass p start == -1 -> NA columns (NanoTel.R:1926) */
+#define NT_ROW_DONE 0x80
+
+typedef struct nt_ctx nt_ctx;
+
+typedef struct {
+  const char* patterns;      /* --patterns, whitespace separated (required) */
+  const char* tvr_patterns;  /* --tvr_patterns or NULL */
+  int32_t subseq_length;     /* --subseq_length (100) */
+  double min_density;        /* --min_density (0.6) */
+  int32_t check_right_edge;  /* --check_right_edge */
+  int32_t rc;                /* --rc: reverse-complement every read before the scan */
+  int32_t legacy_no_ext;     /* test switch: 2023 code without search_left/right_patterns */
+} nt_params;
+
+typedef struct {
+  int32_t n_pass; /* 2 (exact, 1-mismatch) or 3 (+TVR) */
+  int32_t n_pat;  /* unique() patterns */
+  int32_t n_tvr;
+  int32_t n_hits; /* hit counters per read: 2*n_pat + n_tvr */
+  int32_t raw_p1; /* P1 keeps raw views (single fixed pattern) */
+} nt_program_info;
+
+/* Device-resident read batch (device pointers).  Layout: see DESIGN.md
+ * "HBM layout": planes = uint2 {lo,hi} bit planes per 32 bases. */
+typedef struct {
+  const uint32_t* planes;
+  const uint64_t* blk_off;  /* [n_reads] first 32-base block of each read */
+  const uint32_t* len;      /* [n_reads] */
+  const uint64_t* win_off;  /* [n_reads] prefix sum of split_telo window counts */
+  const uint32_t* exc_off;  /* [n_reads+1] or NULL: non-ACGT letters */
+  const uint32_t* exc_pos;
+  const uint8_t* exc_code;
+  uint64_t n_reads;
+} nt_batch;
+
+/* Device-resident outputs (device pointers). */
+typedef struct {
+  uint16_t* win_counts; /* [sum windows * n_pass] or NULL */
+  int32_t* start;       /* [n_reads*3] */
+  int32_t* end;         /* [n_reads*3] */
+  double* density;      /* [n_reads*3] */
+  uint8_t* flags;       /* [n_reads] */
+  uint32_t* hits;       /* [n_reads*n_hits] or NULL */
+} nt_out;
+
+typedef struct {
+  uint64_t seed;
+  uint64_t first_read;
+  uint64_t read_len;
+  double p_tract;       /* 0.5 */
+  double sub_rate;      /* 0.02 */
+  double variant_rate;  /* 0 (C2) / 0.05 (C3, C4) */
+  uint32_t tract_min;   /* 1000 */
+  uint32_t tract_max;   /* 15000 */
+  int32_t rc_layout;    /* tract at the right end (for --rc configs) */
+} nt_synth_params;
+
+const char* nt_version(void);
+
+/* --- context ------------------------------------------------------------ */
+int nt_create(int device, nt_ctx** out);
+void nt_destroy(nt_ctx* ctx);
+const char* nt_last_error(const nt_ctx* ctx);
+int nt_set_stream(nt_ctx* ctx, void* hip_stream); /* NULL = the context's own stream */
+int nt_synchronize(nt_ctx* ctx);
+
+/* --- A1: patterns and flags (extract_patterns NanoTel.R:2322-2334) ------- */
+int nt_compile(nt_ctx* ctx, const nt_params* params, nt_program_info* info);
+
+/* --- host packing (A14 reverseComplement fused when params.rc) ----------- */
+int64_t nt_window_count(int64_t n, int32_t subseq_length);
+/* Pass 1: sizes.  Returns NT_E_LETTER (and *bad_read) on an invalid letter. */
+int nt_pack_count(const char* const* seqs, const uint64_t* lens, uint64_t n_reads,
+                  int32_t subseq_length, uint64_t* total_blocks, uint64_t* total_windows,
+                  uint64_t* total_exc, uint64_t* max_len, uint64_t* bad_read);
+/* Pass 2: fill host arrays sized by nt_pack_count (exc_* may be NULL when total_exc == 0). */
+int nt_pack_reads(const char* const* seqs, const uint64_t* lens, uint64_t n_reads, int32_t rc,
+                  int32_t subseq_length, uint32_t* planes, uint64_t* blk_off, uint32_t* len,
+                  uint64_t* win_off, uint32_t* exc_off, uint32_t* exc_pos, uint8_t* exc_code);
+
+/* --- the hot path --------------------------------------------------------- */
+/* Asynchronous on the context stream.  max_len = longest read of the batch. */
+int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t max_len);
+
+/* Host-buffer convenience: pack (+rc), upload, scan+call, download, sync.
+ * win_counts/hits optional.  Returns the first per-read error, if any. */
+int nt_analyze_host(nt_ctx* ctx, const char* const* seqs, const uint64_t* lens, uint64_t n_reads,
+                    int32_t* start, int32_t* end, double* density, uint8_t* flags,
+                    uint16_t* win_counts, uint32_t* hits);
+
+/* --- A15: serials and row order of one chunk (host only) ----------------- */
+/* Same contract as the reference: serial_start_io = this chunk's serial_start
+ * (1.0 first), becomes max(Serial)+1; max_serial_io running max (-Inf first). */
+int64_t nt_assign_serials(const uint8_t* is_telo, uint64_t n, double* serial_start_io,
+                          double* max_serial_io, double* serial_out, int64_t* order_out);
+
+/* --- synthetic long reads (bench / tests) --------------------------------- */
+int nt_synth_device(nt_ctx* ctx, const nt_synth_params* sp, uint64_t n_reads, uint32_t* planes_dev);
+int nt_uniform_layout_device(nt_ctx* ctx, uint64_t n_reads, uint64_t read_len, int32_t subseq_length,
+                             uint64_t* blk_off_dev, uint32_t* len_dev, uint64_t* win_off_dev);
+int nt_synth_ascii(const nt_synth_params* sp, uint64_t read_index, char* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

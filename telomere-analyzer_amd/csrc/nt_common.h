@@ -1,0 +1,72 @@
+// nt_common.h -- structures shared by the host library and the gfx950 kernels.
+//
+// HBM layout of a read batch ("bit-plane 2-bit packing"):
+//   planes[b] = {lo, hi} (two uint32) for the 32-base block b; bit i of lo/hi is
+//   the low/high bit of the 2-bit code of base 32*b+i (A=0 C=1 G=2 T=3).
+//   Read r occupies blocks [blk_off[r], blk_off[r] + ceil(len[r]/32)); padding
+//   bits past the read end are zero.  Letters other than A/C/G/T (N, IUPAC
+//   ambiguity codes, '-', '+', '.') are stored as A in the planes and listed in
+//   a per-read exception list (position, Biostrings DNA code) -- see
+//   DESIGN.md "Exceptions".
+// Window counts: uint16 at win_counts[win_off[r]*n_pass + p*nw(r) + i]
+//   (covered bases of window i of pass p; nw = split_telo window count).
+#pragma once
+#include <stdint.h>
+
+#define NT_MAX_PAT 8      // unique patterns per list (--patterns / --tvr_patterns)
+#define NT_MAX_M 18       // testit::assert(str_length(pattern) <= 18), NanoTel.R:589,647
+#define NT_MAX_TVR_M 32   // TVRs are only length-limited by the 32-bit start words
+#define NT_MAX_PASS 3
+
+// Per-read flag bits (rows.flags)
+#define NT_FLAG_TELOMERIC 0x01   // row emitted (max width >= 30), NanoTel.R:1847-1868
+#define NT_FLAG_NA_SHIFT 1       // bit 1+p: pass p start == -1 (NA columns)
+#define NT_FLAG_ERR_RIGHT 0x20   // find_right_telo on a 0-row window table (R errors)
+#define NT_FLAG_ERR_WIDTH 0x40   // IRanges(start, end) with negative width (R errors)
+#define NT_FLAG_DONE 0x80        // the kernel processed this read
+
+// One compiled pattern.  tt_scan[j]: 4-bit truth table over subject bases
+// A,C,G,T (bit c) for matchPattern(fixed = <regex test>) in
+// get_density_iranges; tt_eq[j]: the same for fixed=TRUE (code equality), used
+// by the edge-extension steps (NanoTel.R:502-566, 614, 676 call matchPattern
+// with the default fixed=TRUE).
+struct NtPat {
+  int32_t m;
+  int32_t fixed;               // !str_detect(pat, "[WSMKRYBDHVN]")
+  uint8_t code[NT_MAX_TVR_M];  // Biostrings DNA codes (for exception positions)
+  uint8_t tt_scan[NT_MAX_TVR_M];
+  uint8_t tt_eq[NT_MAX_TVR_M];
+};
+
+struct NtProgram {
+  int32_t n_pat, n_tvr;   // unique() lists
+  int32_t n_pass;         // 2, or 3 with --tvr_patterns
+  int32_t raw_p1;         // P1 keeps raw views: single fixed pattern (NanoTel.R:349-355)
+  int32_t L;              // --subseq_length
+  int32_t right_edge;     // --check_right_edge
+  int32_t legacy_no_ext;  // test switch: skip search_left/right_patterns (2023 code)
+  int32_t n_hits;         // 2*n_pat + n_tvr hit counters per read
+  double min_density;     // --min_density
+  NtPat pat[NT_MAX_PAT];
+  NtPat tvr[NT_MAX_PAT];
+};
+
+struct NtBatch {
+  const uint32_t* planes;   // uint2 blocks
+  const uint64_t* blk_off;  // [n_reads]
+  const uint32_t* len;      // [n_reads]
+  const uint64_t* win_off;  // [n_reads] prefix sum of window counts
+  const uint32_t* exc_off;  // [n_reads+1] or nullptr (no exceptions in batch)
+  const uint32_t* exc_pos;  // sorted per read, 0-based positions
+  const uint8_t* exc_code;  // Biostrings DNA codes
+  uint64_t n_reads;
+};
+
+struct NtOut {
+  uint16_t* win_counts;  // see layout above (may be nullptr)
+  int32_t* start;        // [n_reads*3], 1-based, -1 = NA
+  int32_t* end;          // [n_reads*3]
+  double* density;       // [n_reads*3]
+  uint8_t* flags;        // [n_reads]
+  uint32_t* hits;        // [n_reads*n_hits] or nullptr
+};

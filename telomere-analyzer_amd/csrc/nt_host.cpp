@@ -1,0 +1,627 @@
+// nt_host.cpp -- the C-ABI of include/nanotel.h: pattern compilation (A1),
+// host packing (+ reverse complement, A14), launches of the gfx950 kernels,
+// serial assignment (A15) and the synthetic-read generator.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "nanotel.h"
+#include "nt_common.h"
+#include "nt_rng.h"
+
+extern "C" {
+uint32_t nt_dev_lds_words(int64_t n, int L, int np);
+hipError_t nt_dev_launch_scan_call(const NtProgram* prog_dev, const NtBatch* B, const NtOut* O,
+                                   uint32_t len_lo, uint32_t len_hi, int global_scratch,
+                                   uint32_t* gscratch, uint64_t scratch_words, uint32_t lds_words,
+                                   int grid, hipStream_t stream);
+hipError_t nt_dev_set_lds_limit(uint32_t bytes);
+hipError_t nt_dev_launch_synth(const NtSynth* S, uint32_t* planes, uint64_t n_reads,
+                               hipStream_t stream);
+hipError_t nt_dev_launch_uniform_layout(uint64_t n_reads, uint64_t nblk, uint64_t read_len,
+                                        uint64_t nw, uint64_t* blk_off, uint32_t* len,
+                                        uint64_t* win_off, hipStream_t stream);
+}
+
+namespace {
+
+constexpr uint32_t kLdsCapBytes = 96 * 1024;  // per workgroup; longer reads use global scratch
+constexpr uint32_t kLdsStaticBytes = 512;
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= cap) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    const size_t want = std::max<size_t>(bytes, 256);
+    hipError_t e = hipMalloc(&p, want);
+    if (e == hipSuccess) cap = want;
+    return e;
+  }
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+};
+
+// Biostrings DNA_ALPHABET codes (A=1 C=2 G=4 T=8, IUPAC = OR, '-'=16 '+'=32 '.'=64);
+// lower case letters are upper-cased by DNAString().
+uint8_t letter_code(unsigned char c) {
+  static uint8_t tab[256];
+  static bool init = false;
+  if (!init) {
+    const char* up = "ACGTMRWSYKVHDBN";
+    const uint8_t codes[] = {1, 2, 4, 8, 3, 5, 9, 6, 10, 12, 7, 11, 13, 14, 15};
+    for (int i = 0; i < 15; ++i) {
+      tab[(unsigned char)up[i]] = codes[i];
+      tab[(unsigned char)(up[i] - 'A' + 'a')] = codes[i];
+    }
+    tab[(unsigned char)'-'] = 16;
+    tab[(unsigned char)'+'] = 32;
+    tab[(unsigned char)'.'] = 64;
+    init = true;
+  }
+  return tab[c];
+}
+
+// 2-bit code for A/C/G/T (either case), else -1.
+inline int base2(unsigned char c) {
+  switch (c) {
+    case 'A': case 'a': return 0;
+    case 'C': case 'c': return 1;
+    case 'G': case 'g': return 2;
+    case 'T': case 't': return 3;
+    default: return -1;
+  }
+}
+
+inline uint8_t complement_code(uint8_t x) {
+  return (uint8_t)((x & 0xF0) | ((x & 1) << 3) | ((x & 8) >> 3) | ((x & 2) << 1) | ((x & 4) >> 1));
+}
+
+int64_t window_count(int64_t n, int L) {
+  if (n <= 0 || L <= 0) return 0;
+  int64_t c = (n - 1) / L + 1;                      // seq(1, n, by = L)
+  const int64_t last_start = 1 + (c - 1) * (int64_t)L;
+  if ((double)(n - last_start) < (double)L / 2.0) c -= 1;  // NanoTel.R:220
+  return c;
+}
+
+template <class F>
+void parallel_for(uint64_t n, F&& f) {
+  unsigned nt = std::thread::hardware_concurrency();
+  if (nt == 0) nt = 1;
+  if (nt > 32) nt = 32;
+  if (n < 64 || nt == 1) {
+    for (uint64_t i = 0; i < n; ++i) f(i);
+    return;
+  }
+  std::vector<std::thread> th;
+  const uint64_t chunk = (n + nt - 1) / nt;
+  for (unsigned t = 0; t < nt; ++t) {
+    const uint64_t lo = t * chunk, hi = std::min<uint64_t>(n, lo + chunk);
+    if (lo >= hi) break;
+    th.emplace_back([lo, hi, &f] {
+      for (uint64_t i = lo; i < hi; ++i) f(i);
+    });
+  }
+  for (auto& x : th) x.join();
+}
+
+// One token list of --patterns / --tvr_patterns: str_split(x, "\\s+"), as.list
+// when > 1 token, unique() (NanoTel.R:2322-2334, 328, 362).
+int parse_tokens(const char* s, std::vector<std::string>& uniq, bool& is_list, std::string& err) {
+  std::vector<std::string> toks;
+  const char* p = s;
+  auto ws = [](char c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r' || c == '\f' || c == '\v'; };
+  for (;;) {
+    const char* b = p;
+    while (*p && !ws(*p)) ++p;
+    toks.emplace_back(b, p);
+    if (!*p) break;
+    while (*p && ws(*p)) ++p;
+  }
+  is_list = toks.size() > 1;
+  for (auto& t : toks) {
+    if (t.empty()) {
+      err = "empty pattern (leading/trailing whitespace in the pattern list)";
+      return NT_E_PATTERN;
+    }
+    if (std::find(uniq.begin(), uniq.end(), t) == uniq.end()) uniq.push_back(t);
+  }
+  return NT_OK;
+}
+
+int build_pat(const std::string& s, int max_m, NtPat& P, std::string& err) {
+  if ((int)s.size() > max_m) {
+    err = "pattern '" + s + "' is longer than " + std::to_string(max_m) + " letters";
+    return max_m == NT_MAX_M ? NT_E_PATTERN : NT_E_LIMIT;
+  }
+  std::memset(&P, 0, sizeof P);
+  P.m = (int32_t)s.size();
+  P.fixed = 1;
+  for (char ch : s)
+    if (std::strchr("WSMKRYBDHVN", ch)) P.fixed = 0;  // uppercase-only regex, NanoTel.R:334
+  for (int j = 0; j < P.m; ++j) {
+    const uint8_t c = letter_code((unsigned char)s[j]);
+    if (!c) {
+      err = "pattern '" + s + "' has a letter outside DNA_ALPHABET";
+      return NT_E_PATTERN;
+    }
+    P.code[j] = c;
+    uint8_t ts = 0, te = 0;
+    for (int b = 0; b < 4; ++b) {
+      const uint8_t bc = (uint8_t)(1u << b);
+      if (P.fixed ? (c == bc) : ((c & bc) != 0)) ts |= (uint8_t)(1u << b);
+      if (c == bc) te |= (uint8_t)(1u << b);
+    }
+    P.tt_scan[j] = ts;
+    P.tt_eq[j] = te;
+  }
+  return NT_OK;
+}
+
+}  // namespace
+
+struct nt_ctx {
+  int device = 0;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  std::string err;
+  bool compiled = false;
+  bool lds_limit_set = false;
+  NtProgram prog{};
+  nt_params params{};
+  NtProgram* prog_dev = nullptr;
+  int cu_count = 256;
+  DevBuf planes, blk_off, len, win_off, exc_off, exc_pos, exc_code;
+  DevBuf wc, start, end, dens, flags, hits, scratch;
+};
+
+static int fail(nt_ctx* ctx, int code, const std::string& msg) {
+  if (ctx) ctx->err = msg;
+  return code;
+}
+
+static int hip_fail(nt_ctx* ctx, hipError_t e, const char* what) {
+  return fail(ctx, NT_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+extern "C" {
+
+const char* nt_version(void) { return "nanotel-mi355x 0.1.0 (NanoTel v1.1.9-beta hot path)"; }
+
+int nt_create(int device, nt_ctx** out) {
+  if (!out) return NT_E_ARG;
+  *out = nullptr;
+  nt_ctx* ctx = new (std::nothrow) nt_ctx();
+  if (!ctx) return NT_E_NOMEM;
+  ctx->device = device;
+  hipError_t e = hipSetDevice(device);
+  if (e != hipSuccess) {
+    delete ctx;
+    return NT_E_HIP;
+  }
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+    ctx->cu_count = prop.multiProcessorCount;
+  e = hipStreamCreateWithFlags(&ctx->own_stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    delete ctx;
+    return NT_E_HIP;
+  }
+  ctx->stream = ctx->own_stream;
+  e = hipMalloc(&ctx->prog_dev, sizeof(NtProgram));
+  if (e != hipSuccess) {
+    (void)hipStreamDestroy(ctx->own_stream);
+    delete ctx;
+    return NT_E_HIP;
+  }
+  *out = ctx;
+  return NT_OK;
+}
+
+void nt_destroy(nt_ctx* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->prog_dev) (void)hipFree(ctx->prog_dev);
+  if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
+  delete ctx;
+}
+
+const char* nt_last_error(const nt_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int nt_set_stream(nt_ctx* ctx, void* hip_stream) {
+  if (!ctx) return NT_E_ARG;
+  ctx->stream = hip_stream ? (hipStream_t)hip_stream : ctx->own_stream;
+  return NT_OK;
+}
+
+int nt_synchronize(nt_ctx* ctx) {
+  if (!ctx) return NT_E_ARG;
+  hipError_t e = hipStreamSynchronize(ctx->stream);
+  return e == hipSuccess ? NT_OK : hip_fail(ctx, e, "hipStreamSynchronize");
+}
+
+int64_t nt_window_count(int64_t n, int32_t subseq_length) { return window_count(n, subseq_length); }
+
+int nt_compile(nt_ctx* ctx, const nt_params* prm, nt_program_info* info) {
+  if (!ctx || !prm) return NT_E_ARG;
+  if (!prm->patterns) return fail(ctx, NT_E_ARG, "Missing required parameter:  --patterns");
+  if (prm->subseq_length <= 0) return fail(ctx, NT_E_ARG, "--subseq_length must be >= 1");
+  if (prm->subseq_length > 43690)
+    return fail(ctx, NT_E_LIMIT, "--subseq_length > 43690 overflows the uint16 window counts");
+  NtProgram P;
+  std::memset(&P, 0, sizeof P);
+  std::vector<std::string> pats, tvrs;
+  bool pat_list = false, tvr_list = false;
+  std::string err;
+  int rc = parse_tokens(prm->patterns, pats, pat_list, err);
+  if (rc) return fail(ctx, rc, err);
+  if (pats.size() > NT_MAX_PAT) return fail(ctx, NT_E_LIMIT, "more than 8 unique patterns");
+  for (size_t i = 0; i < pats.size(); ++i) {
+    rc = build_pat(pats[i], NT_MAX_M, P.pat[i], err);
+    if (rc) return fail(ctx, rc, err);
+  }
+  if (prm->tvr_patterns) {
+    rc = parse_tokens(prm->tvr_patterns, tvrs, tvr_list, err);
+    if (rc) return fail(ctx, rc, err);
+    if (tvrs.size() > NT_MAX_PAT) return fail(ctx, NT_E_LIMIT, "more than 8 unique TVR patterns");
+    for (size_t i = 0; i < tvrs.size(); ++i) {
+      rc = build_pat(tvrs[i], NT_MAX_TVR_M, P.tvr[i], err);
+      if (rc) return fail(ctx, rc, err);
+    }
+  }
+  P.n_pat = (int32_t)pats.size();
+  P.n_tvr = (int32_t)tvrs.size();
+  P.n_pass = prm->tvr_patterns ? 3 : 2;
+  P.raw_p1 = (!pat_list && P.pat[0].fixed) ? 1 : 0;  // NanoTel.R:347-355
+  P.L = prm->subseq_length;
+  P.right_edge = prm->check_right_edge ? 1 : 0;
+  P.legacy_no_ext = prm->legacy_no_ext ? 1 : 0;
+  P.n_hits = 2 * P.n_pat + P.n_tvr;
+  P.min_density = prm->min_density;
+  (void)hipSetDevice(ctx->device);
+  hipError_t e = hipMemcpy(ctx->prog_dev, &P, sizeof P, hipMemcpyHostToDevice);
+  if (e != hipSuccess) return hip_fail(ctx, e, "hipMemcpy(program)");
+  ctx->prog = P;
+  ctx->params = *prm;
+  ctx->compiled = true;
+  if (info) {
+    info->n_pass = P.n_pass;
+    info->n_pat = P.n_pat;
+    info->n_tvr = P.n_tvr;
+    info->n_hits = P.n_hits;
+    info->raw_p1 = P.raw_p1;
+  }
+  return NT_OK;
+}
+
+int nt_pack_count(const char* const* seqs, const uint64_t* lens, uint64_t n_reads,
+                  int32_t subseq_length, uint64_t* total_blocks, uint64_t* total_windows,
+                  uint64_t* total_exc, uint64_t* max_len, uint64_t* bad_read) {
+  if ((!seqs || !lens) && n_reads) return NT_E_ARG;
+  std::vector<uint64_t> exc(n_reads, 0);
+  std::vector<int> bad(n_reads, 0);
+  parallel_for(n_reads, [&](uint64_t r) {
+    const unsigned char* s = (const unsigned char*)seqs[r];
+    uint64_t e = 0;
+    int b = lens[r] == 0 ? 2 : 0;
+    for (uint64_t i = 0; i < lens[r] && !b; ++i) {
+      if (base2(s[i]) >= 0) continue;
+      if (letter_code(s[i])) ++e; else b = 1;
+    }
+    exc[r] = e;
+    bad[r] = b;
+  });
+  uint64_t tb = 0, tw = 0, te = 0, ml = 0;
+  for (uint64_t r = 0; r < n_reads; ++r) {
+    if (bad[r]) {
+      if (bad_read) *bad_read = r;
+      return bad[r] == 2 ? NT_E_EMPTY_READ : NT_E_LETTER;
+    }
+    tb += (lens[r] + 31) / 32;
+    tw += (uint64_t)window_count((int64_t)lens[r], subseq_length);
+    te += exc[r];
+    ml = std::max(ml, lens[r]);
+  }
+  if (total_blocks) *total_blocks = tb;
+  if (total_windows) *total_windows = tw;
+  if (total_exc) *total_exc = te;
+  if (max_len) *max_len = ml;
+  return NT_OK;
+}
+
+int nt_pack_reads(const char* const* seqs, const uint64_t* lens, uint64_t n_reads, int32_t rc,
+                  int32_t subseq_length, uint32_t* planes, uint64_t* blk_off, uint32_t* len,
+                  uint64_t* win_off, uint32_t* exc_off, uint32_t* exc_pos, uint8_t* exc_code) {
+  if (n_reads && (!seqs || !lens || !planes || !blk_off || !len || !win_off)) return NT_E_ARG;
+  // prefix sums (serial, cheap), then the per-read fill in parallel
+  std::vector<uint64_t> eoff(n_reads + 1, 0);
+  uint64_t b = 0, w = 0;
+  for (uint64_t r = 0; r < n_reads; ++r) {
+    if (lens[r] > 0xFFFFFFFFull) return NT_E_LIMIT;
+    blk_off[r] = b;
+    win_off[r] = w;
+    len[r] = (uint32_t)lens[r];
+    b += (lens[r] + 31) / 32;
+    w += (uint64_t)window_count((int64_t)lens[r], subseq_length);
+  }
+  if (exc_off) {
+    std::vector<uint64_t> cnt(n_reads, 0);
+    parallel_for(n_reads, [&](uint64_t r) {
+      const unsigned char* s = (const unsigned char*)seqs[r];
+      uint64_t e = 0;
+      for (uint64_t i = 0; i < lens[r]; ++i) e += base2(s[i]) < 0;
+      cnt[r] = e;
+    });
+    for (uint64_t r = 0; r < n_reads; ++r) eoff[r + 1] = eoff[r] + cnt[r];
+    for (uint64_t r = 0; r <= n_reads; ++r) {
+      if (eoff[r] > 0xFFFFFFFFull) return NT_E_LIMIT;
+      exc_off[r] = (uint32_t)eoff[r];
+    }
+  }
+  std::atomic<int> bad{0};
+  parallel_for(n_reads, [&](uint64_t r) {
+    const unsigned char* s = (const unsigned char*)seqs[r];
+    const uint64_t n = lens[r];
+    uint32_t* out = planes + 2 * blk_off[r];
+    uint64_t e = exc_off ? eoff[r] : 0;
+    for (uint64_t blk = 0; blk * 32 < n; ++blk) {
+      uint32_t lo = 0, hi = 0;
+      for (uint32_t i = 0; i < 32 && blk * 32 + i < n; ++i) {
+        const uint64_t pos = blk * 32 + i;
+        // reverseComplement: position pos of the RC read is the complement of n-1-pos
+        const unsigned char ch = rc ? s[n - 1 - pos] : s[pos];
+        int c = base2(ch);
+        if (c < 0) {
+          uint8_t code = letter_code(ch);
+          if (!code || !exc_off) { bad.store(1); c = 0; }
+          else {
+            if (rc) code = complement_code(code);
+            exc_pos[e] = (uint32_t)pos;
+            exc_code[e] = code;
+            ++e;
+            c = 0;  // planes hold A at exception positions
+          }
+        } else if (rc) {
+          c = 3 - c;
+        }
+        lo |= (uint32_t)(c & 1) << i;
+        hi |= (uint32_t)((c >> 1) & 1) << i;
+      }
+      out[2 * blk] = lo;
+      out[2 * blk + 1] = hi;
+    }
+  });
+  return bad.load() ? NT_E_LETTER : NT_OK;
+}
+
+int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t max_len) {
+  if (!ctx || !batch || !out) return NT_E_ARG;
+  if (!ctx->compiled) return fail(ctx, NT_E_STATE, "nt_compile() not called");
+  if (batch->n_reads == 0) return NT_OK;
+  if (!out->start || !out->end || !out->density || !out->flags)
+    return fail(ctx, NT_E_ARG, "start/end/density/flags outputs are required");
+  if (max_len > 0x7FFFFFFFull) return fail(ctx, NT_E_LIMIT, "read longer than 2^31-1");
+  (void)hipSetDevice(ctx->device);
+  const int np = ctx->prog.n_pass, L = ctx->prog.L;
+  NtBatch B{batch->planes, batch->blk_off, batch->len, batch->win_off,
+            batch->exc_off, batch->exc_pos, batch->exc_code, batch->n_reads};
+  NtOut O{out->win_counts, out->start, out->end, out->density, out->flags, out->hits};
+  if (!ctx->lds_limit_set) {
+    hipError_t e = nt_dev_set_lds_limit(kLdsCapBytes);
+    if (e != hipSuccess) return hip_fail(ctx, e, "hipFuncSetAttribute");
+    ctx->lds_limit_set = true;
+  }
+  // longest read served from LDS
+  auto lds_bytes = [&](uint64_t n) { return (uint64_t)nt_dev_lds_words((int64_t)n, L, np) * 4u; };
+  uint64_t len_cap = max_len;
+  if (lds_bytes(max_len) > kLdsCapBytes) {
+    uint64_t lo = 0, hi = max_len;  // largest n with lds_bytes(n) <= cap
+    while (lo < hi) {
+      const uint64_t mid = (lo + hi + 1) / 2;
+      if (lds_bytes(mid) <= kLdsCapBytes) lo = mid; else hi = mid - 1;
+    }
+    len_cap = lo;
+  }
+  const uint32_t lw = nt_dev_lds_words((int64_t)len_cap, L, np);
+  const uint64_t per_block = (uint64_t)lw * 4u + kLdsStaticBytes;
+  uint64_t bpc = (160u * 1024u) / per_block;
+  bpc = std::max<uint64_t>(1, std::min<uint64_t>(bpc, 8));
+  const uint64_t grid = std::min<uint64_t>(batch->n_reads, (uint64_t)ctx->cu_count * bpc);
+  hipError_t e = nt_dev_launch_scan_call(ctx->prog_dev, &B, &O, 0u, (uint32_t)len_cap, 0, nullptr, 0,
+                                         lw, (int)grid, ctx->stream);
+  if (e != hipSuccess) return hip_fail(ctx, e, "launch nt_scan_call_kernel<lds>");
+  if (len_cap < max_len) {
+    const uint64_t words = nt_dev_lds_words((int64_t)max_len, L, np);
+    const uint64_t g2 = std::min<uint64_t>(batch->n_reads, (uint64_t)ctx->cu_count * 2);
+    e = ctx->scratch.ensure(g2 * words * 4u);
+    if (e != hipSuccess) return hip_fail(ctx, e, "hipMalloc(scratch)");
+    e = nt_dev_launch_scan_call(ctx->prog_dev, &B, &O, (uint32_t)len_cap, 0xFFFFFFFFu, 1,
+                                (uint32_t*)ctx->scratch.p, words, 0, (int)g2, ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e, "launch nt_scan_call_kernel<global>");
+  }
+  return NT_OK;
+}
+
+int nt_analyze_host(nt_ctx* ctx, const char* const* seqs, const uint64_t* lens, uint64_t n_reads,
+                    int32_t* start, int32_t* end, double* density, uint8_t* flags,
+                    uint16_t* win_counts, uint32_t* hits) {
+  if (!ctx) return NT_E_ARG;
+  if (!ctx->compiled) return fail(ctx, NT_E_STATE, "nt_compile() not called");
+  if (n_reads == 0) return NT_OK;
+  const int L = ctx->prog.L, np = ctx->prog.n_pass;
+  uint64_t tb = 0, tw = 0, te = 0, ml = 0, badr = 0;
+  int rc = nt_pack_count(seqs, lens, n_reads, L, &tb, &tw, &te, &ml, &badr);
+  if (rc == NT_E_EMPTY_READ)
+    return fail(ctx, rc, "read " + std::to_string(badr) + " is empty (seq(1, 0, by=L) errors)");
+  if (rc == NT_E_LETTER)
+    return fail(ctx, rc, "read " + std::to_string(badr) + " has a letter outside DNA_ALPHABET");
+  if (rc) return fail(ctx, rc, "nt_pack_count failed");
+  std::vector<uint32_t> h_planes(2 * tb + 2);
+  std::vector<uint64_t> h_blk(n_reads), h_win(n_reads);
+  std::vector<uint32_t> h_len(n_reads), h_eoff(te ? n_reads + 1 : 0), h_epos(te);
+  std::vector<uint8_t> h_ecode(te);
+  rc = nt_pack_reads(seqs, lens, n_reads, ctx->params.rc, L, h_planes.data(), h_blk.data(),
+                     h_len.data(), h_win.data(), te ? h_eoff.data() : nullptr,
+                     te ? h_epos.data() : nullptr, te ? h_ecode.data() : nullptr);
+  if (rc) return fail(ctx, rc, "nt_pack_reads failed");
+  (void)hipSetDevice(ctx->device);
+  hipError_t e;
+#define NT_UP(buf, vec)                                                                      \
+  e = ctx->buf.ensure(vec.size() * sizeof(vec[0]));                                          \
+  if (e != hipSuccess) return hip_fail(ctx, e, "hipMalloc(" #buf ")");                       \
+  if (!vec.empty()) {                                                                        \
+    e = hipMemcpyAsync(ctx->buf.p, vec.data(), vec.size() * sizeof(vec[0]),                  \
+                       hipMemcpyHostToDevice, ctx->stream);                                  \
+    if (e != hipSuccess) return hip_fail(ctx, e, "hipMemcpyAsync(" #buf ")");                \
+  }
+  NT_UP(planes, h_planes);
+  NT_UP(blk_off, h_blk);
+  NT_UP(len, h_len);
+  NT_UP(win_off, h_win);
+  if (te) {
+    NT_UP(exc_off, h_eoff);
+    NT_UP(exc_pos, h_epos);
+    NT_UP(exc_code, h_ecode);
+  }
+#undef NT_UP
+  const uint64_t nwc = tw * np;
+  if ((e = ctx->wc.ensure(std::max<uint64_t>(1, nwc) * 2)) != hipSuccess) return hip_fail(ctx, e, "hipMalloc(wc)");
+  if ((e = ctx->start.ensure(n_reads * 3 * 4)) != hipSuccess) return hip_fail(ctx, e, "hipMalloc(start)");
+  if ((e = ctx->end.ensure(n_reads * 3 * 4)) != hipSuccess) return hip_fail(ctx, e, "hipMalloc(end)");
+  if ((e = ctx->dens.ensure(n_reads * 3 * 8)) != hipSuccess) return hip_fail(ctx, e, "hipMalloc(dens)");
+  if ((e = ctx->flags.ensure(n_reads)) != hipSuccess) return hip_fail(ctx, e, "hipMalloc(flags)");
+  const uint64_t nh = (uint64_t)ctx->prog.n_hits * n_reads;
+  if ((e = ctx->hits.ensure(std::max<uint64_t>(1, nh) * 4)) != hipSuccess) return hip_fail(ctx, e, "hipMalloc(hits)");
+  nt_batch B{(const uint32_t*)ctx->planes.p, (const uint64_t*)ctx->blk_off.p,
+             (const uint32_t*)ctx->len.p, (const uint64_t*)ctx->win_off.p,
+             te ? (const uint32_t*)ctx->exc_off.p : nullptr,
+             te ? (const uint32_t*)ctx->exc_pos.p : nullptr,
+             te ? (const uint8_t*)ctx->exc_code.p : nullptr, n_reads};
+  nt_out O{win_counts ? (uint16_t*)ctx->wc.p : nullptr, (int32_t*)ctx->start.p, (int32_t*)ctx->end.p,
+           (double*)ctx->dens.p, (uint8_t*)ctx->flags.p, hits ? (uint32_t*)ctx->hits.p : nullptr};
+  rc = nt_scan_call(ctx, &B, &O, ml);
+  if (rc) return rc;
+  std::vector<uint8_t> h_flags(n_reads);
+#define NT_DOWN(dst, buf, bytes)                                                              \
+  e = hipMemcpyAsync(dst, ctx->buf.p, bytes, hipMemcpyDeviceToHost, ctx->stream);            \
+  if (e != hipSuccess) return hip_fail(ctx, e, "hipMemcpyAsync(" #buf ")");
+  NT_DOWN(start, start, n_reads * 3 * 4);
+  NT_DOWN(end, end, n_reads * 3 * 4);
+  NT_DOWN(density, dens, n_reads * 3 * 8);
+  NT_DOWN(h_flags.data(), flags, n_reads);
+  if (win_counts && nwc) { NT_DOWN(win_counts, wc, nwc * 2); }
+  if (hits && nh) { NT_DOWN(hits, hits, nh * 4); }
+#undef NT_DOWN
+  e = hipStreamSynchronize(ctx->stream);
+  if (e != hipSuccess) return hip_fail(ctx, e, "hipStreamSynchronize");
+  if (flags) std::memcpy(flags, h_flags.data(), n_reads);
+  for (uint64_t r = 0; r < n_reads; ++r) {
+    const uint8_t f = h_flags[r];
+    if (!(f & NT_FLAG_DONE)) return fail(ctx, NT_E_HIP, "read " + std::to_string(r) + " not processed");
+    if (f & NT_FLAG_ERR_RIGHT)
+      return fail(ctx, NT_E_RIGHT_EMPTY,
+                  "read " + std::to_string(r) + ": find_right_telo on a read without windows");
+    if (f & NT_FLAG_ERR_WIDTH)
+      return fail(ctx, NT_E_NEG_WIDTH, "read " + std::to_string(r) + ": negative IRanges width");
+  }
+  return NT_OK;
+}
+
+int64_t nt_assign_serials(const uint8_t* is_telo, uint64_t n, double* serial_start_io,
+                          double* max_serial_io, double* serial_out, int64_t* order_out) {
+  if (!serial_start_io || !max_serial_io || (n && (!is_telo || !serial_out || !order_out)))
+    return NT_E_ARG;
+  const uint64_t groups = 8;  // groups_length (NanoTel.R:2234)
+  const double ss = *serial_start_io;
+  double mx = *max_serial_io;
+  int64_t rows = 0;
+  for (uint64_t j = 0; j < n; ++j) serial_out[j] = std::nan("");
+  auto run = [&](uint64_t first, uint64_t stride, double serial) {
+    // search_patterns: current_serial advances only on telomeric reads (NanoTel.R:2050-2070)
+    for (uint64_t j = first; j < n; j += stride) {
+      if (!is_telo[j]) continue;
+      serial_out[j] = serial;
+      order_out[rows++] = (int64_t)j;
+      if (serial > mx) mx = serial;
+      serial = serial + 1.0;
+    }
+  };
+  if (n < groups) {
+    run(0, 1, ss);  // plan(sequential) (NanoTel.R:2236-2239)
+  } else {
+    // split(1:n, f = 1:8): group g = reads g, g+8, ...; serial_start of group g is
+    // serial_start + number of reads in groups < g (NanoTel.R:2245-2252)
+    uint64_t before = 0;
+    for (uint64_t g = 0; g < groups; ++g) {
+      run(g, groups, (double)before + ss);
+      before += (n - g + groups - 1) / groups;
+    }
+  }
+  *max_serial_io = mx;
+  *serial_start_io = mx + 1.0;  // max(df_summary$Serial) + 1 (NanoTel.R:2258)
+  return rows;
+}
+
+static NtSynth to_synth(const nt_synth_params* sp) {
+  NtSynth S;
+  S.seed = sp->seed;
+  S.first_read = sp->first_read;
+  S.read_len = sp->read_len;
+  auto u24 = [](double p) {
+    if (!(p > 0)) return 0u;
+    if (p >= 1) return 1u << 24;
+    return (uint32_t)std::llround(p * 16777216.0);
+  };
+  S.p_tract_u24 = u24(sp->p_tract);
+  S.sub_u24 = u24(sp->sub_rate);
+  S.variant_u24 = u24(sp->variant_rate);
+  S.tract_min = sp->tract_min;
+  S.tract_max = std::max(sp->tract_max, sp->tract_min);
+  S.rc_layout = sp->rc_layout;
+  return S;
+}
+
+int nt_synth_device(nt_ctx* ctx, const nt_synth_params* sp, uint64_t n_reads, uint32_t* planes_dev) {
+  if (!ctx || !sp || (!planes_dev && n_reads)) return NT_E_ARG;
+  if (sp->read_len == 0) return fail(ctx, NT_E_ARG, "read_len must be > 0");
+  (void)hipSetDevice(ctx->device);
+  const NtSynth S = to_synth(sp);
+  hipError_t e = nt_dev_launch_synth(&S, planes_dev, n_reads, ctx->stream);
+  return e == hipSuccess ? NT_OK : hip_fail(ctx, e, "launch nt_synth_kernel");
+}
+
+int nt_uniform_layout_device(nt_ctx* ctx, uint64_t n_reads, uint64_t read_len, int32_t subseq_length,
+                             uint64_t* blk_off_dev, uint32_t* len_dev, uint64_t* win_off_dev) {
+  if (!ctx || read_len == 0 || read_len > 0xFFFFFFFFull) return NT_E_ARG;
+  (void)hipSetDevice(ctx->device);
+  const uint64_t nblk = (read_len + 31) / 32;
+  const uint64_t nw = (uint64_t)window_count((int64_t)read_len, subseq_length);
+  hipError_t e = nt_dev_launch_uniform_layout(n_reads, nblk, read_len, nw, blk_off_dev, len_dev,
+                                              win_off_dev, ctx->stream);
+  return e == hipSuccess ? NT_OK : hip_fail(ctx, e, "launch nt_layout_kernel");
+}
+
+int nt_synth_ascii(const nt_synth_params* sp, uint64_t read_index, char* out) {
+  if (!sp || !out) return NT_E_ARG;
+  const NtSynth S = to_synth(sp);
+  const uint64_t r = S.first_read + read_index;
+  const NtSynthRead R = nt_synth_read(S, r);
+  static const char kBase[4] = {'A', 'C', 'G', 'T'};
+  for (uint64_t p = 0; p < S.read_len; ++p) out[p] = kBase[nt_synth_base(S, R, r, p)];
+  return NT_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,176 @@
+"""Host-side mirror of NanoTel's per-chunk interface over the HIP C-ABI.
+
+`NanoTel` owns one device context and one compiled pattern program
+(extract_patterns, NanoTel.R:2322-2334).  `NanoTel.analyze()` is the
+per-chunk replacement of search_patterns' loop over analyze_read
+(NanoTel.R:2001-2078, 1774-1976): one kernel launch for the whole chunk.
+"""
+import ctypes
+
+import numpy as np
+
+from ._lib import (NanoTelError, NtBatch, NtOut, NtParams, NtProgramInfo, NtSynthParams, lib,
+                   ROW_DONE, ROW_TELOMERIC)
+
+
+def _check(rc, ctx=None):
+    if rc < 0:
+        msg = lib().nt_last_error(ctx).decode() if ctx else ""
+        raise NanoTelError(rc, msg)
+    return rc
+
+
+def window_count(n, subseq_length=100):
+    """split_telo window count (NanoTel.R:199-227)."""
+    return lib().nt_window_count(int(n), int(subseq_length))
+
+
+class NanoTel:
+    """One GPU context + compiled --patterns/--tvr_patterns/flags."""
+
+    def __init__(self, patterns, tvr_patterns=None, subseq_length=100, min_density=0.6,
+                 check_right_edge=False, rc=False, legacy_no_ext=False, device=0):
+        L = lib()
+        h = ctypes.c_void_p()
+        rc_ = L.nt_create(int(device), ctypes.byref(h))
+        if rc_ != 0 or not h.value:
+            raise NanoTelError(rc_, "nt_create failed (no GPU visible?)")
+        self._h = h
+        self._pat_b = patterns.encode() if isinstance(patterns, str) else patterns
+        self._tvr_b = None if tvr_patterns is None else (
+            tvr_patterns.encode() if isinstance(tvr_patterns, str) else tvr_patterns)
+        self.params = NtParams(self._pat_b, self._tvr_b, int(subseq_length), float(min_density),
+                               int(bool(check_right_edge)), int(bool(rc)), int(bool(legacy_no_ext)))
+        info = NtProgramInfo()
+        _check(L.nt_compile(self._h, ctypes.byref(self.params), ctypes.byref(info)), self._h)
+        self.n_pass = info.n_pass
+        self.n_pat = info.n_pat
+        self.n_tvr = info.n_tvr
+        self.n_hits = info.n_hits
+        self.raw_p1 = bool(info.raw_p1)
+        self.subseq_length = int(subseq_length)
+
+    # ------------------------------------------------------------------
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            lib().nt_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    @property
+    def handle(self):
+        return self._h
+
+    def set_stream(self, stream_handle):
+        _check(lib().nt_set_stream(self._h, ctypes.c_void_p(stream_handle)), self._h)
+
+    def synchronize(self):
+        _check(lib().nt_synchronize(self._h), self._h)
+
+    # ------------------------------------------------------------------
+    def analyze(self, seqs, want_windows=False, want_hits=False):
+        """Scan + call every read of a chunk (host buffers in, host arrays out).
+
+        Returns a dict of numpy arrays: start/end (n,3) int32 (1-based, -1 =
+        no telomere), density (n,3) float64, flags (n,) uint8, width (n,3),
+        telomeric (n,) bool [, win_counts (flat uint16), win_off (n,) ]
+        [, hits (n, n_hits) uint32].
+        """
+        bseqs = [s.encode() if isinstance(s, str) else bytes(s) for s in seqs]
+        n = len(bseqs)
+        out = {
+            "start": np.full((n, 3), -1, np.int32),
+            "end": np.full((n, 3), -1, np.int32),
+            "density": np.zeros((n, 3), np.float64),
+            "flags": np.zeros(n, np.uint8),
+        }
+        if n == 0:
+            out["width"] = np.zeros((0, 3), np.int64)
+            out["telomeric"] = np.zeros(0, bool)
+            return out
+        ptrs = (ctypes.c_char_p * n)(*bseqs)
+        lens = np.array([len(b) for b in bseqs], np.uint64)
+        wc = None
+        if want_windows:
+            nw = np.array([window_count(int(x), self.subseq_length) for x in lens], np.int64)
+            win_off = np.zeros(n, np.int64)
+            win_off[1:] = np.cumsum(nw)[:-1]
+            wc = np.zeros(max(1, int(nw.sum()) * self.n_pass), np.uint16)
+            out["win_off"] = win_off
+            out["n_windows"] = nw
+        hits = np.zeros((n, max(1, self.n_hits)), np.uint32) if want_hits else None
+        rc = lib().nt_analyze_host(
+            self._h, ctypes.cast(ptrs, ctypes.c_void_p), lens.ctypes.data, n,
+            out["start"].ctypes.data, out["end"].ctypes.data, out["density"].ctypes.data,
+            out["flags"].ctypes.data, None if wc is None else wc.ctypes.data,
+            None if hits is None else hits.ctypes.data)
+        _check(rc, self._h)
+        out["width"] = out["end"].astype(np.int64) - out["start"].astype(np.int64) + 1
+        out["telomeric"] = (out["flags"] & ROW_TELOMERIC) != 0
+        assert np.all(out["flags"] & ROW_DONE), "kernel did not process every read"
+        if wc is not None:
+            out["win_counts"] = wc
+        if hits is not None:
+            out["hits"] = hits[:, :self.n_hits]
+        return out
+
+    def window_counts(self, res, read, p):
+        """Window counts of pass p for read `read` from an analyze(want_windows) result."""
+        nw = int(res["n_windows"][read])
+        off = int(res["win_off"][read]) * self.n_pass + p * nw
+        return res["win_counts"][off:off + nw]
+
+    # ------------------------------------------------------------------
+    def scan_call_device(self, planes, blk_off, lengths, win_off, n_reads, max_len, start, end,
+                         density, flags, win_counts=0, hits=0, exc_off=0, exc_pos=0, exc_code=0):
+        """Device-resident hot path: all arguments are device pointers (ints).
+        Asynchronous on the context stream (see set_stream)."""
+        B = NtBatch(planes, blk_off, lengths, win_off, exc_off or None, exc_pos or None,
+                    exc_code or None, int(n_reads))
+        O = NtOut(win_counts or None, start, end, density, flags, hits or None)
+        _check(lib().nt_scan_call(self._h, ctypes.byref(B), ctypes.byref(O), int(max_len)), self._h)
+
+    def synth_device(self, sp, n_reads, planes_ptr):
+        _check(lib().nt_synth_device(self._h, ctypes.byref(sp), int(n_reads), planes_ptr), self._h)
+
+    def uniform_layout_device(self, n_reads, read_len, blk_off_ptr, len_ptr, win_off_ptr):
+        _check(lib().nt_uniform_layout_device(self._h, int(n_reads), int(read_len), self.subseq_length,
+                                              blk_off_ptr, len_ptr, win_off_ptr), self._h)
+
+
+def synth_params(seed=20260501, first_read=0, read_len=50000, p_tract=0.5, sub_rate=0.02,
+                 variant_rate=0.0, tract_min=1000, tract_max=15000, rc_layout=False):
+    return NtSynthParams(int(seed), int(first_read), int(read_len), float(p_tract), float(sub_rate),
+                         float(variant_rate), int(tract_min), int(tract_max), int(bool(rc_layout)))
+
+
+def synth_read_ascii(sp, index):
+    """Host twin of the device generator (nt_rng.h): read `first_read + index`."""
+    buf = ctypes.create_string_buffer(int(sp.read_len))
+    _check(lib().nt_synth_ascii(ctypes.byref(sp), int(index), buf))
+    return buf.raw[:int(sp.read_len)].decode()
+
+
+def assign_serials(is_telo, serial_start=1.0, max_serial=float("-inf")):
+    """A15 for one chunk: returns (serials, row_order, next_serial_start, max_serial)."""
+    t = np.ascontiguousarray(np.asarray(is_telo, dtype=np.uint8))
+    n = t.size
+    ser = np.zeros(max(1, n), np.float64)
+    order = np.zeros(max(1, n), np.int64)
+    ss = ctypes.c_double(serial_start)
+    mx = ctypes.c_double(max_serial)
+    rows = lib().nt_assign_serials(t.ctypes.data if n else None, n, ctypes.byref(ss), ctypes.byref(mx),
+                                   ser.ctypes.data, order.ctypes.data)
+    _check(rows)
+    return ser[:n], order[:rows], ss.value, mx.value

@@ -1,0 +1,175 @@
+"""Parity of the HIP path (through the C-ABI) against the CPU oracle.
+
+Bit-exact on every output: called start/end per pass, fp64 densities,
+telomeric flag, per-window covered counts, per-pattern hit counts.
+"""
+import os
+import zlib
+
+import numpy as np
+import pytest
+
+import _oracle as O
+from _parity import compare, oracle_rows
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _nt(**kw):
+    from nanotel_amd import NanoTel
+    return NanoTel(**kw)
+
+
+def _example():
+    return O.read_fasta(os.path.join(GOLD, "sample.fasta"))
+
+
+def _telo_read(rng, n, motif="TTAGGG", where="left", tract=(200, 3000), sub=0.03, exc=0.0,
+               exc_letters="NRYKMSWBDHV", lower=0.0):
+    bases = np.array(list("ACGT"))
+    s = list(bases[rng.integers(0, 4, n)])
+    tl = int(rng.integers(tract[0], tract[1] + 1)) if n > 0 else 0
+    tl = min(tl, n)
+    if where == "left":
+        a = 0
+    elif where == "right":
+        a = n - tl
+    else:
+        a = int(rng.integers(0, max(1, n - tl)))
+    for i in range(tl):
+        s[a + i] = motif[i % len(motif)]
+        if rng.random() < sub:
+            s[a + i] = bases[rng.integers(0, 4)]
+    if exc > 0:
+        for i in range(n):
+            if rng.random() < exc:
+                s[i] = exc_letters[rng.integers(0, len(exc_letters))]
+    if lower > 0:
+        for i in range(n):
+            if rng.random() < lower:
+                s[i] = s[i].lower()
+    return "".join(s)
+
+
+def test_example_golden_through_hip():
+    names, seqs = _example()
+    for legacy in (True, False):
+        nt = _nt(patterns="TTAGGG", min_density=0.6, legacy_no_ext=legacy)
+        res = nt.analyze(seqs, want_windows=True, want_hits=True)
+        compare(nt, res, oracle_rows(seqs, "TTAGGG", legacy=legacy))
+        nt.close()
+    # the committed golden itself (legacy) through the HIP path
+    import csv
+    rows = list(csv.DictReader(open(os.path.join(GOLD, "example_summary.csv"))))
+    nt = _nt(patterns="TTAGGG", legacy_no_ext=True)
+    res = nt.analyze(seqs)
+    for i, g in enumerate(rows):
+        assert int(res["start"][i][0]) == int(g["Telomere_start"])
+        assert int(res["end"][i][1]) == int(g["Telomere_end_mismatch"])
+        assert repr(float(res["density"][i][0])) == g["telo_density"]
+        assert repr(float(res["density"][i][1])) == g["telo_density_mismatch"]
+
+
+def test_synthetic_generator_reads():
+    from nanotel_amd import synth_params, synth_read_ascii
+    for read_len, rc_layout, var in ((10000, False, 0.0), (50000, True, 0.05)):
+        sp = synth_params(read_len=read_len, rc_layout=rc_layout, variant_rate=var)
+        seqs = [synth_read_ascii(sp, i) for i in range(24)]
+        nt = _nt(patterns="TTAGGG", rc=rc_layout)
+        res = nt.analyze(seqs, want_windows=True, want_hits=True)
+        compare(nt, res, oracle_rows(seqs, "TTAGGG", rc=rc_layout))
+        assert res["telomeric"].sum() > 0
+
+
+@pytest.mark.parametrize("cfg", [
+    dict(patterns="TTAGGG"),
+    dict(patterns="YYAGGG"),
+    dict(patterns="TTAGGG TCAGGG"),
+    dict(patterns="TTAGGG TTAGGG"),
+    dict(patterns="CCCTAA", check_right_edge=True),
+    dict(patterns="TTAGGG TCAGGG", tvr_patterns="TGAGGG TTGGGG"),
+    dict(patterns="TTAGGG", tvr_patterns="TTGGGG"),
+    dict(patterns="TTAGGG", subseq_length=50, min_density=0.5),
+    dict(patterns="TTAGGG", subseq_length=37, min_density=0.3),
+    dict(patterns="TTAGGG", rc=True),
+    dict(patterns="ttaggg"),
+    dict(patterns="TTAGGN"),
+    dict(patterns="TTRGGG CCCTAA", tvr_patterns="TYAGGG"),
+    dict(patterns="TAGGGTTAGGGTTAGGGT"),
+])
+def test_random_reads(cfg):
+    rng = np.random.default_rng(zlib.crc32(str(sorted(cfg.items())).encode()))
+    seqs = []
+    right = cfg.get("check_right_edge", False)
+    motif = "CCCTAA" if right else "TTAGGG"
+    for i in range(120):
+        n = int(rng.choice([rng.integers(51 if right else 1, 400), rng.integers(400, 5000),
+                            rng.integers(5000, 30000)]))
+        where = ["left", "right", "mid"][i % 3]
+        seqs.append(_telo_read(rng, n, motif=motif, where=where,
+                               exc=0.002 if i % 5 == 0 else 0.0, lower=0.01 if i % 7 == 0 else 0.0))
+    nt = _nt(**cfg)
+    res = nt.analyze(seqs, want_windows=True, want_hits=True)
+    orow = oracle_rows(seqs, cfg["patterns"], tvr=cfg.get("tvr_patterns"), L=cfg.get("subseq_length", 100),
+                       min_density=cfg.get("min_density", 0.6), right_edge=right, rc=cfg.get("rc", False))
+    compare(nt, res, orow)
+
+
+def test_iupac_subject_letters_and_tiny_reads():
+    rng = np.random.default_rng(7)
+    seqs = ["A", "T", "N", "TTAGGG", "TTAGG", "NNNNNNNNNN", "TTAGGGTTAGGGTTAGGGNNNN"]
+    for n in range(1, 140, 3):
+        seqs.append(_telo_read(rng, n, tract=(0, n), exc=0.05))
+    for pats in ("TTAGGG", "YYAGGG", "TTAGGG TCAGGG", "NNNNNN"):
+        nt = _nt(patterns=pats, tvr_patterns="TGAGGG")
+        res = nt.analyze(seqs, want_windows=True, want_hits=True)
+        compare(nt, res, oracle_rows(seqs, pats, tvr="TGAGGG"))
+
+
+def test_long_reads_global_scratch_path():
+    # reads beyond the LDS budget go through the global-scratch kernel
+    rng = np.random.default_rng(11)
+    seqs = [_telo_read(rng, 230000, tract=(5000, 20000)), _telo_read(rng, 1200, where="left"),
+            _telo_read(rng, 181000, where="right", tract=(5000, 9000))]
+    nt = _nt(patterns="TTAGGG", tvr_patterns="TTGGGG")
+    res = nt.analyze(seqs, want_windows=True, want_hits=True)
+    compare(nt, res, oracle_rows(seqs, "TTAGGG", tvr="TTGGGG"))
+
+
+def test_error_behaviour():
+    from nanotel_amd import NanoTelError
+    nt = _nt(patterns="CCCTAA", check_right_edge=True)
+    with pytest.raises(NanoTelError) as e:
+        nt.analyze(["ACGT" * 10])  # n <= 50: find_right_telo on a 0-row table
+    assert e.value.name == "NT_E_RIGHT_EMPTY"
+    nt = _nt(patterns="TTAGGG")
+    with pytest.raises(NanoTelError) as e:
+        nt.analyze(["ACGTX"])
+    assert e.value.name == "NT_E_LETTER"
+    with pytest.raises(NanoTelError) as e:
+        nt.analyze(["ACGT", ""])
+    assert e.value.name == "NT_E_EMPTY_READ"
+    with pytest.raises(NanoTelError) as e:
+        _nt(patterns=" TTAGGG")
+    assert e.value.name == "NT_E_PATTERN"
+
+
+def test_device_synth_matches_host_generator():
+    import torch
+    from nanotel_amd import NanoTel, synth_params, synth_read_ascii
+    sp = synth_params(read_len=5000, first_read=123)
+    nt = NanoTel(patterns="TTAGGG")
+    n = 16
+    nblk = (5000 + 31) // 32
+    planes = torch.zeros(n * nblk * 2, dtype=torch.int32, device="cuda")
+    nt.synth_device(sp, n, planes.data_ptr())
+    nt.synchronize()
+    p = planes.cpu().numpy().view(np.uint32).reshape(n, nblk, 2)
+    for r in range(n):
+        host = synth_read_ascii(sp, r)
+        lo = np.unpackbits(np.ascontiguousarray(p[r, :, 0]).view(np.uint8), bitorder="little")[:5000]
+        hi = np.unpackbits(np.ascontiguousarray(p[r, :, 1]).view(np.uint8), bitorder="little")[:5000]
+        dev = "".join("ACGT"[c] for c in (lo + 2 * hi))
+        assert dev == host
