@@ -42,7 +42,7 @@ def algorithmic_bytes_per_read(read_len, n_pass, n_windows):
     return blocks * 8 + 8 + 4 + 8 + n_windows * n_pass * 2 + 3 * 4 * 2 + 3 * 8 + 1
 
 
-def cpu_baseline(cfg, budget_s=12.0, max_reads=64):
+def cpu_baseline(cfg, budget_s=12.0, max_reads=10 ** 9):
     """CPU oracle (restatement, single core) on the first reads of the same
     synthetic workload (host twin of the device generator)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -97,7 +97,10 @@ def main():
     n = cfg["reads"]
     L = cfg["read_len"]
     nt = NanoTel(patterns=cfg["patterns"], tvr_patterns=cfg["tvr"], rc=False, device=local)
-    stream = torch.cuda.current_stream(dev)
+    # a dedicated (non-null) stream: the library launches on it and the HIP
+    # events that time the kernel are recorded on it
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
     nt.set_stream(stream.cuda_stream)
     npass = nt.n_pass
     nblk = (L + 31) // 32

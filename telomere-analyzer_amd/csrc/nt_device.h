@@ -110,9 +110,11 @@ __device__ __forceinline__ uint32_t code_at(const ReadCtx& rc, int64_t pos) {
 }
 
 // Mismatch count (capped at 2) of pattern P at start s; positions outside
-// [vlo, vhi] count as mismatches.  eq: fixed=TRUE code equality, else IUPAC AND.
+// [vlo, vhi] count as mismatches.  eq (edge steps, always fixed=TRUE) or a
+// fixed pattern: code equality; otherwise IUPAC bit-set AND (fixed=FALSE).
 __device__ __forceinline__ int mism_generic(const ReadCtx& rc, const NtPat& P, bool eq, int64_t s,
                                             int64_t vlo, int64_t vhi) {
+  eq = eq || P.fixed;
   int nm = 0;
   for (int j = 0; j < P.m && nm < 2; ++j) {
     const int64_t pos = s + j;

@@ -101,9 +101,20 @@ _lib = None
 
 
 def lib():
-    """Load libnanotel.so (raises if it was not built: no fallback)."""
+    """Load libnanotel.so (raises if it was not built: no fallback).
+
+    One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64 with
+    the same SONAME (libamdhip64.so.7) as /opt/rocm's.  When torch is
+    importable it is imported first, so that libnanotel binds to torch's
+    already-loaded runtime and device pointers/streams are shared; a second
+    runtime in the process would make torch's own initialisation fail.
+    """
     global _lib
     if _lib is None:
+        try:
+            import torch  # noqa: F401  (load torch's libamdhip64 first)
+        except ImportError:
+            pass
         if not os.path.exists(LIB_PATH):
             raise ImportError(f"{LIB_PATH} not built: run __graft_entry__.build() "
                               "(make -C telomere-analyzer_amd/csrc)")
