@@ -36,6 +36,11 @@ struct NtPat {
   uint8_t code[NT_MAX_TVR_M];  // Biostrings DNA codes (for exception positions)
   uint8_t tt_scan[NT_MAX_TVR_M];
   uint8_t tt_eq[NT_MAX_TVR_M];
+  // the truth tables expanded to bit-select masks (0 or ~0) for bases A,C,G,T:
+  // loaded with scalar loads into SGPRs, so the match of a letter costs three
+  // v_bfi_b32 and no decode
+  uint32_t tm_scan[NT_MAX_TVR_M][4];
+  uint32_t tm_eq[NT_MAX_TVR_M][4];
 };
 
 struct NtProgram {
@@ -47,6 +52,9 @@ struct NtProgram {
   int32_t legacy_no_ext;  // test switch: skip search_left/right_patterns (2023 code)
   int32_t n_hits;         // 2*n_pat + n_tvr hit counters per read
   double min_density;     // --min_density
+  uint64_t div_m;         // floor(p / L) = (p * div_m) >> div_s for p < 2^31 (exact)
+  uint32_t div_s;
+  uint32_t thr_size;      // entries of the per-width telomeric threshold table
   NtPat pat[NT_MAX_PAT];
   NtPat tvr[NT_MAX_PAT];
 };

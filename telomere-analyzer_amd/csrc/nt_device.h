@@ -57,21 +57,21 @@ __device__ __forceinline__ void plane_at(const ReadCtx& rc, int64_t p, uint32_t&
 
 // Bit-sliced approximate matching of one pattern at 32 consecutive starts.
 // Inputs: planes (L,H) and validity (V) of positions [base, base+63] as two
-// words.  tt[j]: truth table of pattern letter j over subject bases A,C,G,T.
-// Invalid positions (outside the subject / window) count as mismatches --
-// Biostrings' out-of-bound rule.  a0 = starts with 0 mismatches, a1 = <= 1.
+// words.  tm[j][c]: all-ones iff pattern letter j matches subject base c
+// (A,C,G,T).  Invalid positions (outside the subject / window) count as
+// mismatches -- Biostrings' out-of-bound rule.  a0 = starts with 0
+// mismatches, a1 = <= 1.  kValid=false: every position is known valid.
+template <bool kValid>
 __device__ __forceinline__ void hits32(uint32_t L0, uint32_t L1, uint32_t H0, uint32_t H1,
-                                       uint32_t V0, uint32_t V1, const uint8_t* __restrict__ tt,
-                                       int m, uint32_t& a0, uint32_t& a1) {
+                                       uint32_t V0, uint32_t V1,
+                                       const uint32_t (*__restrict__ tm)[4], int m, uint32_t& a0,
+                                       uint32_t& a1) {
   uint32_t x0 = 0xFFFFFFFFu, x1 = 0xFFFFFFFFu;
   for (int j = 0; j < m; ++j) {
-    const uint32_t t = tt[j];
     const uint32_t Ls = funnel(L1, L0, (uint32_t)j);
     const uint32_t Hs = funnel(H1, H0, (uint32_t)j);
-    const uint32_t Vs = funnel(V1, V0, (uint32_t)j);
-    const uint32_t T0 = 0u - (t & 1u), T1 = 0u - ((t >> 1) & 1u);
-    const uint32_t T2 = 0u - ((t >> 2) & 1u), T3 = 0u - ((t >> 3) & 1u);
-    const uint32_t q = bfi(Hs, bfi(Ls, T3, T2), bfi(Ls, T1, T0)) & Vs;
+    uint32_t q = bfi(Hs, bfi(Ls, tm[j][3], tm[j][2]), bfi(Ls, tm[j][1], tm[j][0]));
+    if (kValid) q &= funnel(V1, V0, (uint32_t)j);
     x1 = (x1 & q) | x0;
     x0 &= q;
   }
@@ -162,7 +162,7 @@ __device__ __forceinline__ void hits_at(const ReadCtx& rc, const NtPat& P, bool 
   plane_at(rc, base, L0, H0);
   plane_at(rc, base + 32, L1, H1);
   const uint32_t V0 = range_mask(base, vlo, vhi), V1 = range_mask(base + 32, vlo, vhi);
-  hits32(L0, L1, H0, H1, V0, V1, eq ? P.tt_eq : P.tt_scan, P.m, a0, a1);
+  hits32<true>(L0, L1, H0, H1, V0, V1, eq ? P.tm_eq : P.tm_scan, P.m, a0, a1);
   if (P.m <= 1) a1 &= V0;
   if (rc.n_exc) patch_exceptions(rc, base, vlo, vhi, P, eq, a0, a1);
 }

@@ -17,11 +17,13 @@
 #include "nt_rng.h"
 
 extern "C" {
-uint32_t nt_dev_lds_words(int64_t n, int L, int np);
-hipError_t nt_dev_launch_scan_call(const NtProgram* prog_dev, const NtBatch* B, const NtOut* O,
-                                   uint32_t len_lo, uint32_t len_hi, int global_scratch,
-                                   uint32_t* gscratch, uint64_t scratch_words, uint32_t lds_words,
-                                   int grid, hipStream_t stream);
+hipError_t nt_dev_launch_scan(const NtProgram* prog, const NtBatch* B, const NtOut* O,
+                              uint32_t len_lo, uint32_t len_hi, int lds, uint32_t wave_words,
+                              uint32_t* gcnt, uint64_t gcnt_words, int grid, hipStream_t stream);
+hipError_t nt_dev_launch_call(const NtProgram* prog, const uint32_t* thr, const NtBatch* B,
+                              const NtOut* O, uint32_t len_lo, uint32_t len_hi, int lds,
+                              uint32_t tm_words, uint64_t* gtm, int np, int grid,
+                              hipStream_t stream);
 hipError_t nt_dev_set_lds_limit(uint32_t bytes);
 hipError_t nt_dev_launch_synth(const NtSynth* S, uint32_t* planes, uint64_t n_reads,
                                hipStream_t stream);
@@ -32,8 +34,8 @@ hipError_t nt_dev_launch_uniform_layout(uint64_t n_reads, uint64_t nblk, uint64_
 
 namespace {
 
-constexpr uint32_t kLdsCapBytes = 96 * 1024;  // per workgroup; longer reads use global scratch
-constexpr uint32_t kLdsStaticBytes = 512;
+constexpr uint32_t kScanLdsCapBytes = 64 * 1024;  // per 4-wave workgroup; longer reads: global counters
+constexpr uint32_t kCallTmCapWords = 2048;         // per wave (16 KB); longer reads: global bitmask
 
 struct DevBuf {
   void* p = nullptr;
@@ -184,7 +186,7 @@ struct nt_ctx {
   NtProgram* prog_dev = nullptr;
   int cu_count = 256;
   DevBuf planes, blk_off, len, win_off, exc_off, exc_pos, exc_code;
-  DevBuf wc, start, end, dens, flags, hits, scratch;
+  DevBuf wc, start, end, dens, flags, hits, scratch, scratch2, thr;
 };
 
 static int fail(nt_ctx* ctx, int code, const std::string& msg) {
@@ -291,9 +293,39 @@ int nt_compile(nt_ctx* ctx, const nt_params* prm, nt_program_info* info) {
   P.legacy_no_ext = prm->legacy_no_ext ? 1 : 0;
   P.n_hits = 2 * P.n_pat + P.n_tvr;
   P.min_density = prm->min_density;
+  // floor(p / L) by multiply-shift: l = ceil(log2 L), M = floor(2^(32+l) / L) + 1
+  // is exact for every p < 2^32 (error < 2^-l <= 1/L).
+  {
+    uint32_t l = 0;
+    while ((1ull << l) < (uint64_t)P.L) ++l;
+    P.div_s = 32 + l;
+    P.div_m = (uint64_t)((((unsigned __int128)1) << (32 + l)) / (uint64_t)P.L) + 1;
+  }
+  // Telomeric class (NanoTel.R:749-758): -5 iff !(count / width < min_density).
+  // fl(c / w) is monotone in c, so the class is count >= thr[w] with thr[w]
+  // the smallest such count -- found here with the very fp64 division R does.
+  const uint32_t wmax = (uint32_t)P.L + (uint32_t)(P.L + 1) / 2 + 1;
+  std::vector<uint32_t> thr(wmax + 1, 0);
+  for (uint32_t w = 1; w <= wmax; ++w) {
+    uint32_t c = 0;
+    while (c <= w && ((double)c / (double)w < P.min_density)) ++c;
+    thr[w] = c;  // w + 1 = never telomeric
+  }
+  P.thr_size = wmax + 1;
+  for (int i = 0; i < P.n_pat + P.n_tvr; ++i) {
+    NtPat& X = i < P.n_pat ? P.pat[i] : P.tvr[i - P.n_pat];
+    for (int j = 0; j < X.m; ++j)
+      for (int b = 0; b < 4; ++b) {
+        X.tm_scan[j][b] = ((X.tt_scan[j] >> b) & 1u) ? 0xFFFFFFFFu : 0u;
+        X.tm_eq[j][b] = ((X.tt_eq[j] >> b) & 1u) ? 0xFFFFFFFFu : 0u;
+      }
+  }
   (void)hipSetDevice(ctx->device);
   hipError_t e = hipMemcpy(ctx->prog_dev, &P, sizeof P, hipMemcpyHostToDevice);
   if (e != hipSuccess) return hip_fail(ctx, e, "hipMemcpy(program)");
+  if ((e = ctx->thr.ensure(thr.size() * 4)) != hipSuccess) return hip_fail(ctx, e, "hipMalloc(thr)");
+  e = hipMemcpy(ctx->thr.p, thr.data(), thr.size() * 4, hipMemcpyHostToDevice);
+  if (e != hipSuccess) return hip_fail(ctx, e, "hipMemcpy(thr)");
   ctx->prog = P;
   ctx->params = *prm;
   ctx->compiled = true;
@@ -411,46 +443,80 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
   if (!ctx || !batch || !out) return NT_E_ARG;
   if (!ctx->compiled) return fail(ctx, NT_E_STATE, "nt_compile() not called");
   if (batch->n_reads == 0) return NT_OK;
-  if (!out->start || !out->end || !out->density || !out->flags)
-    return fail(ctx, NT_E_ARG, "start/end/density/flags outputs are required");
+  if (!out->win_counts || !out->start || !out->end || !out->density || !out->flags)
+    return fail(ctx, NT_E_ARG, "win_counts/start/end/density/flags outputs are required");
   if (max_len > 0x7FFFFFFFull) return fail(ctx, NT_E_LIMIT, "read longer than 2^31-1");
   (void)hipSetDevice(ctx->device);
-  const int np = ctx->prog.n_pass, L = ctx->prog.L;
+  const int np = ctx->prog.n_pass, L = ctx->prog.L, nh = ctx->prog.n_hits;
   NtBatch B{batch->planes, batch->blk_off, batch->len, batch->win_off,
             batch->exc_off, batch->exc_pos, batch->exc_code, batch->n_reads};
   NtOut O{out->win_counts, out->start, out->end, out->density, out->flags, out->hits};
   if (!ctx->lds_limit_set) {
-    hipError_t e = nt_dev_set_lds_limit(kLdsCapBytes);
+    hipError_t e = nt_dev_set_lds_limit(kScanLdsCapBytes);
     if (e != hipSuccess) return hip_fail(ctx, e, "hipFuncSetAttribute");
     ctx->lds_limit_set = true;
   }
-  // longest read served from LDS
-  auto lds_bytes = [&](uint64_t n) { return (uint64_t)nt_dev_lds_words((int64_t)n, L, np) * 4u; };
+  hipError_t e;
+  // ---- scan: window counters in LDS up to the cap, in global scratch beyond
+  const uint64_t max_nw = (uint64_t)window_count((int64_t)max_len, L);
+  auto scan_words = [&](uint64_t nw) { return (uint64_t)nh * 64 + (uint64_t)np * nw; };
+  uint64_t cap_nw = max_nw;
+  if (scan_words(max_nw) * 4 * 4 > kScanLdsCapBytes)
+    cap_nw = (kScanLdsCapBytes / 16 - (uint64_t)nh * 64) / np;
+  // longest read whose windows fit the LDS counters
   uint64_t len_cap = max_len;
-  if (lds_bytes(max_len) > kLdsCapBytes) {
-    uint64_t lo = 0, hi = max_len;  // largest n with lds_bytes(n) <= cap
+  if (cap_nw < max_nw) {
+    uint64_t lo = 0, hi = max_len;
     while (lo < hi) {
       const uint64_t mid = (lo + hi + 1) / 2;
-      if (lds_bytes(mid) <= kLdsCapBytes) lo = mid; else hi = mid - 1;
+      if ((uint64_t)window_count((int64_t)mid, L) <= cap_nw) lo = mid; else hi = mid - 1;
     }
     len_cap = lo;
   }
-  const uint32_t lw = nt_dev_lds_words((int64_t)len_cap, L, np);
-  const uint64_t per_block = (uint64_t)lw * 4u + kLdsStaticBytes;
-  uint64_t bpc = (160u * 1024u) / per_block;
-  bpc = std::max<uint64_t>(1, std::min<uint64_t>(bpc, 8));
-  const uint64_t grid = std::min<uint64_t>(batch->n_reads, (uint64_t)ctx->cu_count * bpc);
-  hipError_t e = nt_dev_launch_scan_call(ctx->prog_dev, &B, &O, 0u, (uint32_t)len_cap, 0, nullptr, 0,
-                                         lw, (int)grid, ctx->stream);
-  if (e != hipSuccess) return hip_fail(ctx, e, "launch nt_scan_call_kernel<lds>");
+  {
+    const uint64_t ww = scan_words(std::min(cap_nw, max_nw));
+    const uint64_t wg_bytes = ww * 4 * 4;
+    uint64_t bpc = std::min<uint64_t>(8, std::max<uint64_t>(1, (160u * 1024u) / std::max<uint64_t>(wg_bytes, 1)));
+    const uint64_t waves = (batch->n_reads + 0);
+    uint64_t grid = std::min<uint64_t>((waves + 3) / 4, (uint64_t)ctx->cu_count * bpc);
+    e = nt_dev_launch_scan(ctx->prog_dev, &B, &O, 0u, (uint32_t)len_cap, 1, (uint32_t)ww, nullptr, 0,
+                           (int)std::max<uint64_t>(grid, 1), ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e, "launch nt_scan_kernel<lds>");
+  }
   if (len_cap < max_len) {
-    const uint64_t words = nt_dev_lds_words((int64_t)max_len, L, np);
-    const uint64_t g2 = std::min<uint64_t>(batch->n_reads, (uint64_t)ctx->cu_count * 2);
-    e = ctx->scratch.ensure(g2 * words * 4u);
-    if (e != hipSuccess) return hip_fail(ctx, e, "hipMalloc(scratch)");
-    e = nt_dev_launch_scan_call(ctx->prog_dev, &B, &O, (uint32_t)len_cap, 0xFFFFFFFFu, 1,
-                                (uint32_t*)ctx->scratch.p, words, 0, (int)g2, ctx->stream);
-    if (e != hipSuccess) return hip_fail(ctx, e, "launch nt_scan_call_kernel<global>");
+    const uint64_t gwords = (uint64_t)np * max_nw;
+    const uint64_t grid = std::min<uint64_t>((batch->n_reads + 3) / 4, (uint64_t)ctx->cu_count * 2);
+    if ((e = ctx->scratch.ensure(grid * 4 * gwords * 4)) != hipSuccess) return hip_fail(ctx, e, "hipMalloc(scratch)");
+    e = nt_dev_launch_scan(ctx->prog_dev, &B, &O, (uint32_t)len_cap, 0xFFFFFFFFu, 0,
+                           (uint32_t)(nh * 64), (uint32_t*)ctx->scratch.p, gwords, (int)grid, ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e, "launch nt_scan_kernel<global>");
+  }
+  // ---- call: one workgroup (np waves) per read
+  const uint64_t max_nmw = (max_nw + 63) / 64;
+  uint64_t call_cap = max_len;
+  if (max_nmw > kCallTmCapWords) {
+    uint64_t lo = 0, hi = max_len;
+    while (lo < hi) {
+      const uint64_t mid = (lo + hi + 1) / 2;
+      if (((uint64_t)window_count((int64_t)mid, L) + 63) / 64 <= kCallTmCapWords) lo = mid; else hi = mid - 1;
+    }
+    call_cap = lo;
+  }
+  {
+    const uint64_t tmw = std::max<uint64_t>(1, std::min<uint64_t>(max_nmw, kCallTmCapWords));
+    const uint64_t grid = std::min<uint64_t>(batch->n_reads, (uint64_t)ctx->cu_count * 16);
+    e = nt_dev_launch_call(ctx->prog_dev, (const uint32_t*)ctx->thr.p, &B, &O, 0u, (uint32_t)call_cap, 1,
+                           (uint32_t)tmw, nullptr, np, (int)grid, ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e, "launch nt_call_kernel<lds>");
+  }
+  if (call_cap < max_len) {
+    const uint64_t grid = std::min<uint64_t>(batch->n_reads, (uint64_t)ctx->cu_count * 2);
+    if ((e = ctx->scratch2.ensure(grid * NT_MAX_PASS * max_nmw * 8)) != hipSuccess)
+      return hip_fail(ctx, e, "hipMalloc(scratch2)");
+    e = nt_dev_launch_call(ctx->prog_dev, (const uint32_t*)ctx->thr.p, &B, &O, (uint32_t)call_cap,
+                           0xFFFFFFFFu, 0, (uint32_t)max_nmw, (uint64_t*)ctx->scratch2.p, np, (int)grid,
+                           ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e, "launch nt_call_kernel<global>");
   }
   return NT_OK;
 }
@@ -510,7 +576,7 @@ int nt_analyze_host(nt_ctx* ctx, const char* const* seqs, const uint64_t* lens, 
              te ? (const uint32_t*)ctx->exc_off.p : nullptr,
              te ? (const uint32_t*)ctx->exc_pos.p : nullptr,
              te ? (const uint8_t*)ctx->exc_code.p : nullptr, n_reads};
-  nt_out O{win_counts ? (uint16_t*)ctx->wc.p : nullptr, (int32_t*)ctx->start.p, (int32_t*)ctx->end.p,
+  nt_out O{(uint16_t*)ctx->wc.p, (int32_t*)ctx->start.p, (int32_t*)ctx->end.p,
            (double*)ctx->dens.p, (uint8_t*)ctx->flags.p, hits ? (uint32_t*)ctx->hits.p : nullptr};
   rc = nt_scan_call(ctx, &B, &O, ml);
   if (rc) return rc;

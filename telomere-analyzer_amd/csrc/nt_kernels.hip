@@ -1,18 +1,25 @@
 // nt_kernels.hip -- NanoTel hot path on MI355X (gfx950 / CDNA4).
 //
-// One workgroup (4 waves) owns one read at a time (grid-stride over reads):
-//   1. scan   : bit-sliced matchPattern of every pattern at 32 starts per lane
-//               (exact and <=1 mismatch in the same pass, Biostrings OOB rule),
-//               coverage = OR of shifted hit words (trim + IRanges::reduce),
-//               coverage words of every pass kept in LDS.
-//   2. windows: per-window covered-base counts (get_sub_density numerators,
-//               analyze_subtelos NanoTel.R:717-766) -> LDS + HBM (uint16).
-//   3. call   : wave p runs pass p's telomere calling (A8-A12:
-//               find_telo_position, _wraper, get_accurate_*, find_left/right,
-//               search_left/right_patterns) with ballot bitmasks over windows
-//               and LDS coverage range queries; fp64 sums in R's order.
-//   4. row    : analyze_read row fields (NanoTel.R:1840-1974).
-// No MFMA: this is integer/bit work bound by HBM.
+// Two launches per batch:
+//
+//  nt_scan_kernel  (streaming, HBM-bound): one wave per read, grid-stride.
+//     Each lane owns one 32-base word; bit-sliced matchPattern of every
+//     pattern at the 32 starts of its word (exact and <=1 mismatch in one
+//     pass, Biostrings' out-of-bound rule), coverage = OR of shifted hit words
+//     (trim + IRanges::reduce), covered-base counts per subseq_length window
+//     accumulated with LDS atomics -> uint16 window counts in HBM
+//     (analyze_subtelos / get_sub_density numerators, NanoTel.R:717-766,
+//     449-468) and matchPattern hit counts.
+//
+//  nt_call_kernel  (latency-bound, tiny traffic): one workgroup per read,
+//     wave p = pass p.  Telomere calling from the window counts: telomeric
+//     window bitmask by ballot, find_telo_position / _wraper run scans,
+//     get_accurate_start/end, find_left/right_telo, search_left/right_patterns
+//     (NanoTel.R:973-1155, 1692-1764, 843-959, 496-697) and the row densities.
+//     Coverage near the telomere boundaries is recomputed from the 2-bit
+//     planes ("regions"), so no per-base state is ever written to HBM.
+//
+// No MFMA: integer/bit work, bound by HBM bandwidth.
 #include <hip/hip_runtime.h>
 
 #include "nt_common.h"
@@ -21,40 +28,216 @@
 
 namespace nt {
 
+// floor(p / L) for 0 <= p < 2^31 (exact: libdivide-style round-up magic)
+__device__ __forceinline__ int64_t div_l(const NtProgram* prog, int64_t p) {
+  return (int64_t)(((uint64_t)p * prog->div_m) >> prog->div_s);
+}
+
+// ================================================================= scan
+
+// Add the popcount of coverage word `cov` (positions [p0, p0+31]) to the
+// window counters; window k = min(p / L, nw - 1) (split_telo's last window
+// absorbs the tail).
+template <bool kLds>
+__device__ __forceinline__ void window_add(uint32_t* cnt, const NtProgram* prog, int L, int64_t nw,
+                                           int64_t p0, uint32_t cov) {
+  if (!cov) return;
+  int64_t k0 = div_l(prog, p0), k1 = div_l(prog, p0 + 31);
+  if (k0 > nw - 1) k0 = nw - 1;
+  if (k1 > nw - 1) k1 = nw - 1;
+  if (k0 == k1) {
+    atomicAdd(&cnt[k0], (uint32_t)__builtin_popcount(cov));
+    return;
+  }
+  for (int64_t k = k0; k <= k1; ++k) {
+    const int64_t lo = k * L > p0 ? k * L - p0 : 0;
+    const int64_t hi = k == k1 ? 31 : (k + 1) * L - 1 - p0;
+    const uint32_t mhi = hi >= 31 ? 0xFFFFFFFFu : ((1u << (uint32_t)(hi + 1)) - 1u);
+    const uint32_t part = cov & mhi & (0xFFFFFFFFu << (uint32_t)lo);
+    if (part) atomicAdd(&cnt[k], (uint32_t)__builtin_popcount(part));
+  }
+}
+
+// One pattern at this lane's 32 starts: hit words (exact a0, <=1 mismatch a1).
+template <bool kValid>
+__device__ __forceinline__ void chunk_hits(const ReadCtx& rc, const NtPat& P, int64_t base,
+                                           uint2 b0, uint2 b1, uint32_t V0, uint32_t V1,
+                                           uint32_t& a0, uint32_t& a1) {
+  hits32<kValid>(b0.x, b1.x, b0.y, b1.y, V0, V1, P.tm_scan, P.m, a0, a1);
+  if (kValid && P.m <= 1) a1 &= V0;
+  if (rc.n_exc) patch_exceptions(rc, base, 0, rc.n - 1, P, false, a0, a1);
+}
+
+template <bool kValid, bool kLds>
+__device__ __forceinline__ void scan_chunk(const NtProgram* __restrict__ prog, const ReadCtx& rc,
+                                           int64_t c0, int lane, int np, int64_t nw,
+                                           uint32_t* cnt, uint32_t* hitacc) {
+  const int n_pat = prog->n_pat, n_tvr = prog->n_tvr, L = prog->L;
+  const int64_t n = rc.n;
+  const int64_t w = c0 + lane - 1;    // offset-space word: positions [32(w-1), 32(w-1)+31]
+  const int64_t base = 32 * (w - 1);
+  const bool owned = lane >= 1 && w <= rc.nblk;
+  // planes of positions [base, base+63] = blocks w-1 and w; lane l's block w-1
+  // is lane l-1's block w (one coalesced load + a lane shift)
+  const uint2 b1 = load_blk(rc, w);
+  uint2 b0;
+  b0.x = __shfl_up(b1.x, 1, kWave);
+  b0.y = __shfl_up(b1.y, 1, kWave);
+  if (lane == 0) b0 = load_blk(rc, w - 1);
+  uint32_t V0 = 0xFFFFFFFFu, V1 = 0xFFFFFFFFu;
+  if (kValid) {
+    V0 = range_mask(base, 0, n - 1);
+    V1 = range_mask(base + 32, 0, n - 1);
+  }
+  uint32_t cv0 = 0u, cv1 = 0u;
+  for (int p = 0; p < n_pat; ++p) {
+    const NtPat& P = prog->pat[p];
+    uint32_t a0, a1;
+    chunk_hits<kValid>(rc, P, base, b0, b1, V0, V1, a0, a1);
+    if (owned) {
+      atomicAdd(&hitacc[p * kWave + lane], (uint32_t)__builtin_popcount(a0));
+      atomicAdd(&hitacc[(n_pat + p) * kWave + lane], (uint32_t)__builtin_popcount(a1));
+    }
+    const uint32_t p0 = __shfl_up(a0, 1, kWave), p1 = __shfl_up(a1, 1, kWave);
+    cv0 |= spread(a0, p0, P.m);
+    cv1 |= spread(a1, p1, P.m);
+  }
+  uint32_t cv2 = cv1;
+  if (np == 3) {
+    for (int t = 0; t < n_tvr; ++t) {
+      const NtPat& P = prog->tvr[t];
+      uint32_t a0, a1;
+      chunk_hits<kValid>(rc, P, base, b0, b1, V0, V1, a0, a1);
+      if (owned) atomicAdd(&hitacc[(2 * n_pat + t) * kWave + lane], (uint32_t)__builtin_popcount(a0));
+      const uint32_t p0 = __shfl_up(a0, 1, kWave);
+      cv2 |= spread(a0, p0, P.m);
+    }
+  }
+  if (owned && w >= 1 && nw > 0) {
+    if (kValid) {
+      cv0 &= V0;
+      cv1 &= V0;
+      cv2 &= V0;
+    }
+    window_add<kLds>(cnt, prog, L, nw, base, cv0);
+    window_add<kLds>(cnt + nw, prog, L, nw, base, cv1);
+    if (np == 3) window_add<kLds>(cnt + 2 * nw, prog, L, nw, base, cv2);
+  }
+}
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// LDS per wave: [n_hits][64] per-lane hit accumulators, then (kLds) the
+// window counters [pass][window] (uint32).  !kLds: counters in global scratch.
+template <bool kLds>
+__global__ void __launch_bounds__(kWG)
+nt_scan_kernel(const NtProgram* __restrict__ prog, NtBatch B, NtOut O, uint32_t len_lo,
+               uint32_t len_hi, uint32_t wave_words, uint32_t* __restrict__ gcnt,
+               uint64_t gcnt_words) {
+  extern __shared__ uint32_t smem[];
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x >> 6;
+  const uint64_t gw = (uint64_t)blockIdx.x * kNWaves + wave, GW = (uint64_t)gridDim.x * kNWaves;
+  const int np = prog->n_pass, nh = prog->n_hits, L = prog->L;
+  uint32_t* hitacc = smem + (uint64_t)wave * wave_words;
+  uint32_t* cnt = kLds ? hitacc + nh * kWave : gcnt + gw * gcnt_words;
+
+  for (uint64_t r = gw; r < B.n_reads; r += GW) {
+    const uint32_t n32 = B.len[r];
+    if (n32 <= len_lo || n32 > len_hi) continue;
+    ReadCtx rc;
+    rc.n = n32;
+    rc.nblk = (int32_t)((n32 + 31u) >> 5);
+    rc.blk = reinterpret_cast<const uint2*>(B.planes) + B.blk_off[r];
+    rc.n_exc = 0;
+    rc.exc_pos = nullptr;
+    rc.exc_code = nullptr;
+    if (B.exc_off) {
+      const uint32_t e0 = B.exc_off[r], e1 = B.exc_off[r + 1];
+      rc.n_exc = (int32_t)(e1 - e0);
+      rc.exc_pos = B.exc_pos + e0;
+      rc.exc_code = B.exc_code + e0;
+    }
+    const int64_t n = rc.n, nblk = rc.nblk;
+    const int64_t nw = split_window_count(n, L);
+    const int64_t ncnt = nw * np;
+    for (int64_t i = lane; i < ncnt; i += kWave) cnt[i] = 0u;
+    for (int c = 0; c < nh; ++c) hitacc[c * kWave + lane] = 0u;
+    wave_sync();
+
+    for (int64_t c0 = 0; c0 <= nblk; c0 += kOwned) {
+      // interior chunk: every lane's positions [base, base+63] inside the read
+      if (c0 >= 2 && 32 * c0 + 32 * kWave <= n)
+        scan_chunk<false, kLds>(prog, rc, c0, lane, np, nw, cnt, hitacc);
+      else
+        scan_chunk<true, kLds>(prog, rc, c0, lane, np, nw, cnt, hitacc);
+    }
+    wave_sync();
+
+    if (O.win_counts) {
+      uint16_t* out = O.win_counts + B.win_off[r] * np;
+      for (int64_t i = lane; i < ncnt; i += kWave) out[i] = (uint16_t)cnt[i];
+    }
+    if (O.hits) {
+      for (int c = 0; c < nh; ++c) {
+        const uint32_t v = wave_sum_u32(hitacc[c * kWave + lane]);
+        if (lane == 0) O.hits[r * (uint64_t)nh + c] = v;
+      }
+    }
+    wave_sync();
+  }
+}
+
+// ================================================================= call
+
 struct Pos {
   int64_t s, e;
 };
 
-// Per-pass calling context (uniform across the calling wave).
-struct PassCtx {
-  ReadCtx rc;  // by value: taking the address of a local would force it to scratch
-  const NtProgram* prog;
-  const uint32_t* cov;  // coverage words, position space: word i = positions [32i, 32i+31]
-  const uint16_t* cnt;  // window counts
-  const uint64_t* tm;   // telomeric-window bitmask
-  int64_t n, nw, nmw;
-  int32_t nblk;
-  int L;
-  int k;        // 0 for P1, 1 for P2/P3
-  bool use_tvr; // P3
-  bool raw;     // P1 with raw views (single fixed pattern)
-  int lane;
+// A "region": coverage of 63*32 = 2016 consecutive positions [P0, P0+2015]
+// recomputed from the planes, one 32-bit word per lane (lanes 1..63).
+// S/E: range-start / range-end marks of this pass's range set (run starts
+// and ends of the reduced coverage, or raw view starts/ends for P1 with a
+// single fixed pattern).
+struct Region {
+  int64_t P0;
+  uint32_t cov, S, E;
 };
 
-__device__ __forceinline__ int64_t wstart(const PassCtx& c, int64_t i) { return 1 + i * (int64_t)c.L; }
-__device__ __forceinline__ int64_t wend(const PassCtx& c, int64_t i) {
+constexpr int64_t kRegionSpan = 32 * kOwned;
+
+struct CallCtx {
+  ReadCtx rc;
+  const NtProgram* prog;
+  const uint16_t* cnt;  // this pass's window counts (HBM)
+  const uint64_t* tm;   // telomeric window bitmask (LDS)
+  int64_t n, nw, nmw;
+  int L;
+  int k;         // 0 for P1, 1 for P2/P3
+  bool use_tvr;  // P3
+  bool raw;      // P1 raw views
+  int lane;
+  Region R0, R1;  // two-entry region cache
+  int lru;
+};
+
+__device__ __forceinline__ int64_t wstart(const CallCtx& c, int64_t i) { return 1 + i * (int64_t)c.L; }
+__device__ __forceinline__ int64_t wend(const CallCtx& c, int64_t i) {
   return i == c.nw - 1 ? c.n : wstart(c, i) + c.L - 1;
 }
-__device__ __forceinline__ double wdens(const PassCtx& c, int64_t i) {
-  return (double)c.cnt[i] / (double)(wend(c, i) - wstart(c, i) + 1);
+__device__ __forceinline__ uint32_t wcount(const CallCtx& c, int64_t i) { return c.cnt[i]; }
+__device__ __forceinline__ double wdens(const CallCtx& c, int64_t i) {
+  return (double)wcount(c, i) / (double)(wend(c, i) - wstart(c, i) + 1);
 }
 
-// ---------------------------------------------------------- window bitmask
+// --------------------------------------------------------- window bitmask
 
-__device__ __forceinline__ bool tbit(const PassCtx& c, int64_t i) {
-  return (c.tm[i >> 6] >> (i & 63)) & 1ull;
-}
-__device__ __forceinline__ int64_t next_set(const PassCtx& c, int64_t pos, bool inv) {
+__device__ __forceinline__ bool tbit(const CallCtx& c, int64_t i) { return (c.tm[i >> 6] >> (i & 63)) & 1ull; }
+
+__device__ __forceinline__ int64_t next_set(const CallCtx& c, int64_t pos, bool inv) {
   if (pos >= c.nw) return c.nw;
   int64_t wi = pos >> 6;
   uint64_t x = (inv ? ~c.tm[wi] : c.tm[wi]) & (~0ull << (pos & 63));
@@ -67,7 +250,8 @@ __device__ __forceinline__ int64_t next_set(const PassCtx& c, int64_t pos, bool 
     x = inv ? ~c.tm[wi] : c.tm[wi];
   }
 }
-__device__ __forceinline__ int64_t prev_set(const PassCtx& c, int64_t pos, bool inv) {
+
+__device__ __forceinline__ int64_t prev_set(const CallCtx& c, int64_t pos, bool inv) {
   if (pos < 0) return -1;
   if (pos >= c.nw) pos = c.nw - 1;
   int64_t wi = pos >> 6;
@@ -80,114 +264,156 @@ __device__ __forceinline__ int64_t prev_set(const PassCtx& c, int64_t pos, bool 
   }
 }
 
-// ------------------------------------------------------ coverage queries
+// ---------------------------------------------------------------- regions
 
-// 32 coverage bits of positions [p, p+31] (0 outside the read).
-__device__ __forceinline__ uint32_t cov_at(const PassCtx& c, int64_t p) {
-  const int64_t b = p >> 5;
-  const uint32_t off = (uint32_t)(p & 31);
-  const uint32_t x = (b >= 0 && b < c.nblk) ? c.cov[b] : 0u;
-  const uint32_t y = (b + 1 >= 0 && b + 1 < c.nblk) ? c.cov[b + 1] : 0u;
-  return funnel(y, x, off);
+__device__ __forceinline__ Region make_region(const CallCtx& c, int64_t P0) {
+  const ReadCtx& rc = c.rc;
+  const int64_t q = P0 + 32 * (int64_t)(c.lane - 1);  // this lane's 32 positions / starts
+  const NtProgram* prog = c.prog;
+  uint32_t cov = 0u, raw = 0u;
+  for (int p = 0; p < prog->n_pat; ++p) {
+    const NtPat& P = prog->pat[p];
+    uint32_t a0, a1;
+    hits_at(rc, P, false, q, 0, rc.n - 1, a0, a1);
+    const uint32_t h = c.k ? a1 : a0;
+    if (p == 0) raw = a0;
+    cov |= spread(h, __shfl_up(h, 1, kWave), P.m);
+  }
+  if (c.use_tvr) {
+    for (int t = 0; t < prog->n_tvr; ++t) {
+      const NtPat& P = prog->tvr[t];
+      uint32_t a0, a1;
+      hits_at(rc, P, false, q, 0, rc.n - 1, a0, a1);
+      cov |= spread(a0, __shfl_up(a0, 1, kWave), P.m);
+    }
+  }
+  cov &= range_mask(q, 0, rc.n - 1);
+  const uint32_t cprev = __shfl_up(cov, 1, kWave), cnext = __shfl_down(cov, 1, kWave);
+  const uint32_t rprev = __shfl_up(raw, 1, kWave);
+  Region R;
+  R.P0 = P0;
+  R.cov = cov;
+  if (c.raw) {
+    // raw views of pattern 0: starts = hit starts, ends = starts + m - 1
+    const int m = prog->pat[0].m;
+    R.S = raw;
+    R.E = m > 1 ? funnel(raw, rprev, (uint32_t)(33 - m)) : raw;
+  } else {
+    R.S = cov & ~((cov << 1) | (cprev >> 31));
+    R.E = cov & ~((cov >> 1) | (cnext << 31));
+  }
+  if (c.lane == 0) R.cov = R.S = R.E = 0u;  // helper lane
+  return R;
 }
 
-// sum(width(intersect(IRanges(a1, b1), ranges))) -- wave-parallel popcount.
-__device__ __forceinline__ int64_t range_count(const PassCtx& c, int64_t a1, int64_t b1) {
-  int64_t a = (a1 < 1 ? 1 : a1) - 1, b = (b1 > c.n ? c.n : b1) - 1;
-  if (a > b) return 0;
-  const int64_t ia = a >> 5, ib = b >> 5;
-  uint32_t acc = 0;
-  for (int64_t i = ia + c.lane; i <= ib; i += kWave) {
-    uint32_t w = c.cov[i];
-    if (i == ia) w &= 0xFFFFFFFFu << (uint32_t)(a & 31);
-    if (i == ib) w &= 0xFFFFFFFFu >> (uint32_t)(31 - (b & 31));
-    acc += __builtin_popcount(w);
+// A cached region containing [x, y] (y - x < kRegionSpan - 64).
+__device__ __forceinline__ Region region_for(CallCtx& c, int64_t x, int64_t y) {
+  if (c.R0.P0 != INT64_MIN && x >= c.R0.P0 && y <= c.R0.P0 + kRegionSpan - 1) {
+    c.lru = 1;
+    return c.R0;
   }
+  if (c.R1.P0 != INT64_MIN && x >= c.R1.P0 && y <= c.R1.P0 + kRegionSpan - 1) {
+    c.lru = 0;
+    return c.R1;
+  }
+  // new region: x sits ~1/4 into it (aligned to 32 so lanes load whole blocks)
+  int64_t P0 = x - (kRegionSpan / 4);
+  P0 = (P0 >> 5) << 5;
+  if (y > P0 + kRegionSpan - 1) P0 = (x >> 5) << 5;
+  const Region R = make_region(c, P0);
+  if (c.lru == 0) { c.R0 = R; c.lru = 1; }
+  else { c.R1 = R; c.lru = 0; }
+  return R;
+}
+
+// |coverage ∩ [x, y]| for 0-based positions, any span (region-sized pieces).
+__device__ __forceinline__ int64_t region_count(CallCtx& c, int64_t x, int64_t y) {
+  int64_t tot = 0;
+  while (x <= y) {
+    const int64_t y2 = (y - x > kRegionSpan - 128) ? x + kRegionSpan - 129 : y;
+    const Region R = region_for(c, x, y2);
+    const int64_t q = R.P0 + 32 * (int64_t)(c.lane - 1);
+    const uint32_t w = c.lane ? (R.cov & range_mask(q, x, y2)) : 0u;
+    tot += (int64_t)wave_sum_u32((uint32_t)__builtin_popcount(w));
+    x = y2 + 1;
+  }
+  return tot;
+}
+
+// sum of window counts k in [ka, kb]
+__device__ __forceinline__ int64_t count_sum(const CallCtx& c, int64_t ka, int64_t kb) {
+  uint32_t acc = 0;
+  for (int64_t i = ka + c.lane; i <= kb; i += kWave) acc += wcount(c, i);
   return (int64_t)wave_sum_u32(acc);
 }
 
-__device__ __forceinline__ double sub_density(const PassCtx& c, int64_t s, int64_t e) {
+// sum(width(intersect(IRanges(a1, b1), ranges))) -- window counts for whole
+// windows, recomputed coverage for the partial windows at the two ends.
+__device__ __forceinline__ int64_t range_count(CallCtx& c, int64_t a1, int64_t b1) {
+  const int64_t a = (a1 < 1 ? 1 : a1) - 1, b = (b1 > c.n ? c.n : b1) - 1;
+  if (a > b) return 0;
+  if (c.nw == 0) return region_count(c, a, b);
+  const int64_t L = c.L;
+  int64_t ka = div_l(c.prog, a), kb = div_l(c.prog, b);
+  if (ka > c.nw - 1) ka = c.nw - 1;
+  if (kb > c.nw - 1) kb = c.nw - 1;
+  const int64_t ws_a = ka * L, we_b = kb == c.nw - 1 ? c.n - 1 : (kb + 1) * L - 1;
+  if (ka == kb) {
+    if (a == ws_a && b == we_b) return wcount(c, ka);
+    return region_count(c, a, b);
+  }
+  const int64_t we_a = (ka + 1) * L - 1, ws_b = kb * L;
+  int64_t tot = a == ws_a ? (int64_t)wcount(c, ka) : region_count(c, a, we_a);
+  if (kb > ka + 1) tot += count_sum(c, ka + 1, kb - 1);
+  tot += b == we_b ? (int64_t)wcount(c, kb) : region_count(c, ws_b, b);
+  return tot;
+}
+
+__device__ __forceinline__ double sub_density(CallCtx& c, int64_t s, int64_t e) {
   return (double)range_count(c, s, e) / (double)(e - s + 1);
 }
 
-// Run-start / run-end / raw-hit bits for positions [p, p+31] of this pass's
-// range set (IRanges starts/ends).  kind: 0 = starts, 1 = ends.
-__device__ __forceinline__ uint32_t range_marks(const PassCtx& c, int64_t p, int kind) {
-  if (c.raw) {
-    // raw views of the single fixed pattern: starts = hit starts; ends =
-    // starts + m - 1 (bit for position e-1 set when a view ends at e).
-    const NtPat& P = c.prog->pat[0];
-    const int64_t base = kind == 0 ? p : p - (P.m - 1);
-    uint32_t a0, a1;
-    hits_at(c.rc, P, false, base, 0, c.n - 1, a0, a1);
-    return a0;
-  }
-  const uint32_t cw = cov_at(c, p);
-  return kind == 0 ? (cw & ~cov_at(c, p - 1)) : (cw & ~cov_at(c, p + 1));
-}
-
-// min(start(ranges)) with start in [a1, b1] (1-based); returns fallback if none.
-__device__ __forceinline__ int64_t min_start_in(const PassCtx& c, int64_t a1, int64_t b1, int64_t fallback) {
-  int64_t a = a1 - 1, b = b1 - 1;  // 0-based position of the start
+// min(start(ranges)) with start in [a1, b1] (span <= 100); fallback if none.
+__device__ __forceinline__ int64_t min_start_in(CallCtx& c, int64_t a1, int64_t b1, int64_t fallback) {
+  int64_t a = a1 - 1, b = b1 - 1;
   if (a < 0) a = 0;
   if (b > c.n - 1) b = c.n - 1;
   if (a > b) return fallback;
-  const int64_t nchunk = ((b - a) >> 5) + 1;  // <= 4 for the A10 spans
-  int64_t best = INT64_MAX;
-  for (int64_t c0 = 0; c0 < nchunk; c0 += kWave) {
-    const int64_t ch = c0 + c.lane;
-    uint32_t w = 0u;
-    if (ch < nchunk) {
-      const int64_t p = a + 32 * ch;
-      w = range_marks(c, p, 0) & range_mask(p, a, b);
-    }
-    const uint64_t bal = __ballot(w != 0u);
-    if (bal) {
-      const int l = __builtin_ctzll(bal);
-      const uint32_t wl = __shfl(w, l, kWave);
-      best = a + 32 * (c0 + l) + __builtin_ctz(wl);
-      break;
-    }
-  }
-  return best == INT64_MAX ? fallback : best + 1;
+  const Region R = region_for(c, a, b);
+  const int64_t q = R.P0 + 32 * (int64_t)(c.lane - 1);
+  const uint32_t w = c.lane ? (R.S & range_mask(q, a, b)) : 0u;
+  const uint64_t bal = __ballot(w != 0u);
+  if (!bal) return fallback;
+  const int l = __builtin_ctzll(bal);
+  const uint32_t wl = __shfl(w, l, kWave);
+  return R.P0 + 32 * (int64_t)(l - 1) + __builtin_ctz(wl) + 1;
 }
 
-// max(end(ranges)) with end in [a1, b1]; returns fallback if none.
-__device__ __forceinline__ int64_t max_end_in(const PassCtx& c, int64_t a1, int64_t b1, int64_t fallback) {
-  int64_t a = a1 - 1, b = b1 - 1;  // 0-based position of the last base
+// max(end(ranges)) with end in [a1, b1] (span <= 100); fallback if none.
+__device__ __forceinline__ int64_t max_end_in(CallCtx& c, int64_t a1, int64_t b1, int64_t fallback) {
+  int64_t a = a1 - 1, b = b1 - 1;
   if (a < 0) a = 0;
   if (b > c.n - 1) b = c.n - 1;
   if (a > b) return fallback;
-  const int64_t nchunk = ((b - a) >> 5) + 1;
-  int64_t best = -1;
-  const int64_t top = ((nchunk + kWave - 1) / kWave) * kWave;
-  for (int64_t c0 = top - kWave; c0 >= 0; c0 -= kWave) {
-    const int64_t ch = c0 + c.lane;
-    uint32_t w = 0u;
-    if (ch < nchunk) {
-      const int64_t p = a + 32 * ch;
-      w = range_marks(c, p, 1) & range_mask(p, a, b);
-    }
-    const uint64_t bal = __ballot(w != 0u);
-    if (bal) {
-      const int l = 63 - __builtin_clzll(bal);
-      const uint32_t wl = __shfl(w, l, kWave);
-      best = a + 32 * (c0 + l) + 31 - __builtin_clz(wl);
-      break;
-    }
-  }
-  return best < 0 ? fallback : best + 1;
+  const Region R = region_for(c, a, b);
+  const int64_t q = R.P0 + 32 * (int64_t)(c.lane - 1);
+  const uint32_t w = c.lane ? (R.E & range_mask(q, a, b)) : 0u;
+  const uint64_t bal = __ballot(w != 0u);
+  if (!bal) return fallback;
+  const int l = 63 - __builtin_clzll(bal);
+  const uint32_t wl = __shfl(w, l, kWave);
+  return R.P0 + 32 * (int64_t)(l - 1) + (31 - __builtin_clz(wl)) + 1;
 }
 
-// ----------------------------------------------------------- A8 / A9 / A11
+// -------------------------------------------------------- A8 / A11
 
 // find_telo_position (NanoTel.R:973-1077) on the window bitmask.
-__device__ __forceinline__ Pos find_telo_position(const PassCtx& c, int64_t min_in_a_row, double thr) {
+__device__ __forceinline__ Pos find_telo_position(const CallCtx& c, int64_t min_in_a_row, double thr) {
   int64_t pos = 0, found = -1, start = -1;
   for (;;) {
     const int64_t r = next_set(c, pos, false);
     if (r >= c.nw) break;
-    const int64_t q = next_set(c, r, true) - 1;  // end of the run of telomeric windows
+    const int64_t q = next_set(c, r, true) - 1;  // last window of the telomeric run
     if (q - r + 1 >= min_in_a_row) {
       double score = 0.0;
       for (int64_t j = r; j <= q; ++j) {
@@ -209,14 +435,14 @@ __device__ __forceinline__ Pos find_telo_position(const PassCtx& c, int64_t min_
       end = wend(c, c.nw - 1);
     }
   } else {
-    // for (i in nrow:end_position): windows nw-1 .. ep-1 (0-based), reset/accumulate
+    // for (i in nrow:end_position): windows nw-1 .. ep-1 (0-based)
     const int64_t lo = ep - 1;
     bool hit = false;
     int64_t p2 = c.nw - 1;
     for (;;) {
       const int64_t q = prev_set(c, p2, false);
       if (q < lo) break;
-      const int64_t rr = prev_set(c, q, true) + 1;  // bottom of the run
+      const int64_t rr = prev_set(c, q, true) + 1;
       const int64_t r = rr > lo ? rr : lo;
       if (q - r + 1 >= min_in_a_row) {
         double score = 0.0;
@@ -235,34 +461,30 @@ __device__ __forceinline__ Pos find_telo_position(const PassCtx& c, int64_t min_
 }
 
 // find_left_telo (NanoTel.R:906-959)
-__device__ __forceinline__ Pos find_left_telo(const PassCtx& c) {
+__device__ __forceinline__ Pos find_left_telo(const CallCtx& c) {
   if (c.nw == 0) return Pos{1, 1};
   const int64_t f = next_set(c, 0, false);
-  if (f < c.nw && wstart(c, f) <= 200) {
-    const int64_t e = next_set(c, f, true) - 1;
-    return Pos{wstart(c, f), wend(c, e)};
-  }
+  if (f < c.nw && wstart(c, f) <= 200) return Pos{wstart(c, f), wend(c, next_set(c, f, true) - 1)};
   if (wstart(c, c.nw - 1) > 200) return Pos{-1, -1};
   return Pos{1, 1};
 }
 
 // find_right_telo (NanoTel.R:843-899).  err=true on a 0-row table.
-__device__ __forceinline__ Pos find_right_telo(const PassCtx& c, bool& err) {
+__device__ __forceinline__ Pos find_right_telo(const CallCtx& c, bool& err) {
   if (c.nw == 0) { err = true; return Pos{1, 1}; }
   const int64_t g = prev_set(c, c.nw - 1, false);
   if (g >= 0) {
     if (wend(c, g) < c.n - 200) return Pos{-1, -1};
-    const int64_t r = prev_set(c, g, true) + 1;
-    return Pos{wstart(c, r), wend(c, g)};
+    return Pos{wstart(c, prev_set(c, g, true) + 1), wend(c, g)};
   }
   if (wend(c, 0) < c.n - 200) return Pos{-1, -1};
   return Pos{1, 1};
 }
 
-// ----------------------------------------------------------------- A10
+// ------------------------------------------------------------------ A10
 
 // get_accurate_start (NanoTel.R:1726-1764)
-__device__ __forceinline__ int64_t accurate_start(const PassCtx& c, int64_t s) {
+__device__ __forceinline__ int64_t accurate_start(CallCtx& c, int64_t s) {
   if (s == -1) return -1;
   const double first_50 = (double)range_count(c, s, s + 49) / 50.0;
   int64_t t = s;
@@ -277,81 +499,78 @@ __device__ __forceinline__ int64_t accurate_start(const PassCtx& c, int64_t s) {
 }
 
 // get_accurate_end (NanoTel.R:1692-1721)
-__device__ __forceinline__ int64_t accurate_end(const PassCtx& c, int64_t e) {
+__device__ __forceinline__ int64_t accurate_end(CallCtx& c, int64_t e) {
   if (e == -1) return -1;
-  int64_t t = max_end_in(c, e - 99, e, e);
-  t = max_end_in(c, e + 1, e + 50, t);
-  return t;
+  const int64_t t = max_end_in(c, e - 99, e, e);
+  return max_end_in(c, e + 1, e + 50, t);
 }
 
-// ----------------------------------------------------------------- A12
+// ------------------------------------------------------------------ A12
 
-// max end / min start of fixed=TRUE matches of the pass's pattern set in the
-// sub-sequence [a1, b1] (multi_pattern_step_right/left NanoTel.R:496-575;
-// out-of-bound relative to the sub-sequence, no trim).
-__device__ __forceinline__ bool step_extreme(const PassCtx& c, int64_t a1, int64_t b1, bool want_end, int64_t& val) {
-  const int64_t A = a1 - 1, B = b1 - 1;
-  const int64_t base = A - 1;
+// The four steps of search_right_patterns / search_left_patterns
+// (NanoTel.R:576-697, width 18, step 10) evaluated in parallel: lane
+// 16*step + q matches pattern q (patterns, then TVRs) against step `step`'s
+// sub-sequence with fixed=TRUE and out-of-bound positions counted relative to
+// the sub-sequence (multi_pattern_step_*, NanoTel.R:496-575); the steps are
+// then consumed in order, stopping at the first step without a match.
+__device__ __forceinline__ int64_t search_edge(const CallCtx& c, int64_t index, bool right) {
+  const NtProgram* prog = c.prog;
+  const int npt = prog->n_pat + (c.use_tvr ? prog->n_tvr : 0);
   const bool only_exact = c.use_tvr && c.k == 0;
-  bool any = false;
-  int64_t best = want_end ? INT64_MIN : INT64_MAX;
-  const int npat = c.prog->n_pat + (c.use_tvr ? c.prog->n_tvr : 0);
-  for (int q = 0; q < npat; ++q) {
-    const bool is_tvr = q >= c.prog->n_pat;
-    const NtPat& P = is_tvr ? c.prog->tvr[q - c.prog->n_pat] : c.prog->pat[q];
-    const int k = (is_tvr || only_exact) ? 0 : c.k;
-    uint32_t a0, a1;
-    hits_at(c.rc, P, true, base, A, B, a0, a1);
-    const uint32_t h = k ? a1 : a0;
-    if (!h) continue;
-    any = true;
-    if (want_end) {
-      const int64_t e1 = base + (31 - __builtin_clz(h)) + P.m;
-      if (e1 > best) best = e1;
-    } else {
-      const int64_t s1 = base + __builtin_ctz(h) + 1;
-      if (s1 < best) best = s1;
+  const int step = c.lane >> 4, q = c.lane & 15;
+  // this lane's step window (1-based inclusive) and whether a further step exists
+  int64_t sa = 1, sb = 1;
+  uint32_t more_mask = 0u;
+  if (right) {
+    int64_t se = index + 18 < c.n ? index + 18 : c.n;
+    for (int i = 0; i < 4; ++i) {
+      if (i == step) { sa = se - 17 > 1 ? se - 17 : 1; sb = se; }
+      const int64_t ne = se + 11 < c.n ? se + 11 : c.n;
+      if (ne != se) more_mask |= 1u << i;
+      se = ne;
+    }
+  } else {
+    int64_t ss = index - 18 > 1 ? index - 18 : 1;
+    for (int i = 0; i < 4; ++i) {
+      if (i == step) { sa = ss; sb = ss + 17 < c.n ? ss + 17 : c.n; }
+      const int64_t ns = ss - 9 > 1 ? ss - 9 : 1;
+      if (ns != ss) more_mask |= 1u << i;
+      ss = ns;
     }
   }
-  if (any) val = best;
-  return any;
-}
-
-// search_right_patterns (NanoTel.R:635-697): width 18, step 10, 4 steps
-__device__ __forceinline__ int64_t search_right(const PassCtx& c, int64_t end_index) {
-  int64_t subseq_end = end_index + 18 < c.n ? end_index + 18 : c.n;
-  int64_t new_end = end_index;
-  for (int it = 0; it < 4; ++it) {
-    const int64_t curr_start = subseq_end - 17 > 1 ? subseq_end - 17 : 1;
-    int64_t v;
-    if (!step_extreme(c, curr_start, subseq_end, true, v)) break;
-    new_end = v;
-    const int64_t ne = subseq_end + 11 < c.n ? subseq_end + 11 : c.n;
-    if (ne == subseq_end) break;
-    subseq_end = ne;
+  bool found = false;
+  int64_t val = right ? INT64_MIN : INT64_MAX;
+  if (q < npt) {
+    const bool is_tvr = q >= prog->n_pat;
+    const NtPat& P = is_tvr ? prog->tvr[q - prog->n_pat] : prog->pat[q];
+    const int k = (is_tvr || only_exact) ? 0 : c.k;
+    const int64_t A = sa - 1, Bz = sb - 1, base = A - 1;
+    uint32_t a0, a1w;
+    hits_at(c.rc, P, true, base, A, Bz, a0, a1w);
+    const uint32_t h = k ? a1w : a0;
+    if (h) {
+      found = true;
+      val = right ? base + (31 - __builtin_clz(h)) + P.m : base + __builtin_ctz(h) + 1;
+    }
   }
-  return new_end;
-}
-
-// search_left_patterns (NanoTel.R:576-633)
-__device__ __forceinline__ int64_t search_left(const PassCtx& c, int64_t start_index) {
-  int64_t subseq_start = start_index - 18 > 1 ? start_index - 18 : 1;
-  int64_t new_start = start_index;
-  for (int it = 0; it < 4; ++it) {
-    const int64_t curr_end = subseq_start + 17 < c.n ? subseq_start + 17 : c.n;
-    int64_t v;
-    if (!step_extreme(c, subseq_start, curr_end, false, v)) break;
-    new_start = v;
-    const int64_t ns = subseq_start - 9 > 1 ? subseq_start - 9 : 1;
-    if (ns == subseq_start) break;
-    subseq_start = ns;
+  // reduce over the patterns of each step (16-lane groups)
+  for (int o = 8; o > 0; o >>= 1) {
+    const int64_t other = __shfl_xor(val, o, 16);
+    val = right ? (other > val ? other : val) : (other < val ? other : val);
   }
-  return new_start;
+  const uint64_t fb = __ballot(found);
+  int64_t result = index;
+  for (int i = 0; i < 4; ++i) {
+    if (!((fb >> (16 * i)) & 0xFFFFull)) break;
+    result = __shfl(val, 16 * i, kWave);
+    if (!((more_mask >> i) & 1u)) break;
+  }
+  return result;
 }
 
 // find_telo_position_wraper (NanoTel.R:1080-1155) + density (NanoTel.R:1840).
-__device__ __forceinline__ void call_pass(const PassCtx& c, int64_t& out_s, int64_t& out_e, double& out_d,
-                          uint32_t& err) {
+__device__ __forceinline__ void call_pass(CallCtx& c, int64_t& out_s, int64_t& out_e, double& out_d,
+                                          uint32_t& err) {
   Pos tp = find_telo_position(c, 3, 2.0);
   const double telo_density = sub_density(c, tp.s, tp.e);
   const int64_t num_rows = (tp.e - tp.s + 1) / c.L;
@@ -375,8 +594,8 @@ __device__ __forceinline__ void call_pass(const PassCtx& c, int64_t& out_s, int6
   }
   if (!c.prog->legacy_no_ext) {
     int64_t e2 = tp.e, s2 = tp.s;
-    if (tp.e < c.n) e2 = search_right(c, tp.e + 1);
-    if (tp.s > 1) s2 = search_left(c, tp.s - 1);
+    if (tp.e < c.n) e2 = search_edge(c, tp.e + 1, true);
+    if (tp.s > 1) s2 = search_edge(c, tp.s - 1, false);
     tp = Pos{s2, e2};
   }
   if (tp.e < tp.s - 1) { err |= NT_FLAG_ERR_WIDTH; out_s = -1; out_e = -1; out_d = 0.0; return; }
@@ -385,172 +604,73 @@ __device__ __forceinline__ void call_pass(const PassCtx& c, int64_t& out_s, int6
   out_d = sub_density(c, tp.s, tp.e);
 }
 
-// --------------------------------------------------------------- the kernel
-
-struct LdsLayout {
-  uint32_t cov_words;  // per pass
-  uint32_t cnt_words;  // per pass (uint16 pairs)
-  uint32_t tm_words;   // per pass (uint32 words of the uint64 mask; even)
-  uint32_t total;      // words for all passes
-};
-
-__host__ __device__ inline LdsLayout lds_layout(int64_t n, int L, int np) {
-  LdsLayout l;
-  const int64_t nblk = (n + 31) / 32;
-  int64_t nw = 0;
-  if (n > 0 && L > 0) {
-    nw = (n - 1) / L + 1;
-    const int64_t last_start = 1 + (nw - 1) * (int64_t)L;
-    if ((double)(n - last_start) < (double)L / 2.0) nw -= 1;
-  }
-  l.cov_words = (uint32_t)((nblk + 1) & ~1ll);
-  l.cnt_words = (uint32_t)((((nw + 1) / 2) + 1) & ~1ll);
-  l.tm_words = (uint32_t)(((nw + 63) / 64) * 2);
-  l.total = (uint32_t)np * (l.cov_words + l.cnt_words + l.tm_words);
-  return l;
-}
-
-template <bool kGlobal>
-__global__ void __launch_bounds__(kWG)
-nt_scan_call_kernel(const NtProgram* __restrict__ prog, NtBatch B, NtOut O, uint32_t len_lo,
-                    uint32_t len_hi, uint32_t* __restrict__ gscratch, uint64_t scratch_words) {
-  extern __shared__ uint32_t smem[];
-  __shared__ uint32_t s_hits[3 * NT_MAX_PAT];
+// One workgroup per read (grid-stride), wave p = pass p; LDS per wave:
+// telomeric-window bitmask (tm_words uint64).  thr[w]: smallest count c with
+// !(c / w < min_density) (exact fp64 compare, host-computed).
+template <bool kLds>
+__global__ void __launch_bounds__(64 * NT_MAX_PASS)
+nt_call_kernel(const NtProgram* __restrict__ prog, const uint32_t* __restrict__ thr, NtBatch B,
+               NtOut O, uint32_t len_lo, uint32_t len_hi, uint32_t tm_words,
+               uint64_t* __restrict__ gtm) {
+  extern __shared__ uint64_t smem64[];
   __shared__ int64_t s_res_s[NT_MAX_PASS], s_res_e[NT_MAX_PASS];
   __shared__ double s_res_d[NT_MAX_PASS];
   __shared__ uint32_t s_err;
-
-  const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid >> 6;
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x >> 6;
   const int np = prog->n_pass, L = prog->L;
-  const int n_pat = prog->n_pat, n_tvr = prog->n_tvr;
-  const double min_density = prog->min_density;
-  uint32_t* store = kGlobal ? gscratch + (uint64_t)blockIdx.x * scratch_words : smem;
+  uint64_t* tm = kLds ? smem64 + (uint64_t)wave * tm_words
+                      : gtm + ((uint64_t)blockIdx.x * NT_MAX_PASS + wave) * tm_words;
 
   for (uint64_t r = blockIdx.x; r < B.n_reads; r += gridDim.x) {
     const uint32_t n32 = B.len[r];
     if (n32 <= len_lo || n32 > len_hi) continue;
-    ReadCtx rc;
-    rc.n = n32;
-    rc.nblk = (int32_t)((n32 + 31u) >> 5);
-    rc.blk = reinterpret_cast<const uint2*>(B.planes) + B.blk_off[r];
-    rc.n_exc = 0;
-    rc.exc_pos = nullptr;
-    rc.exc_code = nullptr;
-    if (B.exc_off) {
-      const uint32_t e0 = B.exc_off[r], e1 = B.exc_off[r + 1];
-      rc.n_exc = (int32_t)(e1 - e0);
-      rc.exc_pos = B.exc_pos + e0;
-      rc.exc_code = B.exc_code + e0;
-    }
-    const int64_t n = rc.n;
-    const int32_t nblk = rc.nblk;
-    const int64_t nw = split_window_count(n, L);
-    const LdsLayout lay = lds_layout(n, L, np);
-    uint32_t* cov = store;
-    uint16_t* cnt = reinterpret_cast<uint16_t*>(store + np * lay.cov_words);
-    uint64_t* tm = reinterpret_cast<uint64_t*>(store + np * (lay.cov_words + lay.cnt_words));
-
-    if (tid < 3 * NT_MAX_PAT) s_hits[tid] = 0u;
-    if (tid == 0) s_err = 0u;
+    if (threadIdx.x == 0) s_err = 0u;
     __syncthreads();
-
-    // ---------------------------------------------------------------- scan
-    // Offset-space word w covers positions [32(w-1), 32(w-1)+31]; words
-    // 0..nblk hold hit starts (start -1 lives in word 0), coverage is kept for
-    // words 1..nblk.  Lane 0 of every wave-chunk recomputes the word before
-    // the chunk so that lanes 1..63 get their carry-in starts by a shuffle.
-    for (int64_t c0 = (int64_t)wave * kOwned; c0 <= nblk; c0 += (int64_t)kOwned * kNWaves) {
-      const int64_t w = c0 + lane - 1;
-      const int64_t base = 32 * (w - 1);
-      const bool owned = lane >= 1 && w <= nblk;
-      const uint2 b0 = load_blk(rc, w - 1), b1 = load_blk(rc, w);
-      const uint32_t V0 = range_mask(base, 0, n - 1), V1 = range_mask(base + 32, 0, n - 1);
-      uint32_t cv0 = 0u, cv1 = 0u, cv2 = 0u;
-      for (int p = 0; p < n_pat; ++p) {
-        const NtPat& P = prog->pat[p];
-        uint32_t a0, a1;
-        hits32(b0.x, b1.x, b0.y, b1.y, V0, V1, P.tt_scan, P.m, a0, a1);
-        if (P.m <= 1) a1 &= V0;
-        if (rc.n_exc) patch_exceptions(rc, base, 0, n - 1, P, false, a0, a1);
-        const uint32_t h0 = wave_sum_u32(owned ? (uint32_t)__builtin_popcount(a0) : 0u);
-        const uint32_t h1 = wave_sum_u32(owned ? (uint32_t)__builtin_popcount(a1) : 0u);
-        if (lane == 0) {
-          atomicAdd(&s_hits[p], h0);
-          atomicAdd(&s_hits[n_pat + p], h1);
-        }
-        const uint32_t p0 = __shfl_up(a0, 1, kWave), p1 = __shfl_up(a1, 1, kWave);
-        cv0 |= spread(a0, p0, P.m);
-        cv1 |= spread(a1, p1, P.m);
-      }
-      if (np == 3) {
-        cv2 = cv1;
-        for (int t = 0; t < n_tvr; ++t) {
-          const NtPat& P = prog->tvr[t];
-          uint32_t a0, a1;
-          hits32(b0.x, b1.x, b0.y, b1.y, V0, V1, P.tt_scan, P.m, a0, a1);
-          if (rc.n_exc) patch_exceptions(rc, base, 0, n - 1, P, false, a0, a1);
-          const uint32_t h0 = wave_sum_u32(owned ? (uint32_t)__builtin_popcount(a0) : 0u);
-          if (lane == 0) atomicAdd(&s_hits[2 * n_pat + t], h0);
-          const uint32_t p0 = __shfl_up(a0, 1, kWave);
-          cv2 |= spread(a0, p0, P.m);
-        }
-      }
-      if (owned && w >= 1) {
-        cov[w - 1] = cv0 & V0;
-        cov[lay.cov_words + w - 1] = cv1 & V0;
-        if (np == 3) cov[2 * lay.cov_words + w - 1] = cv2 & V0;
-      }
-    }
-    __syncthreads();
-
-    // ------------------------------------------------------- window counts
-    for (int64_t i = tid; i < nw; i += kWG) {
-      const int64_t ws = i * (int64_t)L;
-      const int64_t we = (i == nw - 1) ? n - 1 : ws + L - 1;
-      for (int p = 0; p < np; ++p) {
-        const uint32_t* cp = cov + p * lay.cov_words;
-        uint32_t acc = 0;
-        for (int64_t wi = ws >> 5; wi <= (we >> 5); ++wi) {
-          uint32_t x = cp[wi];
-          if (wi == (ws >> 5)) x &= 0xFFFFFFFFu << (uint32_t)(ws & 31);
-          if (wi == (we >> 5)) x &= 0xFFFFFFFFu >> (uint32_t)(31 - (we & 31));
-          acc += __builtin_popcount(x);
-        }
-        cnt[p * (2 * lay.cnt_words) + i] = (uint16_t)acc;
-        if (O.win_counts) O.win_counts[B.win_off[r] * np + (uint64_t)p * nw + i] = (uint16_t)acc;
-      }
-    }
-    __syncthreads();
-
-    // ------------------------------------------------------------- calling
     if (wave < np) {
       const int p = wave;
-      PassCtx c;
-      c.rc = rc;
+      CallCtx c;
+      c.rc.n = n32;
+      c.rc.nblk = (int32_t)((n32 + 31u) >> 5);
+      c.rc.blk = reinterpret_cast<const uint2*>(B.planes) + B.blk_off[r];
+      c.rc.n_exc = 0;
+      c.rc.exc_pos = nullptr;
+      c.rc.exc_code = nullptr;
+      if (B.exc_off) {
+        const uint32_t e0 = B.exc_off[r], e1 = B.exc_off[r + 1];
+        c.rc.n_exc = (int32_t)(e1 - e0);
+        c.rc.exc_pos = B.exc_pos + e0;
+        c.rc.exc_code = B.exc_code + e0;
+      }
       c.prog = prog;
-      c.cov = cov + p * lay.cov_words;
-      c.cnt = cnt + p * (2 * lay.cnt_words);
-      uint64_t* tmp = tm + p * (lay.tm_words / 2);
-      c.tm = tmp;
-      c.n = n;
-      c.nw = nw;
-      c.nmw = (nw + 63) >> 6;
-      c.nblk = nblk;
+      c.n = n32;
+      c.nw = split_window_count(c.n, L);
+      c.nmw = (c.nw + 63) >> 6;
+      c.cnt = O.win_counts + B.win_off[r] * np + (uint64_t)p * c.nw;
+      c.tm = tm;
       c.L = L;
       c.k = p == 0 ? 0 : 1;
       c.use_tvr = p == 2;
       c.raw = p == 0 && prog->raw_p1;
       c.lane = lane;
-      // telomeric-window bitmask: class -5 iff !(density < min_density)
+      c.R0.P0 = INT64_MIN;
+      c.R1.P0 = INT64_MIN;
+      c.lru = 0;
+      // class -5 ("telomeric") iff !(count/width < min_density) iff count >= thr[width]
+      const int64_t tsz = prog->thr_size;
+      const uint32_t thr_full = thr[L < tsz ? L : tsz - 1];
+      uint32_t thr_last = thr_full;
+      if (c.nw > 0) {
+        const int64_t wl = c.n - (c.nw - 1) * (int64_t)L;
+        thr_last = thr[wl < tsz ? wl : tsz - 1];
+      }
       for (int64_t ch = 0; ch < c.nmw; ++ch) {
         const int64_t i = ch * 64 + lane;
         bool t = false;
-        if (i < nw) t = !(wdens(c, i) < min_density);
+        if (i < c.nw) t = wcount(c, i) >= (i == c.nw - 1 ? thr_last : thr_full);
         const uint64_t bal = __ballot(t);
-        if (lane == 0) tmp[ch] = bal;
+        if (lane == 0) tm[ch] = bal;
       }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
+      wave_sync();
       int64_t s, e;
       double d;
       uint32_t err = 0;
@@ -563,9 +683,7 @@ nt_scan_call_kernel(const NtProgram* __restrict__ prog, NtBatch B, NtOut O, uint
       }
     }
     __syncthreads();
-
-    // ----------------------------------------------------------------- row
-    if (tid == 0) {
+    if (threadIdx.x == 0) {
       int64_t maxw = INT64_MIN;
       uint32_t flags = NT_FLAG_DONE | s_err;
       for (int p = 0; p < np; ++p) {
@@ -584,12 +702,10 @@ nt_scan_call_kernel(const NtProgram* __restrict__ prog, NtBatch B, NtOut O, uint
       if (maxw >= 30) flags |= NT_FLAG_TELOMERIC;
       O.flags[r] = (uint8_t)flags;
     }
-    if (O.hits && tid < prog->n_hits) O.hits[r * (uint64_t)prog->n_hits + tid] = s_hits[tid];
-    __syncthreads();
   }
 }
 
-// ------------------------------------------------------------ synthetic reads
+// ============================================================ synthetic reads
 
 // One thread per 32-base block: bases from the counter-based generator of
 // nt_rng.h (identical on the host: nt_synth_base()).
@@ -628,30 +744,43 @@ nt_layout_kernel(uint64_t n_reads, uint64_t nblk, uint64_t read_len, uint64_t nw
 
 }  // namespace nt
 
-// ------------------------------------------------------------- launchers
+// ================================================================ launchers
 
 extern "C" {
 
-uint32_t nt_dev_lds_words(int64_t n, int L, int np) { return nt::lds_layout(n, L, np).total; }
+hipError_t nt_dev_set_lds_limit(uint32_t bytes) {
+  hipError_t e = hipFuncSetAttribute((const void*)nt::nt_scan_kernel<true>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  if (e != hipSuccess) return e;
+  return hipFuncSetAttribute((const void*)nt::nt_call_kernel<true>,
+                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
 
-hipError_t nt_dev_launch_scan_call(const NtProgram* prog_dev, const NtBatch* B, const NtOut* O,
-                                   uint32_t len_lo, uint32_t len_hi, int global_scratch,
-                                   uint32_t* gscratch, uint64_t scratch_words, uint32_t lds_words,
-                                   int grid, hipStream_t stream) {
-  if (global_scratch) {
-    hipLaunchKernelGGL(nt::nt_scan_call_kernel<true>, dim3(grid), dim3(nt::kWG), 0, stream,
-                       prog_dev, *B, *O, len_lo, len_hi, gscratch, scratch_words);
-  } else {
-    hipLaunchKernelGGL(nt::nt_scan_call_kernel<false>, dim3(grid), dim3(nt::kWG),
-                       (size_t)lds_words * 4u, stream, prog_dev, *B, *O, len_lo, len_hi,
-                       (uint32_t*)nullptr, (uint64_t)0);
-  }
+hipError_t nt_dev_launch_scan(const NtProgram* prog, const NtBatch* B, const NtOut* O,
+                              uint32_t len_lo, uint32_t len_hi, int lds, uint32_t wave_words,
+                              uint32_t* gcnt, uint64_t gcnt_words, int grid, hipStream_t stream) {
+  const size_t lds_bytes = (size_t)wave_words * 4u * nt::kNWaves;
+  if (lds)
+    hipLaunchKernelGGL(nt::nt_scan_kernel<true>, dim3(grid), dim3(nt::kWG), lds_bytes, stream, prog,
+                       *B, *O, len_lo, len_hi, wave_words, gcnt, gcnt_words);
+  else
+    hipLaunchKernelGGL(nt::nt_scan_kernel<false>, dim3(grid), dim3(nt::kWG), lds_bytes, stream, prog,
+                       *B, *O, len_lo, len_hi, wave_words, gcnt, gcnt_words);
   return hipGetLastError();
 }
 
-hipError_t nt_dev_set_lds_limit(uint32_t bytes) {
-  return hipFuncSetAttribute((const void*)nt::nt_scan_call_kernel<false>,
-                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+hipError_t nt_dev_launch_call(const NtProgram* prog, const uint32_t* thr, const NtBatch* B,
+                              const NtOut* O, uint32_t len_lo, uint32_t len_hi, int lds,
+                              uint32_t tm_words, uint64_t* gtm, int np, int grid,
+                              hipStream_t stream) {
+  const size_t lds_bytes = lds ? (size_t)tm_words * 8u * np : 0;
+  if (lds)
+    hipLaunchKernelGGL(nt::nt_call_kernel<true>, dim3(grid), dim3(64 * np), lds_bytes, stream, prog,
+                       thr, *B, *O, len_lo, len_hi, tm_words, gtm);
+  else
+    hipLaunchKernelGGL(nt::nt_call_kernel<false>, dim3(grid), dim3(64 * np), 0, stream, prog, thr,
+                       *B, *O, len_lo, len_hi, tm_words, gtm);
+  return hipGetLastError();
 }
 
 hipError_t nt_dev_launch_synth(const NtSynth* S, uint32_t* planes, uint64_t n_reads,
