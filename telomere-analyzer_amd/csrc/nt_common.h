@@ -54,6 +54,8 @@ struct NtProgram {
   double min_density;     // --min_density
   uint64_t div_m;         // floor(p / L) = (p * div_m) >> div_s for p < 2^31 (exact)
   uint32_t div_s;
+  uint32_t div32_m;       // floor(p / L) = umulhi(p, div32_m) >> div32_s, p < 2^31, L >= 2
+  uint32_t div32_s;
   uint32_t thr_size;      // entries of the per-width telomeric threshold table
   NtPat pat[NT_MAX_PAT];
   NtPat tvr[NT_MAX_PAT];

@@ -46,6 +46,16 @@ __device__ __forceinline__ uint2 load_blk(const ReadCtx& rc, int64_t b) {
   return (b >= 0 && b < rc.nblk) ? rc.blk[b] : make_uint2(0u, 0u);
 }
 
+// The same, but the load itself is unconditional (clamped address, result
+// zeroed afterwards): straight-line loads let hipcc count them with partial
+// s_waitcnt vmcnt(N) instead of draining the prefetch ring with vmcnt(0).
+__device__ __forceinline__ uint2 load_blk_nc(const ReadCtx& rc, int b) {
+  const int bc = b < 0 ? 0 : (b >= rc.nblk ? rc.nblk - 1 : b);
+  const uint2 x = rc.blk[bc];
+  const bool ok = (b >= 0) & (b < rc.nblk);
+  return make_uint2(ok ? x.x : 0u, ok ? x.y : 0u);
+}
+
 // Planes of the 32 positions [p, p+31] (any p; out-of-read positions read 0).
 __device__ __forceinline__ void plane_at(const ReadCtx& rc, int64_t p, uint32_t& L, uint32_t& H) {
   const int64_t b = p >> 5;  // floor for negative p
@@ -62,18 +72,29 @@ __device__ __forceinline__ void plane_at(const ReadCtx& rc, int64_t p, uint32_t&
 // mismatches -- Biostrings' out-of-bound rule.  a0 = starts with 0
 // mismatches, a1 = <= 1.  kValid=false: every position is known valid.
 template <bool kValid>
+__device__ __forceinline__ void hits_step(uint32_t L0, uint32_t L1, uint32_t H0, uint32_t H1,
+                                          uint32_t V0, uint32_t V1, const uint32_t* __restrict__ t,
+                                          int j, uint32_t& x0, uint32_t& x1) {
+  const uint32_t Ls = funnel(L1, L0, (uint32_t)j);
+  const uint32_t Hs = funnel(H1, H0, (uint32_t)j);
+  uint32_t q = bfi(Hs, bfi(Ls, t[3], t[2]), bfi(Ls, t[1], t[0]));
+  if (kValid) q &= funnel(V1, V0, (uint32_t)j);
+  x1 = (x1 & q) | x0;
+  x0 &= q;
+}
+
+// kM > 0: pattern length known at compile time (fully unrolled, masks hoisted).
+template <bool kValid, int kM = 0>
 __device__ __forceinline__ void hits32(uint32_t L0, uint32_t L1, uint32_t H0, uint32_t H1,
                                        uint32_t V0, uint32_t V1,
                                        const uint32_t (*__restrict__ tm)[4], int m, uint32_t& a0,
                                        uint32_t& a1) {
   uint32_t x0 = 0xFFFFFFFFu, x1 = 0xFFFFFFFFu;
-  for (int j = 0; j < m; ++j) {
-    const uint32_t Ls = funnel(L1, L0, (uint32_t)j);
-    const uint32_t Hs = funnel(H1, H0, (uint32_t)j);
-    uint32_t q = bfi(Hs, bfi(Ls, tm[j][3], tm[j][2]), bfi(Ls, tm[j][1], tm[j][0]));
-    if (kValid) q &= funnel(V1, V0, (uint32_t)j);
-    x1 = (x1 & q) | x0;
-    x0 &= q;
+  if (kM) {
+#pragma unroll
+    for (int j = 0; j < kM; ++j) hits_step<kValid>(L0, L1, H0, H1, V0, V1, tm[j], j, x0, x1);
+  } else {
+    for (int j = 0; j < m; ++j) hits_step<kValid>(L0, L1, H0, H1, V0, V1, tm[j], j, x0, x1);
   }
   a0 = x0;
   a1 = x1;
@@ -81,9 +102,15 @@ __device__ __forceinline__ void hits32(uint32_t L0, uint32_t L1, uint32_t H0, ui
 
 // Coverage of 32 positions from the hit-start words of this and the previous
 // 32 starts: C[p] = OR_{j<m} H[p-j]  (trimmed views, IRanges::reduce runs).
+template <int kM = 0>
 __device__ __forceinline__ uint32_t spread(uint32_t h, uint32_t hprev, int m) {
   uint32_t c = h;
-  for (int j = 1; j < m; ++j) c |= funnel(h, hprev, (uint32_t)(32 - j));
+  if (kM) {
+#pragma unroll
+    for (int j = 1; j < kM; ++j) c |= funnel(h, hprev, (uint32_t)(32 - j));
+  } else {
+    for (int j = 1; j < m; ++j) c |= funnel(h, hprev, (uint32_t)(32 - j));
+  }
   return c;
 }
 

@@ -17,13 +17,11 @@
 #include "nt_rng.h"
 
 extern "C" {
-hipError_t nt_dev_launch_scan(const NtProgram* prog, const NtBatch* B, const NtOut* O,
-                              uint32_t len_lo, uint32_t len_hi, int lds, uint32_t wave_words,
-                              uint32_t* gcnt, uint64_t gcnt_words, int grid, hipStream_t stream);
-hipError_t nt_dev_launch_call(const NtProgram* prog, const uint32_t* thr, const NtBatch* B,
-                              const NtOut* O, uint32_t len_lo, uint32_t len_hi, int lds,
-                              uint32_t tm_words, uint64_t* gtm, int np, int grid,
-                              hipStream_t stream);
+uint32_t nt_dev_wave_words(int single, int n_hits, int np, uint32_t nw_cap);
+hipError_t nt_dev_launch(const NtProgram* prog, const uint32_t* thr, const NtBatch* B,
+                         const NtOut* O, uint32_t len_lo, uint32_t len_hi, int single, int m6,
+                         int lds, uint32_t wave_words, uint32_t nw_cap, uint32_t* gscr, int grid,
+                         hipStream_t stream);
 hipError_t nt_dev_set_lds_limit(uint32_t bytes);
 hipError_t nt_dev_launch_synth(const NtSynth* S, uint32_t* planes, uint64_t n_reads,
                                hipStream_t stream);
@@ -34,8 +32,7 @@ hipError_t nt_dev_launch_uniform_layout(uint64_t n_reads, uint64_t nblk, uint64_
 
 namespace {
 
-constexpr uint32_t kScanLdsCapBytes = 64 * 1024;  // per 4-wave workgroup; longer reads: global counters
-constexpr uint32_t kCallTmCapWords = 2048;         // per wave (16 KB); longer reads: global bitmask
+constexpr uint32_t kLdsCapBytes = 64 * 1024;  // per 4-wave workgroup; longer reads: global scratch
 
 struct DevBuf {
   void* p = nullptr;
@@ -300,6 +297,16 @@ int nt_compile(nt_ctx* ctx, const nt_params* prm, nt_program_info* info) {
     while ((1ull << l) < (uint64_t)P.L) ++l;
     P.div_s = 32 + l;
     P.div_m = (uint64_t)((((unsigned __int128)1) << (32 + l)) / (uint64_t)P.L) + 1;
+    // 32-bit form for p < 2^31: M = floor(2^(31+l) / L) + 1 < 2^32, error < 2^-l <= 1/L
+    if (P.L >= 2) {
+      const uint64_t m32 = ((1ull << (31 + l)) / (uint64_t)P.L) + 1;
+      if (m32 > 0xFFFFFFFFull) return fail(ctx, NT_E_LIMIT, "divisor magic overflow");
+      P.div32_m = (uint32_t)m32;
+      P.div32_s = l - 1;
+    } else {
+      P.div32_m = 0;
+      P.div32_s = 0;
+    }
   }
   // Telomeric class (NanoTel.R:749-758): -5 iff !(count / width < min_density).
   // fl(c / w) is monotone in c, so the class is count >= thr[w] with thr[w]
@@ -445,78 +452,55 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
   if (batch->n_reads == 0) return NT_OK;
   if (!out->win_counts || !out->start || !out->end || !out->density || !out->flags)
     return fail(ctx, NT_E_ARG, "win_counts/start/end/density/flags outputs are required");
-  if (max_len > 0x7FFFFFFFull) return fail(ctx, NT_E_LIMIT, "read longer than 2^31-1");
+  if (max_len > (1ull << 30)) return fail(ctx, NT_E_LIMIT, "read longer than 2^30 bases");
   (void)hipSetDevice(ctx->device);
   const int np = ctx->prog.n_pass, L = ctx->prog.L, nh = ctx->prog.n_hits;
+  const int single = (ctx->prog.n_pat == 1 && ctx->prog.n_tvr == 0 && np == 2) ? 1 : 0;
+  const int m6 = (single && ctx->prog.pat[0].m == 6) ? 1 : 0;
   NtBatch B{batch->planes, batch->blk_off, batch->len, batch->win_off,
             batch->exc_off, batch->exc_pos, batch->exc_code, batch->n_reads};
   NtOut O{out->win_counts, out->start, out->end, out->density, out->flags, out->hits};
+  hipError_t e;
   if (!ctx->lds_limit_set) {
-    hipError_t e = nt_dev_set_lds_limit(kScanLdsCapBytes);
-    if (e != hipSuccess) return hip_fail(ctx, e, "hipFuncSetAttribute");
+    if ((e = nt_dev_set_lds_limit(kLdsCapBytes)) != hipSuccess) return hip_fail(ctx, e, "hipFuncSetAttribute");
     ctx->lds_limit_set = true;
   }
-  hipError_t e;
-  // ---- scan: window counters in LDS up to the cap, in global scratch beyond
-  const uint64_t max_nw = (uint64_t)window_count((int64_t)max_len, L);
-  auto scan_words = [&](uint64_t nw) { return (uint64_t)nh * 64 + (uint64_t)np * nw; };
-  uint64_t cap_nw = max_nw;
-  if (scan_words(max_nw) * 4 * 4 > kScanLdsCapBytes)
-    cap_nw = (kScanLdsCapBytes / 16 - (uint64_t)nh * 64) / np;
-  // longest read whose windows fit the LDS counters
+  // per-wave scratch (window counters + bitmasks) lives in LDS up to the cap
+  const uint32_t max_nw = (uint32_t)window_count((int64_t)max_len, L);
+  auto wg_bytes = [&](uint32_t nwc) { return (uint64_t)nt_dev_wave_words(single, nh, np, nwc) * 4u * 4u; };
+  uint32_t cap_nw = max_nw;
   uint64_t len_cap = max_len;
-  if (cap_nw < max_nw) {
-    uint64_t lo = 0, hi = max_len;
+  if (wg_bytes(max_nw) > kLdsCapBytes) {
+    uint32_t lo = 0, hi = max_nw;
     while (lo < hi) {
-      const uint64_t mid = (lo + hi + 1) / 2;
-      if ((uint64_t)window_count((int64_t)mid, L) <= cap_nw) lo = mid; else hi = mid - 1;
+      const uint32_t mid = (lo + hi + 1) / 2;
+      if (wg_bytes(mid) <= kLdsCapBytes) lo = mid; else hi = mid - 1;
     }
-    len_cap = lo;
+    cap_nw = lo;
+    uint64_t a = 0, b = max_len;  // longest read with at most cap_nw windows
+    while (a < b) {
+      const uint64_t mid = (a + b + 1) / 2;
+      if ((uint64_t)window_count((int64_t)mid, L) <= cap_nw) a = mid; else b = mid - 1;
+    }
+    len_cap = a;
   }
+  const uint64_t waves_needed = batch->n_reads;
   {
-    const uint64_t ww = scan_words(std::min(cap_nw, max_nw));
-    const uint64_t wg_bytes = ww * 4 * 4;
-    uint64_t bpc = std::min<uint64_t>(8, std::max<uint64_t>(1, (160u * 1024u) / std::max<uint64_t>(wg_bytes, 1)));
-    const uint64_t waves = (batch->n_reads + 0);
-    uint64_t grid = std::min<uint64_t>((waves + 3) / 4, (uint64_t)ctx->cu_count * bpc);
-    e = nt_dev_launch_scan(ctx->prog_dev, &B, &O, 0u, (uint32_t)len_cap, 1, (uint32_t)ww, nullptr, 0,
-                           (int)std::max<uint64_t>(grid, 1), ctx->stream);
-    if (e != hipSuccess) return hip_fail(ctx, e, "launch nt_scan_kernel<lds>");
+    const uint32_t ww = nt_dev_wave_words(single, nh, np, cap_nw);
+    const uint64_t per_wg = (uint64_t)ww * 16u;
+    const uint64_t bpc = std::min<uint64_t>(8, std::max<uint64_t>(1, (160u * 1024u) / std::max<uint64_t>(per_wg, 1)));
+    const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((waves_needed + 3) / 4, (uint64_t)ctx->cu_count * bpc));
+    e = nt_dev_launch(ctx->prog_dev, (const uint32_t*)ctx->thr.p, &B, &O, 0u, (uint32_t)len_cap, single, m6, 1, ww,
+                      cap_nw, nullptr, (int)grid, ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e, "launch nt_kernel<lds>");
   }
   if (len_cap < max_len) {
-    const uint64_t gwords = (uint64_t)np * max_nw;
-    const uint64_t grid = std::min<uint64_t>((batch->n_reads + 3) / 4, (uint64_t)ctx->cu_count * 2);
-    if ((e = ctx->scratch.ensure(grid * 4 * gwords * 4)) != hipSuccess) return hip_fail(ctx, e, "hipMalloc(scratch)");
-    e = nt_dev_launch_scan(ctx->prog_dev, &B, &O, (uint32_t)len_cap, 0xFFFFFFFFu, 0,
-                           (uint32_t)(nh * 64), (uint32_t*)ctx->scratch.p, gwords, (int)grid, ctx->stream);
-    if (e != hipSuccess) return hip_fail(ctx, e, "launch nt_scan_kernel<global>");
-  }
-  // ---- call: one workgroup (np waves) per read
-  const uint64_t max_nmw = (max_nw + 63) / 64;
-  uint64_t call_cap = max_len;
-  if (max_nmw > kCallTmCapWords) {
-    uint64_t lo = 0, hi = max_len;
-    while (lo < hi) {
-      const uint64_t mid = (lo + hi + 1) / 2;
-      if (((uint64_t)window_count((int64_t)mid, L) + 63) / 64 <= kCallTmCapWords) lo = mid; else hi = mid - 1;
-    }
-    call_cap = lo;
-  }
-  {
-    const uint64_t tmw = std::max<uint64_t>(1, std::min<uint64_t>(max_nmw, kCallTmCapWords));
-    const uint64_t grid = std::min<uint64_t>(batch->n_reads, (uint64_t)ctx->cu_count * 16);
-    e = nt_dev_launch_call(ctx->prog_dev, (const uint32_t*)ctx->thr.p, &B, &O, 0u, (uint32_t)call_cap, 1,
-                           (uint32_t)tmw, nullptr, np, (int)grid, ctx->stream);
-    if (e != hipSuccess) return hip_fail(ctx, e, "launch nt_call_kernel<lds>");
-  }
-  if (call_cap < max_len) {
-    const uint64_t grid = std::min<uint64_t>(batch->n_reads, (uint64_t)ctx->cu_count * 2);
-    if ((e = ctx->scratch2.ensure(grid * NT_MAX_PASS * max_nmw * 8)) != hipSuccess)
-      return hip_fail(ctx, e, "hipMalloc(scratch2)");
-    e = nt_dev_launch_call(ctx->prog_dev, (const uint32_t*)ctx->thr.p, &B, &O, (uint32_t)call_cap,
-                           0xFFFFFFFFu, 0, (uint32_t)max_nmw, (uint64_t*)ctx->scratch2.p, np, (int)grid,
-                           ctx->stream);
-    if (e != hipSuccess) return hip_fail(ctx, e, "launch nt_call_kernel<global>");
+    const uint32_t ww = nt_dev_wave_words(single, nh, np, max_nw);
+    const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((waves_needed + 3) / 4, (uint64_t)ctx->cu_count * 2));
+    if ((e = ctx->scratch.ensure(grid * 4 * (uint64_t)ww * 4)) != hipSuccess) return hip_fail(ctx, e, "hipMalloc(scratch)");
+    e = nt_dev_launch(ctx->prog_dev, (const uint32_t*)ctx->thr.p, &B, &O, (uint32_t)len_cap, 0xFFFFFFFFu, single, 0, 0,
+                      ww, max_nw, (uint32_t*)ctx->scratch.p, (int)grid, ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e, "launch nt_kernel<global>");
   }
   return NT_OK;
 }
