@@ -121,8 +121,8 @@ def main():
 
     def step():
         nt.scan_call_device(planes.data_ptr(), blk_off.data_ptr(), lens.data_ptr(), win_off.data_ptr(),
-                            n, L, start.data_ptr(), end.data_ptr(), dens.data_ptr(), flags.data_ptr(),
-                            win_counts=wc.data_ptr())
+                            n, n * nw, L, start.data_ptr(), end.data_ptr(), dens.data_ptr(),
+                            flags.data_ptr(), wc.data_ptr())
 
     for _ in range(args.warmup):
         step()

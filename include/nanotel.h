@@ -85,6 +85,7 @@ typedef struct {
   const uint32_t* exc_pos;
   const uint8_t* exc_code;
   uint64_t n_reads;
+  uint64_t n_windows;       /* sum of split_telo window counts (win_counts has n_windows*n_pass) */
 } nt_batch;
 
 /* Device-resident outputs (device pointers). */

@@ -41,6 +41,12 @@ struct NtPat {
   // v_bfi_b32 and no decode
   uint32_t tm_scan[NT_MAX_TVR_M][4];
   uint32_t tm_eq[NT_MAX_TVR_M][4];
+  // one-hot fast path (every letter a single base under the scan semantics):
+  // letter j matches base (l,h) iff ((L ^ xl[j]) & (H ^ xh[j])) is set, with
+  // xl = l ? 0 : ~0, xh = h ? 0 : ~0 -- two ops (v_xor + v_bitop3) per letter
+  int32_t onehot;
+  uint32_t xl[NT_MAX_TVR_M];
+  uint32_t xh[NT_MAX_TVR_M];
 };
 
 struct NtProgram {

@@ -18,10 +18,11 @@
 
 extern "C" {
 uint32_t nt_dev_wave_words(int single, int n_hits, int np, uint32_t nw_cap);
+uint64_t nt_dev_tmask_words(uint64_t total_windows, uint64_t n_reads, int np);
 hipError_t nt_dev_launch(const NtProgram* prog, const uint32_t* thr, const NtBatch* B,
-                         const NtOut* O, uint32_t len_lo, uint32_t len_hi, int single, int m6,
-                         int lds, uint32_t wave_words, uint32_t nw_cap, uint32_t* gscr, int grid,
-                         hipStream_t stream);
+                         const NtOut* O, uint64_t* tmask, uint32_t len_lo, uint32_t len_hi,
+                         int single, int fast6, int lds, uint32_t wave_words, uint32_t* gscr,
+                         int grid, int call_grid, hipStream_t stream);
 hipError_t nt_dev_set_lds_limit(uint32_t bytes);
 hipError_t nt_dev_launch_synth(const NtSynth* S, uint32_t* planes, uint64_t n_reads,
                                hipStream_t stream);
@@ -183,7 +184,7 @@ struct nt_ctx {
   NtProgram* prog_dev = nullptr;
   int cu_count = 256;
   DevBuf planes, blk_off, len, win_off, exc_off, exc_pos, exc_code;
-  DevBuf wc, start, end, dens, flags, hits, scratch, scratch2, thr;
+  DevBuf wc, start, end, dens, flags, hits, scratch, tmask, thr;
 };
 
 static int fail(nt_ctx* ctx, int code, const std::string& msg) {
@@ -326,6 +327,14 @@ int nt_compile(nt_ctx* ctx, const nt_params* prm, nt_program_info* info) {
         X.tm_scan[j][b] = ((X.tt_scan[j] >> b) & 1u) ? 0xFFFFFFFFu : 0u;
         X.tm_eq[j][b] = ((X.tt_eq[j] >> b) & 1u) ? 0xFFFFFFFFu : 0u;
       }
+    X.onehot = 1;
+    for (int j = 0; j < X.m; ++j) {
+      const uint32_t t = X.tt_scan[j];
+      if (t != 1 && t != 2 && t != 4 && t != 8) { X.onehot = 0; continue; }
+      const uint32_t c = t == 1 ? 0 : t == 2 ? 1 : t == 4 ? 2 : 3;  // base code l + 2h
+      X.xl[j] = (c & 1u) ? 0u : 0xFFFFFFFFu;
+      X.xh[j] = (c & 2u) ? 0u : 0xFFFFFFFFu;
+    }
   }
   (void)hipSetDevice(ctx->device);
   hipError_t e = hipMemcpy(ctx->prog_dev, &P, sizeof P, hipMemcpyHostToDevice);
@@ -454,9 +463,10 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
     return fail(ctx, NT_E_ARG, "win_counts/start/end/density/flags outputs are required");
   if (max_len > (1ull << 30)) return fail(ctx, NT_E_LIMIT, "read longer than 2^30 bases");
   (void)hipSetDevice(ctx->device);
-  const int np = ctx->prog.n_pass, L = ctx->prog.L, nh = ctx->prog.n_hits;
-  const int single = (ctx->prog.n_pat == 1 && ctx->prog.n_tvr == 0 && np == 2) ? 1 : 0;
-  const int m6 = (single && ctx->prog.pat[0].m == 6) ? 1 : 0;
+  const NtProgram& P = ctx->prog;
+  const int np = P.n_pass, L = P.L, nh = P.n_hits;
+  const int single = (P.n_pat == 1 && P.n_tvr == 0 && np == 2) ? 1 : 0;
+  const int fast6 = (single && P.pat[0].m == 6 && P.pat[0].onehot) ? 1 : 0;
   NtBatch B{batch->planes, batch->blk_off, batch->len, batch->win_off,
             batch->exc_off, batch->exc_pos, batch->exc_code, batch->n_reads};
   NtOut O{out->win_counts, out->start, out->end, out->density, out->flags, out->hits};
@@ -465,7 +475,10 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
     if ((e = nt_dev_set_lds_limit(kLdsCapBytes)) != hipSuccess) return hip_fail(ctx, e, "hipFuncSetAttribute");
     ctx->lds_limit_set = true;
   }
-  // per-wave scratch (window counters + bitmasks) lives in LDS up to the cap
+  const uint64_t tmw = nt_dev_tmask_words(batch->n_windows, batch->n_reads, np);
+  if ((e = ctx->tmask.ensure(tmw * 8)) != hipSuccess) return hip_fail(ctx, e, "hipMalloc(tmask)");
+  uint64_t* tmask = (uint64_t*)ctx->tmask.p;
+  // per-wave window counters live in LDS up to the cap, in global scratch beyond
   const uint32_t max_nw = (uint32_t)window_count((int64_t)max_len, L);
   auto wg_bytes = [&](uint32_t nwc) { return (uint64_t)nt_dev_wave_words(single, nh, np, nwc) * 4u * 4u; };
   uint32_t cap_nw = max_nw;
@@ -484,23 +497,25 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
     }
     len_cap = a;
   }
-  const uint64_t waves_needed = batch->n_reads;
+  const uint64_t call_grid = std::max<uint64_t>(1, std::min<uint64_t>((batch->n_reads + 255) / 256,
+                                                                      (uint64_t)ctx->cu_count * 64));
+  const bool two = len_cap < max_len;
   {
     const uint32_t ww = nt_dev_wave_words(single, nh, np, cap_nw);
-    const uint64_t per_wg = (uint64_t)ww * 16u;
-    const uint64_t bpc = std::min<uint64_t>(8, std::max<uint64_t>(1, (160u * 1024u) / std::max<uint64_t>(per_wg, 1)));
-    const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((waves_needed + 3) / 4, (uint64_t)ctx->cu_count * bpc));
-    e = nt_dev_launch(ctx->prog_dev, (const uint32_t*)ctx->thr.p, &B, &O, 0u, (uint32_t)len_cap, single, m6, 1, ww,
-                      cap_nw, nullptr, (int)grid, ctx->stream);
-    if (e != hipSuccess) return hip_fail(ctx, e, "launch nt_kernel<lds>");
+    const uint64_t per_wg = std::max<uint64_t>((uint64_t)ww * 16u, 1);
+    const uint64_t bpc = std::min<uint64_t>(8, std::max<uint64_t>(1, (160u * 1024u) / per_wg));
+    const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((batch->n_reads + 3) / 4, (uint64_t)ctx->cu_count * bpc));
+    e = nt_dev_launch(ctx->prog_dev, (const uint32_t*)ctx->thr.p, &B, &O, tmask, 0u, (uint32_t)len_cap,
+                      single, fast6, 1, ww, nullptr, (int)grid, two ? 0 : (int)call_grid, ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e, "launch nt_scan_kernel<lds>");
   }
-  if (len_cap < max_len) {
+  if (two) {
     const uint32_t ww = nt_dev_wave_words(single, nh, np, max_nw);
-    const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((waves_needed + 3) / 4, (uint64_t)ctx->cu_count * 2));
+    const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((batch->n_reads + 3) / 4, (uint64_t)ctx->cu_count * 2));
     if ((e = ctx->scratch.ensure(grid * 4 * (uint64_t)ww * 4)) != hipSuccess) return hip_fail(ctx, e, "hipMalloc(scratch)");
-    e = nt_dev_launch(ctx->prog_dev, (const uint32_t*)ctx->thr.p, &B, &O, (uint32_t)len_cap, 0xFFFFFFFFu, single, 0, 0,
-                      ww, max_nw, (uint32_t*)ctx->scratch.p, (int)grid, ctx->stream);
-    if (e != hipSuccess) return hip_fail(ctx, e, "launch nt_kernel<global>");
+    e = nt_dev_launch(ctx->prog_dev, (const uint32_t*)ctx->thr.p, &B, &O, tmask, (uint32_t)len_cap, 0xFFFFFFFFu,
+                      single, 0, 0, ww, (uint32_t*)ctx->scratch.p, (int)grid, (int)call_grid, ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e, "launch nt_scan_kernel<global>");
   }
   return NT_OK;
 }
@@ -559,7 +574,7 @@ int nt_analyze_host(nt_ctx* ctx, const char* const* seqs, const uint64_t* lens, 
              (const uint32_t*)ctx->len.p, (const uint64_t*)ctx->win_off.p,
              te ? (const uint32_t*)ctx->exc_off.p : nullptr,
              te ? (const uint32_t*)ctx->exc_pos.p : nullptr,
-             te ? (const uint8_t*)ctx->exc_code.p : nullptr, n_reads};
+             te ? (const uint8_t*)ctx->exc_code.p : nullptr, n_reads, tw};
   nt_out O{(uint16_t*)ctx->wc.p, (int32_t*)ctx->start.p, (int32_t*)ctx->end.p,
            (double*)ctx->dens.p, (uint8_t*)ctx->flags.p, hits ? (uint32_t*)ctx->hits.p : nullptr};
   rc = nt_scan_call(ctx, &B, &O, ml);

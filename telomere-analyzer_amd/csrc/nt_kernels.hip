@@ -1,28 +1,26 @@
 // nt_kernels.hip -- NanoTel hot path on MI355X (gfx950 / CDNA4).
 //
-// One fused kernel, one wave per read (grid-stride over reads):
+// Two kernels per batch:
 //
-//  scan  (HBM-bound): each lane owns one 32-base word of the read; the wave
-//     streams the read's 2-bit planes (coalesced 8-byte loads, a 2-deep
-//     prefetch ring), runs the bit-sliced matchPattern of every pattern at
-//     the 32 starts of each word (exact and <=1 mismatch in one pass,
-//     Biostrings' out-of-bound rule), builds coverage = OR of shifted hit
-//     words (trim + IRanges::reduce) and accumulates covered bases per
-//     subseq_length window with LDS atomics (analyze_subtelos /
-//     get_sub_density, NanoTel.R:717-766, 449-468).  Window counts (uint16)
-//     and matchPattern hit counts go to HBM.
+//  nt_scan_kernel  -- HBM-bound, one wave per read (grid-stride).  Each lane
+//     owns one 32-base word; the wave streams the read's 2-bit planes with
+//     coalesced 8-byte loads through a prefetch ring, runs the bit-sliced
+//     matchPattern of every pattern at the 32 starts of each word (exact and
+//     <=1 mismatch in one pass, Biostrings' out-of-bound rule), builds the
+//     coverage = OR of shifted hit words (trim + IRanges::reduce) and adds
+//     covered bases per subseq_length window with LDS atomics
+//     (analyze_subtelos / get_sub_density, NanoTel.R:717-766, 449-468).
+//     Writes the uint16 window counts, the telomeric-window bitmask of every
+//     pass (class -5, NanoTel.R:749-758) and the matchPattern hit counts.
 //
-//  call  (latency-bound, no HBM traffic beyond L2/MALL re-reads): the same
-//     wave calls the telomere of every pass from the LDS window counts:
-//     telomeric-window bitmask by ballot, find_telo_position / _wraper run
-//     scans with fp64 sums in R's order, get_accurate_start/end,
-//     find_left/right_telo, search_left/right_patterns (NanoTel.R:973-1155,
-//     1692-1764, 843-959, 496-697) and the row densities.  Coverage near the
-//     boundaries is recomputed from the planes ("regions").  While a wave
-//     calls, the other waves of its CU keep streaming, so the calling latency
-//     hides behind the scan.
+//  nt_call_kernel  -- one LANE per read.  The telomere calling of
+//     find_telo_position_wraper and callees (NanoTel.R:973-1155, 1692-1764,
+//     843-959, 496-697) and analyze_read's row (NanoTel.R:1840-1974) from the
+//     window bitmasks and counts; coverage near the called boundaries is
+//     recomputed from the planes.  Sequential per read (fp64 sums in R's
+//     order) but 64 reads per wave, so its instruction cost is amortised 64x.
 //
-// No MFMA: integer/bit work bound by HBM bandwidth.
+// No MFMA: integer / bit work bound by HBM bandwidth.
 #include <hip/hip_runtime.h>
 
 #include "nt_common.h"
@@ -30,8 +28,6 @@
 #include "nt_rng.h"
 
 namespace nt {
-
-__device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
 
 // floor(p / L), 0 <= p < 2^31 (multiply-shift, exact; see nt_compile)
 __device__ __forceinline__ int div_l(const NtProgram* prog, int p) {
@@ -45,27 +41,48 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// First uint64 of read r's telomeric bitmasks (pass p at + p * nmw):
+// tm_off(r) = (win_off[r] >> 6) + r never overlaps read r+1's block.
+__device__ __forceinline__ uint64_t tm_base(uint64_t win_off, uint64_t r, int np) {
+  return ((win_off >> 6) + r) * (uint64_t)np;
+}
+
 // ================================================================= scan
 
-// Hits of one pattern at this lane's 32 starts: exact a0, <=1 mismatch a1.
-template <bool kValid, int kM = 0>
+// Hits of one pattern at this lane's 32 starts (exact a0, <=1 mismatch a1).
+// kOne: one-hot letters (2 VALU ops per letter); kM: compile-time length.
+template <bool kValid, bool kOne, int kM>
 __device__ __forceinline__ void word_hits(const ReadCtx& rc, const NtPat& P, int base, uint2 b0,
                                           uint2 b1, uint32_t V0, uint32_t V1, uint32_t& a0,
                                           uint32_t& a1) {
-  hits32<kValid, kM>(b0.x, b1.x, b0.y, b1.y, V0, V1, P.tm_scan, P.m, a0, a1);
+  if (kOne) {
+    uint32_t x0 = 0xFFFFFFFFu, x1 = 0xFFFFFFFFu;
+#pragma unroll
+    for (int j = 0; j < kM; ++j) {
+      const uint32_t Ls = funnel(b1.x, b0.x, (uint32_t)j);
+      const uint32_t Hs = funnel(b1.y, b0.y, (uint32_t)j);
+      uint32_t q = (Ls ^ P.xl[j]) & (Hs ^ P.xh[j]);
+      if (kValid) q &= funnel(V1, V0, (uint32_t)j);
+      x1 = (x1 & q) | x0;
+      x0 &= q;
+    }
+    a0 = x0;
+    a1 = x1;
+  } else {
+    hits32<kValid, kM>(b0.x, b1.x, b0.y, b1.y, V0, V1, P.tm_scan, P.m, a0, a1);
+  }
   if (kValid && P.m <= 1) a1 &= V0;
   if (rc.n_exc) patch_exceptions(rc, base, 0, rc.n - 1, P, false, a0, a1);
 }
 
-// Add coverage popcounts of this lane's word (positions [p0, p0+31]) to the
-// window counters of up to three passes; window k = min(p / L, nw - 1)
+// Add the coverage popcounts of this lane's word (positions [p0, p0+31]) to
+// the window counters of up to three passes; window k = min(p / L, nw - 1)
 // (split_telo's last window absorbs the tail).
 __device__ __forceinline__ void windows_add(const NtProgram* prog, uint32_t* cnt, int nw, int np,
                                             int L, int p0, uint32_t c0, uint32_t c1, uint32_t c2) {
   if (!(c0 | c1 | c2)) return;
   const int k0 = min(div_l(prog, p0), nw - 1), k1 = min(div_l(prog, p0 + 31), nw - 1);
-  if (L >= 32 || k0 == k1) {
-    // at most two windows
+  if (L >= 32 || k0 == k1) {  // at most two windows
     const uint32_t lom = k0 == k1 ? 0xFFFFFFFFu : ((1u << (uint32_t)((k0 + 1) * L - p0)) - 1u);
     const uint32_t cv[3] = {c0, c1, c2};
 #pragma unroll
@@ -97,7 +114,7 @@ __device__ __forceinline__ void windows_add(const NtProgram* prog, uint32_t* cnt
 // lanes 1..63 get their carry-in hit starts by a lane shift.  b1: this lane's
 // block w (prefetched); carry: block c0-2 (lane 62's block of the previous
 // chunk) for lane 0.
-template <bool kSingle, bool kValid, int kM>
+template <bool kSingle, bool kValid, bool kOne, int kM>
 __device__ __forceinline__ void scan_chunk(const NtProgram* __restrict__ prog, const ReadCtx& rc,
                                            int c0, int lane, int np, int nw, uint2 b1, uint2 carry,
                                            uint32_t* cnt, uint32_t* hitacc, uint32_t& acc0,
@@ -120,7 +137,7 @@ __device__ __forceinline__ void scan_chunk(const NtProgram* __restrict__ prog, c
   for (int p = 0; p < n_pat; ++p) {
     const NtPat& P = prog->pat[p];
     uint32_t a0, a1;
-    word_hits<kValid, kM>(rc, P, base, b0, b1, V0, V1, a0, a1);
+    word_hits<kValid, kOne, kM>(rc, P, base, b0, b1, V0, V1, a0, a1);
     if (kSingle) {
       if (owned) {
         acc0 += __builtin_popcount(a0);
@@ -138,9 +155,9 @@ __device__ __forceinline__ void scan_chunk(const NtProgram* __restrict__ prog, c
     for (int t = 0; t < prog->n_tvr; ++t) {
       const NtPat& P = prog->tvr[t];
       uint32_t a0, a1;
-      word_hits<kValid>(rc, P, base, b0, b1, V0, V1, a0, a1);
+      word_hits<kValid, false, 0>(rc, P, base, b0, b1, V0, V1, a0, a1);
       if (owned && a0) atomicAdd(&hitacc[(2 * n_pat + t) * kWave + lane], (uint32_t)__builtin_popcount(a0));
-      cv2 |= spread(a0, __shfl_up(a0, 1, kWave), P.m);
+      cv2 |= spread<0>(a0, __shfl_up(a0, 1, kWave), P.m);
     }
   }
   if (owned && w >= 1 && nw > 0) {
@@ -153,25 +170,103 @@ __device__ __forceinline__ void scan_chunk(const NtProgram* __restrict__ prog, c
   }
 }
 
-template <bool kSingle, int kM>
-__device__ __forceinline__ void scan_read(const NtProgram* __restrict__ prog, const ReadCtx& rc,
-                                          int lane, int np, int nw, uint32_t* cnt,
-                                          uint32_t* hitacc, uint32_t& acc0, uint32_t& acc1) {
-  const int n = (int)rc.n, nblk = rc.nblk;
-  // 2-deep prefetch ring of this lane's block for the next chunks
-  uint2 nx1 = load_blk_nc(rc, 0 + lane - 1), nx2 = load_blk_nc(rc, kOwned + lane - 1);
-  uint2 carry = make_uint2(0u, 0u);
-  for (int c0 = 0; c0 <= nblk; c0 += kOwned) {
-    const uint2 b1 = nx1;
-    nx1 = nx2;
-    nx2 = load_blk_nc(rc, c0 + 2 * kOwned + lane - 1);
-    // interior chunk: every lane's positions [base, base+63] inside the read
-    if (c0 >= 2 && 32 * c0 + 32 * kWave <= n)
-      scan_chunk<kSingle, false, kM>(prog, rc, c0, lane, np, nw, b1, carry, cnt, hitacc, acc0, acc1);
-    else
-      scan_chunk<kSingle, true, kM>(prog, rc, c0, lane, np, nw, b1, carry, cnt, hitacc, acc0, acc1);
-    carry.x = __shfl(b1.x, kOwned - 1, kWave);
-    carry.y = __shfl(b1.y, kOwned - 1, kWave);
+// LDS (kLds) or global scratch per wave: [n_hits][64] hit accumulators
+// (generic programs only), then the window counters [pass][window] (uint32).
+template <bool kSingle, bool kLds, bool kOne, int kM>
+__global__ void __launch_bounds__(kWG)
+nt_scan_kernel(const NtProgram* __restrict__ prog, const uint32_t* __restrict__ thr, NtBatch B,
+               NtOut O, uint64_t* __restrict__ tmask, uint32_t len_lo, uint32_t len_hi,
+               uint32_t wave_words, uint32_t* __restrict__ gscr) {
+  extern __shared__ uint32_t smem[];
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x >> 6;
+  const uint64_t gw = (uint64_t)blockIdx.x * kNWaves + wave, GW = (uint64_t)gridDim.x * kNWaves;
+  const int np = prog->n_pass, nh = prog->n_hits, L = prog->L;
+  uint32_t* wmem = kLds ? smem + (uint64_t)wave * wave_words : gscr + gw * wave_words;
+  uint32_t* hitacc = wmem;
+  uint32_t* cnt = wmem + (kSingle ? 0 : nh * kWave);
+  const int tsz = (int)prog->thr_size;
+  const uint32_t thr_full = thr[L < tsz ? L : tsz - 1];
+
+  for (uint64_t r = gw; r < B.n_reads; r += GW) {
+    const uint32_t n32 = B.len[r];
+    if (n32 <= len_lo || n32 > len_hi) continue;
+    ReadCtx rc;
+    rc.n = n32;
+    rc.nblk = (int32_t)((n32 + 31u) >> 5);
+    rc.blk = reinterpret_cast<const uint2*>(B.planes) + B.blk_off[r];
+    rc.n_exc = 0;
+    rc.exc_pos = nullptr;
+    rc.exc_code = nullptr;
+    if (B.exc_off) {
+      const uint32_t e0 = B.exc_off[r], e1 = B.exc_off[r + 1];
+      rc.n_exc = (int32_t)(e1 - e0);
+      rc.exc_pos = B.exc_pos + e0;
+      rc.exc_code = B.exc_code + e0;
+    }
+    const int n = (int)n32, nblk = rc.nblk;
+    const int nw = (int)split_window_count(n, L);
+    const int ncnt = nw * np;
+    for (int i = lane; i < ncnt; i += kWave) cnt[i] = 0u;
+    if (!kSingle)
+      for (int c = 0; c < nh; ++c) hitacc[c * kWave + lane] = 0u;
+    wave_sync();
+
+    // ------------------------------------------------------------ scan
+    uint32_t acc0 = 0u, acc1 = 0u;
+    {
+      // 2-deep prefetch ring of this lane's block for the next chunks
+      uint2 nx1 = load_blk_nc(rc, lane - 1), nx2 = load_blk_nc(rc, kOwned + lane - 1);
+      uint2 carry = make_uint2(0u, 0u);
+      for (int c0 = 0; c0 <= nblk; c0 += kOwned) {
+        const uint2 b1 = nx1;
+        nx1 = nx2;
+        nx2 = load_blk_nc(rc, c0 + 2 * kOwned + lane - 1);
+        // interior chunk: every lane's positions [base, base+63] inside the read
+        if (c0 >= 2 && 32 * c0 + 32 * kWave <= n)
+          scan_chunk<kSingle, false, kOne, kM>(prog, rc, c0, lane, np, nw, b1, carry, cnt, hitacc, acc0, acc1);
+        else
+          scan_chunk<kSingle, true, kOne, kM>(prog, rc, c0, lane, np, nw, b1, carry, cnt, hitacc, acc0, acc1);
+        carry.x = __shfl(b1.x, kOwned - 1, kWave);
+        carry.y = __shfl(b1.y, kOwned - 1, kWave);
+      }
+    }
+    wave_sync();
+
+    // ------------------------------------------------ window outputs
+    uint16_t* wout = O.win_counts + B.win_off[r] * np;
+    for (int i = lane; i < ncnt; i += kWave) wout[i] = (uint16_t)cnt[i];
+    // telomeric window (class -5) iff !(count / width < min_density) iff
+    // count >= thr[width] (exact, host-computed); the last window may be wider
+    uint32_t thr_last = thr_full;
+    if (nw > 0) {
+      const int wl = n - (nw - 1) * L;
+      thr_last = thr[wl < tsz ? wl : tsz - 1];
+    }
+    const int nmw = (nw + 63) >> 6;
+    uint64_t* tmo = tmask + tm_base(B.win_off[r], r, np);
+    for (int p = 0; p < np; ++p) {
+      for (int ch = 0; ch < nmw; ++ch) {
+        const int i = ch * 64 + lane;
+        const bool t = i < nw && cnt[p * nw + i] >= (i == nw - 1 ? thr_last : thr_full);
+        const uint64_t bal = __ballot(t);
+        if (lane == 0) tmo[p * nmw + ch] = bal;
+      }
+    }
+    if (O.hits) {
+      if (kSingle) {
+        const uint32_t h0 = wave_sum_u32(acc0), h1 = wave_sum_u32(acc1);
+        if (lane == 0) {
+          O.hits[r * (uint64_t)nh] = h0;
+          O.hits[r * (uint64_t)nh + 1] = h1;
+        }
+      } else {
+        for (int c = 0; c < nh; ++c) {
+          const uint32_t v = wave_sum_u32(hitacc[c * kWave + lane]);
+          if (lane == 0) O.hits[r * (uint64_t)nh + c] = v;
+        }
+      }
+    }
+    wave_sync();
   }
 }
 
@@ -181,51 +276,32 @@ struct Pos {
   int s, e;
 };
 
-// A "region": coverage of 63*32 = 2016 consecutive positions [P0, P0+2015]
-// recomputed from the planes, one 32-bit word per lane (lanes 1..63).  S/E:
-// range-start / range-end marks of the pass's range set (run starts / ends of
-// the reduced coverage, or raw view starts / ends for P1 with a single fixed
-// pattern, NanoTel.R:349-355).
-struct Region {
-  int P0;
-  uint32_t cov, S, E;
-};
-
-constexpr int kRegionSpan = 32 * kOwned;
-constexpr int kNoRegion = INT_MIN;
-
-struct CallCtx {
+// Per-lane state of one read-pass.
+struct Lane {
   ReadCtx rc;
   const NtProgram* prog;
-  const uint32_t* cnt;  // this pass's window counts
-  const uint64_t* tm;   // telomeric window bitmask
-  int n, nw, nmw;
-  int L;
+  const uint16_t* cnt;   // this pass's window counts
+  const uint64_t* tm;    // this pass's telomeric-window bitmask
+  int n, nw, nmw, L;
   int k;         // 0 for P1, 1 for P2/P3
   bool use_tvr;  // P3
-  bool raw;      // P1 raw views
-  int lane;
-  Region R0, R1;  // two-entry region cache
-  int lru;
+  bool raw;      // P1 raw views (single fixed pattern, NanoTel.R:349-355)
 };
 
-__device__ __forceinline__ int wstart(const CallCtx& c, int i) { return 1 + i * c.L; }
-__device__ __forceinline__ int wend(const CallCtx& c, int i) { return i == c.nw - 1 ? c.n : wstart(c, i) + c.L - 1; }
-__device__ __forceinline__ int wcount(const CallCtx& c, int i) { return uni((int)c.cnt[i]); }
-__device__ __forceinline__ double wdens(const CallCtx& c, int i) {
+__device__ __forceinline__ int wstart(const Lane& c, int i) { return 1 + i * c.L; }
+__device__ __forceinline__ int wend(const Lane& c, int i) { return i == c.nw - 1 ? c.n : wstart(c, i) + c.L - 1; }
+__device__ __forceinline__ int wcount(const Lane& c, int i) { return c.cnt[i]; }
+__device__ __forceinline__ double wdens(const Lane& c, int i) {
   return (double)wcount(c, i) / (double)(wend(c, i) - wstart(c, i) + 1);
 }
 
-// --------------------------------------------------------- window bitmask
-
-__device__ __forceinline__ uint64_t tword(const CallCtx& c, int wi, bool inv) {
+__device__ __forceinline__ uint64_t tword(const Lane& c, int wi, bool inv) {
   const uint64_t x = c.tm[wi];
-  const uint64_t u = ((uint64_t)(uint32_t)uni((int)(uint32_t)(x >> 32)) << 32) | (uint32_t)uni((int)(uint32_t)x);
-  return inv ? ~u : u;
+  return inv ? ~x : x;
 }
-__device__ __forceinline__ bool tbit(const CallCtx& c, int i) { return (tword(c, i >> 6, false) >> (i & 63)) & 1ull; }
+__device__ __forceinline__ bool tbit(const Lane& c, int i) { return (c.tm[i >> 6] >> (i & 63)) & 1ull; }
 
-__device__ __forceinline__ int next_set(const CallCtx& c, int pos, bool inv) {
+__device__ int next_set(const Lane& c, int pos, bool inv) {
   if (pos >= c.nw) return c.nw;
   int wi = pos >> 6;
   uint64_t x = tword(c, wi, inv) & (~0ull << (pos & 63));
@@ -239,7 +315,7 @@ __device__ __forceinline__ int next_set(const CallCtx& c, int pos, bool inv) {
   }
 }
 
-__device__ __forceinline__ int prev_set(const CallCtx& c, int pos, bool inv) {
+__device__ int prev_set(const Lane& c, int pos, bool inv) {
   if (pos < 0) return -1;
   if (pos >= c.nw) pos = c.nw - 1;
   int wi = pos >> 6;
@@ -252,149 +328,99 @@ __device__ __forceinline__ int prev_set(const CallCtx& c, int pos, bool inv) {
   }
 }
 
-// ---------------------------------------------------------------- regions
+// ------------------------------------------------- coverage from the planes
 
-__device__ __forceinline__ Region make_region(const CallCtx& c, int P0) {
-  const ReadCtx& rc = c.rc;
-  const int q = P0 + 32 * (c.lane - 1);  // this lane's 32 positions / starts
+// Coverage bits of positions [q, q+31] of this pass (0 outside the read):
+// OR over the pass's patterns of the trimmed views starting in [q-31, q+31].
+__device__ uint32_t cov32(const Lane& c, int q) {
   const NtProgram* prog = c.prog;
-  uint32_t cov = 0u, raw = 0u;
-  for (int p = 0; p < prog->n_pat; ++p) {
-    const NtPat& P = prog->pat[p];
-    uint32_t a0, a1;
-    hits_at(rc, P, false, q, 0, rc.n - 1, a0, a1);
-    const uint32_t h = c.k ? a1 : a0;
-    if (p == 0) raw = a0;
-    cov |= spread(h, __shfl_up(h, 1, kWave), P.m);
+  uint32_t cov = 0u;
+  const int npt = prog->n_pat + (c.use_tvr ? prog->n_tvr : 0);
+  for (int i = 0; i < npt; ++i) {
+    const bool is_tvr = i >= prog->n_pat;
+    const NtPat& P = is_tvr ? prog->tvr[i - prog->n_pat] : prog->pat[i];
+    uint32_t p0, p1, c0w, c1w;
+    hits_at(c.rc, P, false, (int64_t)q - 32, 0, c.n - 1, p0, p1);
+    hits_at(c.rc, P, false, q, 0, c.n - 1, c0w, c1w);
+    const bool use_a1 = !is_tvr && c.k;
+    cov |= spread<0>(use_a1 ? c1w : c0w, use_a1 ? p1 : p0, P.m);
   }
-  if (c.use_tvr) {
-    for (int t = 0; t < prog->n_tvr; ++t) {
-      const NtPat& P = prog->tvr[t];
-      uint32_t a0, a1;
-      hits_at(rc, P, false, q, 0, rc.n - 1, a0, a1);
-      cov |= spread(a0, __shfl_up(a0, 1, kWave), P.m);
-    }
-  }
-  cov &= range_mask(q, 0, rc.n - 1);
-  const uint32_t cprev = __shfl_up(cov, 1, kWave), cnext = __shfl_down(cov, 1, kWave);
-  const uint32_t rprev = __shfl_up(raw, 1, kWave);
-  Region R;
-  R.P0 = P0;
-  R.cov = cov;
-  if (c.raw) {
-    // raw views of pattern 0: starts = hit starts, ends = starts + m - 1
-    const int m = prog->pat[0].m;
-    R.S = raw;
-    R.E = m > 1 ? funnel(raw, rprev, (uint32_t)(33 - m)) : raw;
-  } else {
-    R.S = cov & ~((cov << 1) | (cprev >> 31));
-    R.E = cov & ~((cov >> 1) | (cnext << 31));
-  }
-  if (c.lane == 0) R.cov = R.S = R.E = 0u;  // helper lane
-  return R;
+  return cov & range_mask(q, 0, c.n - 1);
 }
 
-// A cached region containing [x, y] (y - x < kRegionSpan - 64).
-__device__ __forceinline__ Region region_for(CallCtx& c, int x, int y) {
-  if (c.R0.P0 != kNoRegion && x >= c.R0.P0 && y <= c.R0.P0 + kRegionSpan - 1) {
-    c.lru = 1;
-    return c.R0;
-  }
-  if (c.R1.P0 != kNoRegion && x >= c.R1.P0 && y <= c.R1.P0 + kRegionSpan - 1) {
-    c.lru = 0;
-    return c.R1;
-  }
-  // new region: x sits ~1/4 into it (32-aligned so lanes load whole blocks)
-  int P0 = x - (kRegionSpan / 4);
-  P0 = (P0 >> 5) << 5;
-  if (y > P0 + kRegionSpan - 1) P0 = (x >> 5) << 5;
-  const Region R = make_region(c, P0);
-  if (c.lru == 0) { c.R0 = R; c.lru = 1; }
-  else { c.R1 = R; c.lru = 0; }
-  return R;
-}
-
-// |coverage ∩ [x, y]| for 0-based positions, any span (region-sized pieces).
-__device__ __forceinline__ int region_count(CallCtx& c, int x, int y) {
+// |coverage ∩ [x, y]| (0-based positions)
+__device__ int cov_count(const Lane& c, int x, int y) {
   int tot = 0;
-  while (x <= y) {
-    const int y2 = (y - x > kRegionSpan - 128) ? x + kRegionSpan - 129 : y;
-    const Region R = region_for(c, x, y2);
-    const int q = R.P0 + 32 * (c.lane - 1);
-    const uint32_t w = c.lane ? (R.cov & range_mask(q, x, y2)) : 0u;
-    tot += (int)wave_sum_u32((uint32_t)__builtin_popcount(w));
-    x = y2 + 1;
-  }
-  return uni(tot);
-}
-
-// sum of window counts k in [ka, kb]
-__device__ __forceinline__ int count_sum(const CallCtx& c, int ka, int kb) {
-  uint32_t acc = 0;
-  for (int i = ka + c.lane; i <= kb; i += kWave) acc += c.cnt[i];
-  return uni((int)wave_sum_u32(acc));
+  for (int q = x; q <= y; q += 32) tot += __builtin_popcount(cov32(c, q) & range_mask(q, x, y));
+  return tot;
 }
 
 // sum(width(intersect(IRanges(a1, b1), ranges))): window counts for whole
 // windows, recomputed coverage for the partial windows at the two ends.
-__device__ __forceinline__ int range_count(CallCtx& c, int a1, int b1) {
+__device__ int range_count(const Lane& c, int a1, int b1) {
   const int a = (a1 < 1 ? 1 : a1) - 1, b = (b1 > c.n ? c.n : b1) - 1;
   if (a > b) return 0;
-  if (c.nw == 0) return region_count(c, a, b);
+  if (c.nw == 0) return cov_count(c, a, b);
   const int L = c.L;
   const int ka = min(div_l(c.prog, a), c.nw - 1), kb = min(div_l(c.prog, b), c.nw - 1);
   const int ws_a = ka * L, we_b = kb == c.nw - 1 ? c.n - 1 : (kb + 1) * L - 1;
-  if (ka == kb) {
-    if (a == ws_a && b == we_b) return wcount(c, ka);
-    return region_count(c, a, b);
-  }
+  if (ka == kb) return (a == ws_a && b == we_b) ? wcount(c, ka) : cov_count(c, a, b);
   const int we_a = (ka + 1) * L - 1, ws_b = kb * L;
-  int tot = a == ws_a ? wcount(c, ka) : region_count(c, a, we_a);
-  if (kb > ka + 1) tot += count_sum(c, ka + 1, kb - 1);
-  tot += b == we_b ? wcount(c, kb) : region_count(c, ws_b, b);
+  int tot = a == ws_a ? wcount(c, ka) : cov_count(c, a, we_a);
+  for (int k = ka + 1; k < kb; ++k) tot += wcount(c, k);
+  tot += b == we_b ? wcount(c, kb) : cov_count(c, ws_b, b);
   return tot;
 }
 
-__device__ __forceinline__ double sub_density(CallCtx& c, int s, int e) {
+__device__ __forceinline__ double sub_density(const Lane& c, int s, int e) {
   return (double)range_count(c, s, e) / (double)(e - s + 1);
 }
 
-// min(start(ranges)) with start in [a1, b1] (span <= 100); fallback if none.
-__device__ __forceinline__ int min_start_in(CallCtx& c, int a1, int b1, int fallback) {
+// Range-start (kind 0) / range-end (kind 1) marks of the pass's range set at
+// positions [q, q+31]: run starts / ends of the reduced coverage, or the raw
+// view starts / ends of P1's single fixed pattern.
+__device__ uint32_t marks32(const Lane& c, int q, int kind) {
+  if (c.raw) {
+    const NtPat& P = c.prog->pat[0];
+    uint32_t a0, a1;
+    hits_at(c.rc, P, false, kind == 0 ? q : (int64_t)q - (P.m - 1), 0, c.n - 1, a0, a1);
+    return a0;
+  }
+  const uint32_t cur = cov32(c, q);
+  if (!cur) return 0u;
+  if (kind == 0) return cur & ~((cur << 1) | (cov32(c, q - 32) >> 31));
+  return cur & ~((cur >> 1) | (cov32(c, q + 32) << 31));
+}
+
+// min(start(ranges)) with start in [a1, b1]; fallback if none.
+__device__ int min_start_in(const Lane& c, int a1, int b1, int fallback) {
+  int a = a1 - 1, b = b1 - 1;
+  if (a < 0) a = 0;
+  if (b > c.n - 1) b = c.n - 1;
+  for (int q = a; q <= b; q += 32) {
+    const uint32_t m = marks32(c, q, 0) & range_mask(q, a, b);
+    if (m) return q + __builtin_ctz(m) + 1;
+  }
+  return fallback;
+}
+
+// max(end(ranges)) with end in [a1, b1]; fallback if none.
+__device__ int max_end_in(const Lane& c, int a1, int b1, int fallback) {
   int a = a1 - 1, b = b1 - 1;
   if (a < 0) a = 0;
   if (b > c.n - 1) b = c.n - 1;
   if (a > b) return fallback;
-  const Region R = region_for(c, a, b);
-  const int q = R.P0 + 32 * (c.lane - 1);
-  const uint32_t w = c.lane ? (R.S & range_mask(q, a, b)) : 0u;
-  const uint64_t bal = __ballot(w != 0u);
-  if (!bal) return fallback;
-  const int l = __builtin_ctzll(bal);
-  const uint32_t wl = (uint32_t)uni((int)__shfl(w, l, kWave));
-  return R.P0 + 32 * (l - 1) + __builtin_ctz(wl) + 1;
+  for (int q = b - 31; q + 31 >= a; q -= 32) {
+    const uint32_t m = marks32(c, q, 1) & range_mask(q, a, b);
+    if (m) return q + (31 - __builtin_clz(m)) + 1;
+  }
+  return fallback;
 }
 
-// max(end(ranges)) with end in [a1, b1] (span <= 100); fallback if none.
-__device__ __forceinline__ int max_end_in(CallCtx& c, int a1, int b1, int fallback) {
-  int a = a1 - 1, b = b1 - 1;
-  if (a < 0) a = 0;
-  if (b > c.n - 1) b = c.n - 1;
-  if (a > b) return fallback;
-  const Region R = region_for(c, a, b);
-  const int q = R.P0 + 32 * (c.lane - 1);
-  const uint32_t w = c.lane ? (R.E & range_mask(q, a, b)) : 0u;
-  const uint64_t bal = __ballot(w != 0u);
-  if (!bal) return fallback;
-  const int l = 63 - __builtin_clzll(bal);
-  const uint32_t wl = (uint32_t)uni((int)__shfl(w, l, kWave));
-  return R.P0 + 32 * (l - 1) + (31 - __builtin_clz(wl)) + 1;
-}
-
-// -------------------------------------------------------- A8 / A11
+// ---------------------------------------------------------------- A8 / A11
 
 // find_telo_position (NanoTel.R:973-1077) on the window bitmask.
-__device__ __forceinline__ Pos find_telo_position(const CallCtx& c, int min_in_a_row, double thr) {
+__device__ Pos find_telo_position(const Lane& c, int min_in_a_row, double thr) {
   int pos = 0, found = -1, start = -1;
   for (;;) {
     const int r = next_set(c, pos, false);
@@ -447,7 +473,7 @@ __device__ __forceinline__ Pos find_telo_position(const CallCtx& c, int min_in_a
 }
 
 // find_left_telo (NanoTel.R:906-959)
-__device__ __forceinline__ Pos find_left_telo(const CallCtx& c) {
+__device__ Pos find_left_telo(const Lane& c) {
   if (c.nw == 0) return Pos{1, 1};
   const int f = next_set(c, 0, false);
   if (f < c.nw && wstart(c, f) <= 200) return Pos{wstart(c, f), wend(c, next_set(c, f, true) - 1)};
@@ -456,7 +482,7 @@ __device__ __forceinline__ Pos find_left_telo(const CallCtx& c) {
 }
 
 // find_right_telo (NanoTel.R:843-899).  err=true on a 0-row table.
-__device__ __forceinline__ Pos find_right_telo(const CallCtx& c, bool& err) {
+__device__ Pos find_right_telo(const Lane& c, bool& err) {
   if (c.nw == 0) { err = true; return Pos{1, 1}; }
   const int g = prev_set(c, c.nw - 1, false);
   if (g >= 0) {
@@ -470,7 +496,7 @@ __device__ __forceinline__ Pos find_right_telo(const CallCtx& c, bool& err) {
 // ------------------------------------------------------------------ A10
 
 // get_accurate_start (NanoTel.R:1726-1764)
-__device__ __forceinline__ int accurate_start(CallCtx& c, int s) {
+__device__ int accurate_start(const Lane& c, int s) {
   if (s == -1) return -1;
   const double first_50 = (double)range_count(c, s, s + 49) / 50.0;
   int t = s;
@@ -485,7 +511,7 @@ __device__ __forceinline__ int accurate_start(CallCtx& c, int s) {
 }
 
 // get_accurate_end (NanoTel.R:1692-1721)
-__device__ __forceinline__ int accurate_end(CallCtx& c, int e) {
+__device__ int accurate_end(const Lane& c, int e) {
   if (e == -1) return -1;
   const int t = max_end_in(c, e - 99, e, e);
   return max_end_in(c, e + 1, e + 50, t);
@@ -493,68 +519,66 @@ __device__ __forceinline__ int accurate_end(CallCtx& c, int e) {
 
 // ------------------------------------------------------------------ A12
 
-// The four steps of search_right_patterns / search_left_patterns
-// (NanoTel.R:576-697: width 18, step 10) evaluated in parallel: lane
-// 16*step + q matches pattern q (patterns, then TVRs) against step `step`'s
-// sub-sequence with fixed=TRUE, out-of-bound positions counted relative to the
-// sub-sequence (multi_pattern_step_*, NanoTel.R:496-575); the steps are then
-// consumed in order, stopping at the first step without a match.
-__device__ __forceinline__ int search_edge(const CallCtx& c, int index, bool right) {
+// max end (right) / min start (left) of the fixed=TRUE matches of the pass's
+// pattern set in the sub-sequence [a1, b1], out-of-bound relative to the
+// sub-sequence (multi_pattern_step_right/left, NanoTel.R:496-575).
+__device__ bool step_extreme(const Lane& c, int a1, int b1, bool right, int& val) {
   const NtProgram* prog = c.prog;
-  const int npt = prog->n_pat + (c.use_tvr ? prog->n_tvr : 0);
+  const int A = a1 - 1, Bz = b1 - 1, base = A - 1;
   const bool only_exact = c.use_tvr && c.k == 0;
-  const int step = c.lane >> 4, q = c.lane & 15;
-  int sa = 1, sb = 1;
-  uint32_t more_mask = 0u;
-  if (right) {
-    int se = index + 18 < c.n ? index + 18 : c.n;
-    for (int i = 0; i < 4; ++i) {
-      if (i == step) { sa = se - 17 > 1 ? se - 17 : 1; sb = se; }
-      const int ne = se + 11 < c.n ? se + 11 : c.n;
-      if (ne != se) more_mask |= 1u << i;
-      se = ne;
-    }
-  } else {
-    int ss = index - 18 > 1 ? index - 18 : 1;
-    for (int i = 0; i < 4; ++i) {
-      if (i == step) { sa = ss; sb = ss + 17 < c.n ? ss + 17 : c.n; }
-      const int ns = ss - 9 > 1 ? ss - 9 : 1;
-      if (ns != ss) more_mask |= 1u << i;
-      ss = ns;
-    }
-  }
-  bool found = false;
-  int val = right ? INT_MIN : INT_MAX;
-  if (q < npt) {
-    const bool is_tvr = q >= prog->n_pat;
-    const NtPat& P = is_tvr ? prog->tvr[q - prog->n_pat] : prog->pat[q];
+  const int npt = prog->n_pat + (c.use_tvr ? prog->n_tvr : 0);
+  bool any = false;
+  int best = right ? INT_MIN : INT_MAX;
+  for (int i = 0; i < npt; ++i) {
+    const bool is_tvr = i >= prog->n_pat;
+    const NtPat& P = is_tvr ? prog->tvr[i - prog->n_pat] : prog->pat[i];
     const int k = (is_tvr || only_exact) ? 0 : c.k;
-    const int A = sa - 1, Bz = sb - 1, base = A - 1;
     uint32_t a0, a1w;
     hits_at(c.rc, P, true, base, A, Bz, a0, a1w);
     const uint32_t h = k ? a1w : a0;
-    if (h) {
-      found = true;
-      val = right ? base + (31 - __builtin_clz(h)) + P.m : base + __builtin_ctz(h) + 1;
-    }
+    if (!h) continue;
+    any = true;
+    if (right) best = max(best, base + (31 - __builtin_clz(h)) + P.m);
+    else best = min(best, base + __builtin_ctz(h) + 1);
   }
-  for (int o = 8; o > 0; o >>= 1) {  // reduce over the patterns of each step
-    const int other = __shfl_xor(val, o, 16);
-    val = right ? (other > val ? other : val) : (other < val ? other : val);
+  if (any) val = best;
+  return any;
+}
+
+// search_right_patterns (NanoTel.R:635-697): width 18, step 10, 4 steps
+__device__ int search_right(const Lane& c, int end_index) {
+  int subseq_end = min(end_index + 18, c.n);
+  int new_end = end_index;
+  for (int it = 0; it < 4; ++it) {
+    const int curr_start = max(subseq_end - 17, 1);
+    int v;
+    if (!step_extreme(c, curr_start, subseq_end, true, v)) break;
+    new_end = v;
+    const int ne = min(subseq_end + 11, c.n);
+    if (ne == subseq_end) break;
+    subseq_end = ne;
   }
-  const uint64_t fb = __ballot(found);
-  int result = index;
-  for (int i = 0; i < 4; ++i) {
-    if (!((fb >> (16 * i)) & 0xFFFFull)) break;
-    result = uni(__shfl(val, 16 * i, kWave));
-    if (!((more_mask >> i) & 1u)) break;
+  return new_end;
+}
+
+// search_left_patterns (NanoTel.R:576-633)
+__device__ int search_left(const Lane& c, int start_index) {
+  int subseq_start = max(start_index - 18, 1);
+  int new_start = start_index;
+  for (int it = 0; it < 4; ++it) {
+    const int curr_end = min(subseq_start + 17, c.n);
+    int v;
+    if (!step_extreme(c, subseq_start, curr_end, false, v)) break;
+    new_start = v;
+    const int ns = max(subseq_start - 9, 1);
+    if (ns == subseq_start) break;
+    subseq_start = ns;
   }
-  return result;
+  return new_start;
 }
 
 // find_telo_position_wraper (NanoTel.R:1080-1155) + density (NanoTel.R:1840).
-__device__ __forceinline__ void call_pass(CallCtx& c, int& out_s, int& out_e, double& out_d,
-                                          uint32_t& err) {
+__device__ void call_pass(const Lane& c, int& out_s, int& out_e, double& out_d, uint32_t& err) {
   Pos tp = find_telo_position(c, 3, 2.0);
   const double telo_density = sub_density(c, tp.s, tp.e);
   const int num_rows = (tp.e - tp.s + 1) / c.L;
@@ -578,8 +602,8 @@ __device__ __forceinline__ void call_pass(CallCtx& c, int& out_s, int& out_e, do
   }
   if (!c.prog->legacy_no_ext) {
     int e2 = tp.e, s2 = tp.s;
-    if (tp.e < c.n) e2 = search_edge(c, tp.e + 1, true);
-    if (tp.s > 1) s2 = search_edge(c, tp.s - 1, false);
+    if (tp.e < c.n) e2 = search_right(c, tp.e + 1);
+    if (tp.s > 1) s2 = search_left(c, tp.s - 1);
     tp = Pos{s2, e2};
   }
   if (tp.e < tp.s - 1) { err |= NT_FLAG_ERR_WIDTH; out_s = -1; out_e = -1; out_d = 0.0; return; }
@@ -588,138 +612,60 @@ __device__ __forceinline__ void call_pass(CallCtx& c, int& out_s, int& out_e, do
   out_d = sub_density(c, tp.s, tp.e);
 }
 
-// ============================================================== the kernel
-
-// Per-wave scratch: [n_hits][64] hit accumulators (generic programs), the
-// window counters [pass][window] (uint32) and the telomeric bitmasks
-// [pass][nmw] (uint64).  kLds: in LDS; otherwise in a global scratch slice
-// (reads too long for the LDS budget).
-template <bool kSingle, bool kLds, int kM>
-__global__ void __launch_bounds__(kWG)
-nt_kernel(const NtProgram* __restrict__ prog, const uint32_t* __restrict__ thr, NtBatch B, NtOut O,
-          uint32_t len_lo, uint32_t len_hi, uint32_t wave_words, uint32_t nw_cap,
-          uint32_t* __restrict__ gscr) {
-  extern __shared__ uint32_t smem[];
-  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x >> 6;
-  const uint64_t gw = (uint64_t)blockIdx.x * kNWaves + wave, GW = (uint64_t)gridDim.x * kNWaves;
-  const int np = prog->n_pass, nh = prog->n_hits, L = prog->L;
-  uint32_t* wmem = kLds ? smem + (uint64_t)wave * wave_words : gscr + gw * wave_words;
-  uint32_t* hitacc = wmem;
-  uint32_t* cnt = wmem + (kSingle ? 0 : nh * kWave);
-  uint64_t* tm = reinterpret_cast<uint64_t*>(cnt + ((np * nw_cap + 1) & ~1u));
-  const int nmw_cap = (int)((nw_cap + 63) / 64);
-
-  for (uint64_t r = gw; r < B.n_reads; r += GW) {
+// One lane per read (grid-stride over reads).
+__global__ void __launch_bounds__(256)
+nt_call_kernel(const NtProgram* __restrict__ prog, NtBatch B, NtOut O,
+               const uint64_t* __restrict__ tmask) {
+  const int np = prog->n_pass, L = prog->L;
+  for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < B.n_reads;
+       r += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t n32 = B.len[r];
-    if (n32 <= len_lo || n32 > len_hi) continue;
-    ReadCtx rc;
-    rc.n = n32;
-    rc.nblk = (int32_t)((n32 + 31u) >> 5);
-    rc.blk = reinterpret_cast<const uint2*>(B.planes) + B.blk_off[r];
-    rc.n_exc = 0;
-    rc.exc_pos = nullptr;
-    rc.exc_code = nullptr;
+    Lane c;
+    c.rc.n = n32;
+    c.rc.nblk = (int32_t)((n32 + 31u) >> 5);
+    c.rc.blk = reinterpret_cast<const uint2*>(B.planes) + B.blk_off[r];
+    c.rc.n_exc = 0;
+    c.rc.exc_pos = nullptr;
+    c.rc.exc_code = nullptr;
     if (B.exc_off) {
       const uint32_t e0 = B.exc_off[r], e1 = B.exc_off[r + 1];
-      rc.n_exc = (int32_t)(e1 - e0);
-      rc.exc_pos = B.exc_pos + e0;
-      rc.exc_code = B.exc_code + e0;
+      c.rc.n_exc = (int32_t)(e1 - e0);
+      c.rc.exc_pos = B.exc_pos + e0;
+      c.rc.exc_code = B.exc_code + e0;
     }
-    const int n = (int)n32;
-    const int nw = (int)split_window_count(n, L);
-    const int ncnt = nw * np;
-    for (int i = lane; i < ncnt; i += kWave) cnt[i] = 0u;
-    if (!kSingle)
-      for (int cix = 0; cix < nh; ++cix) hitacc[cix * kWave + lane] = 0u;
-    wave_sync();
-
-    // ---------------------------------------------------------- scan
-    uint32_t acc0 = 0u, acc1 = 0u;
-    scan_read<kSingle, kM>(prog, rc, lane, np, nw, cnt, hitacc, acc0, acc1);
-    wave_sync();
-
-    uint16_t* wout = O.win_counts + B.win_off[r] * np;
-    for (int i = lane; i < ncnt; i += kWave) wout[i] = (uint16_t)cnt[i];
-    if (O.hits) {
-      if (kSingle) {
-        const uint32_t h0 = wave_sum_u32(acc0), h1 = wave_sum_u32(acc1);
-        if (lane == 0) {
-          O.hits[r * (uint64_t)nh] = h0;
-          O.hits[r * (uint64_t)nh + 1] = h1;
-        }
-      } else {
-        for (int cix = 0; cix < nh; ++cix) {
-          const uint32_t v = wave_sum_u32(hitacc[cix * kWave + lane]);
-          if (lane == 0) O.hits[r * (uint64_t)nh + cix] = v;
-        }
-      }
-    }
-
-    // ---------------------------------------------------------- call
-    const int tsz = (int)prog->thr_size;
-    const uint32_t thr_full = thr[L < tsz ? L : tsz - 1];
-    uint32_t thr_last = thr_full;
-    if (nw > 0) {
-      const int wl = n - (nw - 1) * L;
-      thr_last = thr[wl < tsz ? wl : tsz - 1];
-    }
-    const int nmw = (nw + 63) >> 6;
+    c.prog = prog;
+    c.n = (int)n32;
+    c.L = L;
+    c.nw = (int)split_window_count(c.n, L);
+    c.nmw = (c.nw + 63) >> 6;
+    const uint64_t woff = B.win_off[r];
+    const uint64_t* tmr = tmask + tm_base(woff, r, np);
     int maxw = INT_MIN;
     uint32_t flags = NT_FLAG_DONE;
     for (int p = 0; p < np; ++p) {
-      const uint32_t* pc = cnt + p * nw;
-      uint64_t* ptm = tm + p * nmw_cap;
-      // class -5 ("telomeric") iff !(count/width < min_density) iff count >= thr[width]
-      for (int ch = 0; ch < nmw; ++ch) {
-        const int i = ch * 64 + lane;
-        const bool t = i < nw && pc[i] >= (i == nw - 1 ? thr_last : thr_full);
-        const uint64_t bal = __ballot(t);
-        if (lane == 0) ptm[ch] = bal;
-      }
-      wave_sync();
-      CallCtx c;
-      c.rc = rc;
-      c.prog = prog;
-      c.cnt = pc;
-      c.tm = ptm;
-      c.n = n;
-      c.nw = nw;
-      c.nmw = nmw;
-      c.L = L;
+      c.cnt = O.win_counts + woff * np + (uint64_t)p * c.nw;
+      c.tm = tmr + p * c.nmw;
       c.k = p == 0 ? 0 : 1;
       c.use_tvr = p == 2;
       c.raw = p == 0 && prog->raw_p1;
-      c.lane = lane;
-      c.R0.P0 = kNoRegion;
-      c.R1.P0 = kNoRegion;
-      c.lru = 0;
       int s, e;
       double d;
       uint32_t err = 0;
-#ifndef NT_NO_CALL
       call_pass(c, s, e, d, err);
-#else
-      s = c.nw; e = c.nmw; d = 0.0; asm volatile("" :: "v"(c.tm), "v"(c.cnt));
-#endif
       flags |= err;
       if (s == -1) flags |= 1u << (NT_FLAG_NA_SHIFT + p);
-      if (e - s + 1 > maxw) maxw = e - s + 1;
-      if (lane == 0) {
-        O.start[r * 3 + p] = s;
-        O.end[r * 3 + p] = e;
-        O.density[r * 3 + p] = d;
-      }
+      maxw = max(maxw, e - s + 1);
+      O.start[r * 3 + p] = s;
+      O.end[r * 3 + p] = e;
+      O.density[r * 3 + p] = d;
     }
-    if (lane == 0) {
-      for (int p = np; p < 3; ++p) {
-        O.start[r * 3 + p] = -1;
-        O.end[r * 3 + p] = -1;
-        O.density[r * 3 + p] = 0.0;
-      }
-      if (maxw >= 30) flags |= NT_FLAG_TELOMERIC;
-      O.flags[r] = (uint8_t)flags;
+    for (int p = np; p < 3; ++p) {
+      O.start[r * 3 + p] = -1;
+      O.end[r * 3 + p] = -1;
+      O.density[r * 3 + p] = 0.0;
     }
-    wave_sync();
+    if (maxw >= 30) flags |= NT_FLAG_TELOMERIC;
+    O.flags[r] = (uint8_t)flags;
   }
 }
 
@@ -766,39 +712,53 @@ nt_layout_kernel(uint64_t n_reads, uint64_t nblk, uint64_t read_len, uint64_t nw
 
 extern "C" {
 
-// per-wave scratch words for a read with nw_cap windows
+// per-wave scan scratch words for reads with at most nw_cap windows
 uint32_t nt_dev_wave_words(int single, int n_hits, int np, uint32_t nw_cap) {
-  const uint32_t hit = single ? 0u : (uint32_t)n_hits * 64u;
-  const uint32_t cntw = ((uint32_t)np * nw_cap + 1u) & ~1u;
-  const uint32_t tmw = 2u * (uint32_t)np * ((nw_cap + 63u) / 64u);
-  return hit + cntw + tmw;
+  return (single ? 0u : (uint32_t)n_hits * 64u) + (uint32_t)np * nw_cap;
 }
+
+// uint64 words of the telomeric-bitmask scratch for a batch
+uint64_t nt_dev_tmask_words(uint64_t total_windows, uint64_t n_reads, int np) {
+  return ((total_windows >> 6) + n_reads + 1) * (uint64_t)np;
+}
+
+#define NT_SCAN_VARIANTS(X) \
+  X(true, true, true, 6)    \
+  X(true, true, false, 0)   \
+  X(true, false, false, 0)  \
+  X(false, true, false, 0)  \
+  X(false, false, false, 0)
 
 hipError_t nt_dev_set_lds_limit(uint32_t bytes) {
-  const void* fns[3] = {(const void*)nt::nt_kernel<true, true, 6>, (const void*)nt::nt_kernel<true, true, 0>,
-                        (const void*)nt::nt_kernel<false, true, 0>};
-  for (const void* f : fns) {
-    hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-    if (e != hipSuccess) return e;
-  }
-  return hipSuccess;
+  hipError_t e = hipSuccess;
+#define NT_ATTR(S, G, O, M)                                                                    \
+  if (G && e == hipSuccess)                                                                    \
+    e = hipFuncSetAttribute((const void*)nt::nt_scan_kernel<S, G, O, M>,                       \
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  NT_SCAN_VARIANTS(NT_ATTR)
+#undef NT_ATTR
+  return e;
 }
 
-// single: 1 pattern, no TVR; m6: that pattern has 6 letters (compile-time length)
+// single: 1 pattern, no TVR; fast6: that pattern has 6 one-hot letters
 hipError_t nt_dev_launch(const NtProgram* prog, const uint32_t* thr, const NtBatch* B,
-                         const NtOut* O, uint32_t len_lo, uint32_t len_hi, int single, int m6,
-                         int lds, uint32_t wave_words, uint32_t nw_cap, uint32_t* gscr, int grid,
-                         hipStream_t stream) {
+                         const NtOut* O, uint64_t* tmask, uint32_t len_lo, uint32_t len_hi,
+                         int single, int fast6, int lds, uint32_t wave_words, uint32_t* gscr,
+                         int grid, int call_grid, hipStream_t stream) {
   const size_t lds_bytes = lds ? (size_t)wave_words * 4u * nt::kNWaves : 0;
-#define NT_LAUNCH(S, G, M)                                                                          \
-  hipLaunchKernelGGL((nt::nt_kernel<S, G, M>), dim3(grid), dim3(nt::kWG), lds_bytes, stream, prog, \
-                     thr, *B, *O, len_lo, len_hi, wave_words, nw_cap, gscr)
-  if (single && lds && m6) NT_LAUNCH(true, true, 6);
-  else if (single && lds) NT_LAUNCH(true, true, 0);
-  else if (single) NT_LAUNCH(true, false, 0);
-  else if (lds) NT_LAUNCH(false, true, 0);
-  else NT_LAUNCH(false, false, 0);
+  bool done = false;
+#define NT_LAUNCH(S, G, O_, M)                                                                 \
+  if (!done && single == (int)S && lds == (int)G && fast6 == (int)O_) {                        \
+    hipLaunchKernelGGL((nt::nt_scan_kernel<S, G, O_, M>), dim3(grid), dim3(nt::kWG), lds_bytes, \
+                       stream, prog, thr, *B, *O, tmask, len_lo, len_hi, wave_words, gscr);    \
+    done = true;                                                                               \
+  }
+  NT_SCAN_VARIANTS(NT_LAUNCH)
 #undef NT_LAUNCH
+  if (!done) return hipErrorInvalidValue;
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || call_grid <= 0) return e;
+  hipLaunchKernelGGL(nt::nt_call_kernel, dim3(call_grid), dim3(256), 0, stream, prog, *B, *O, tmask);
   return hipGetLastError();
 }
 

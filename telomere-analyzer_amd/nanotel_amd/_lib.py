@@ -52,7 +52,7 @@ class NtBatch(ctypes.Structure):
     _fields_ = [
         ("planes", ctypes.c_void_p), ("blk_off", ctypes.c_void_p), ("len", ctypes.c_void_p),
         ("win_off", ctypes.c_void_p), ("exc_off", ctypes.c_void_p), ("exc_pos", ctypes.c_void_p),
-        ("exc_code", ctypes.c_void_p), ("n_reads", ctypes.c_uint64),
+        ("exc_code", ctypes.c_void_p), ("n_reads", ctypes.c_uint64), ("n_windows", ctypes.c_uint64),
     ]
 
 

@@ -132,12 +132,13 @@ class NanoTel:
         return res["win_counts"][off:off + nw]
 
     # ------------------------------------------------------------------
-    def scan_call_device(self, planes, blk_off, lengths, win_off, n_reads, max_len, start, end,
-                         density, flags, win_counts=0, hits=0, exc_off=0, exc_pos=0, exc_code=0):
-        """Device-resident hot path: all arguments are device pointers (ints).
-        Asynchronous on the context stream (see set_stream)."""
+    def scan_call_device(self, planes, blk_off, lengths, win_off, n_reads, n_windows, max_len, start,
+                         end, density, flags, win_counts, hits=0, exc_off=0, exc_pos=0, exc_code=0):
+        """Device-resident hot path: all pointer arguments are device pointers
+        (ints); n_windows = sum of window counts.  Asynchronous on the context
+        stream (see set_stream)."""
         B = NtBatch(planes, blk_off, lengths, win_off, exc_off or None, exc_pos or None,
-                    exc_code or None, int(n_reads))
+                    exc_code or None, int(n_reads), int(n_windows))
         O = NtOut(win_counts or None, start, end, density, flags, hits or None)
         _check(lib().nt_scan_call(self._h, ctypes.byref(B), ctypes.byref(O), int(max_len)), self._h)
 
