@@ -80,7 +80,7 @@ def main():
 
     import torch
     import torch.distributed as dist
-    from nanotel_amd import NanoTel, synth_params, window_count
+    from nanotel_amd import NanoTel, read_blocks, synth_params, window_count
 
     cfg = dict(CONFIGS[args.config])
     if args.reads:
@@ -103,7 +103,7 @@ def main():
     torch.cuda.set_stream(stream)
     nt.set_stream(stream.cuda_stream)
     npass = nt.n_pass
-    nblk = (L + 31) // 32
+    nblk = read_blocks(L)  # even block slot per read (16-byte segments)
     nw = window_count(L, 100)
     planes = torch.empty(n * nblk * 2, dtype=torch.int32, device=dev)
     blk_off = torch.empty(n, dtype=torch.int64, device=dev)

@@ -52,6 +52,7 @@ extern "C" {
 /* summary flags per read */
 #define NT_ROW_TELOMERIC 0x01 /* row emitted: max telomere width >= 30 (NanoTel.R:1847) */
 #define NT_ROW_NA(p) (0x02 << (p)) /* pass p start == -1 -> NA columns (NanoTel.R:1926) */
+#define NT_ROW_ERR_ALIGN 0x10 /* blk_off[r] odd: read skipped (layout contract) */
 #define NT_ROW_DONE 0x80
 
 typedef struct nt_ctx nt_ctx;
@@ -75,10 +76,11 @@ typedef struct {
 } nt_program_info;
 
 /* Device-resident read batch (device pointers).  Layout: see DESIGN.md
- * "HBM layout": planes = uint2 {lo,hi} bit planes per 32 bases. */
+ * "HBM layout": planes = uint2 {lo,hi} bit planes per 32 bases; read r owns
+ * nt_read_blocks(len[r]) blocks from the even block index blk_off[r]. */
 typedef struct {
   const uint32_t* planes;
-  const uint64_t* blk_off;  /* [n_reads] first 32-base block of each read */
+  const uint64_t* blk_off;  /* [n_reads] first 32-base block of each read (even) */
   const uint32_t* len;      /* [n_reads] */
   const uint64_t* win_off;  /* [n_reads] prefix sum of split_telo window counts */
   const uint32_t* exc_off;  /* [n_reads+1] or NULL: non-ACGT letters */
@@ -124,6 +126,9 @@ int nt_compile(nt_ctx* ctx, const nt_params* params, nt_program_info* info);
 
 /* --- host packing (A14 reverseComplement fused when params.rc) ----------- */
 int64_t nt_window_count(int64_t n, int32_t subseq_length);
+/* 32-base blocks of a read's slot in the plane buffer: 2*ceil(n/64).  Slots
+ * start at EVEN block offsets (the scan loads 64-base segments, 16 bytes). */
+uint64_t nt_read_blocks(uint64_t n);
 /* Pass 1: sizes.  Returns NT_E_LETTER (and *bad_read) on an invalid letter. */
 int nt_pack_count(const char* const* seqs, const uint64_t* lens, uint64_t n_reads,
                   int32_t subseq_length, uint64_t* total_blocks, uint64_t* total_windows,

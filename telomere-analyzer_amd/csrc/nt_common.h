@@ -3,8 +3,9 @@
 // HBM layout of a read batch ("bit-plane 2-bit packing"):
 //   planes[b] = {lo, hi} (two uint32) for the 32-base block b; bit i of lo/hi is
 //   the low/high bit of the 2-bit code of base 32*b+i (A=0 C=1 G=2 T=3).
-//   Read r occupies blocks [blk_off[r], blk_off[r] + ceil(len[r]/32)); padding
-//   bits past the read end are zero.  Letters other than A/C/G/T (N, IUPAC
+//   Read r occupies the slot of 2*ceil(len[r]/64) blocks starting at the EVEN
+//   block blk_off[r] (the scan loads 64-base segments = 16 bytes); bits past
+//   the read end are don't-care (the kernels mask them).  Letters other than A/C/G/T (N, IUPAC
 //   ambiguity codes, '-', '+', '.') are stored as A in the planes and listed in
 //   a per-read exception list (position, Biostrings DNA code) -- see
 //   DESIGN.md "Exceptions".
@@ -21,6 +22,7 @@
 // Per-read flag bits (rows.flags)
 #define NT_FLAG_TELOMERIC 0x01   // row emitted (max width >= 30), NanoTel.R:1847-1868
 #define NT_FLAG_NA_SHIFT 1       // bit 1+p: pass p start == -1 (NA columns)
+#define NT_FLAG_ERR_ALIGN 0x10   // blk_off[r] odd: segments must be 16-byte aligned
 #define NT_FLAG_ERR_RIGHT 0x20   // find_right_telo on a 0-row window table (R errors)
 #define NT_FLAG_ERR_WIDTH 0x40   // IRanges(start, end) with negative width (R errors)
 #define NT_FLAG_DONE 0x80        // the kernel processed this read

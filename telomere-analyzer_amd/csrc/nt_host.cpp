@@ -21,7 +21,7 @@ uint32_t nt_dev_wave_words(int single, int n_hits, int np, uint32_t nw_cap);
 uint64_t nt_dev_tmask_words(uint64_t total_windows, uint64_t n_reads, int np);
 hipError_t nt_dev_launch(const NtProgram* prog, const uint32_t* thr, const NtBatch* B,
                          const NtOut* O, uint64_t* tmask, uint32_t len_lo, uint32_t len_hi,
-                         int single, int fast6, int lds, uint32_t wave_words, uint32_t* gscr,
+                         int single, int one, int m6, int lds, uint32_t wave_words, uint32_t* gscr,
                          int grid, int call_grid, hipStream_t stream);
 hipError_t nt_dev_set_lds_limit(uint32_t bytes);
 hipError_t nt_dev_launch_synth(const NtSynth* S, uint32_t* planes, uint64_t n_reads,
@@ -95,6 +95,9 @@ int64_t window_count(int64_t n, int L) {
   if ((double)(n - last_start) < (double)L / 2.0) c -= 1;  // NanoTel.R:220
   return c;
 }
+
+// 32-base blocks in a read's slot: whole 64-base segments (16-byte loads)
+inline uint64_t read_blocks(uint64_t n) { return 2 * ((n + 63) / 64); }
 
 template <class F>
 void parallel_for(uint64_t n, F&& f) {
@@ -255,6 +258,8 @@ int nt_synchronize(nt_ctx* ctx) {
 
 int64_t nt_window_count(int64_t n, int32_t subseq_length) { return window_count(n, subseq_length); }
 
+uint64_t nt_read_blocks(uint64_t n) { return read_blocks(n); }
+
 int nt_compile(nt_ctx* ctx, const nt_params* prm, nt_program_info* info) {
   if (!ctx || !prm) return NT_E_ARG;
   if (!prm->patterns) return fail(ctx, NT_E_ARG, "Missing required parameter:  --patterns");
@@ -378,7 +383,7 @@ int nt_pack_count(const char* const* seqs, const uint64_t* lens, uint64_t n_read
       if (bad_read) *bad_read = r;
       return bad[r] == 2 ? NT_E_EMPTY_READ : NT_E_LETTER;
     }
-    tb += (lens[r] + 31) / 32;
+    tb += read_blocks(lens[r]);
     tw += (uint64_t)window_count((int64_t)lens[r], subseq_length);
     te += exc[r];
     ml = std::max(ml, lens[r]);
@@ -402,7 +407,7 @@ int nt_pack_reads(const char* const* seqs, const uint64_t* lens, uint64_t n_read
     blk_off[r] = b;
     win_off[r] = w;
     len[r] = (uint32_t)lens[r];
-    b += (lens[r] + 31) / 32;
+    b += read_blocks(lens[r]);
     w += (uint64_t)window_count((int64_t)lens[r], subseq_length);
   }
   if (exc_off) {
@@ -451,6 +456,10 @@ int nt_pack_reads(const char* const* seqs, const uint64_t* lens, uint64_t n_read
       out[2 * blk] = lo;
       out[2 * blk + 1] = hi;
     }
+    if ((n + 31) / 32 < read_blocks(n)) {  // zero the pad block of the 64-base segment
+      out[2 * ((n + 31) / 32)] = 0u;
+      out[2 * ((n + 31) / 32) + 1] = 0u;
+    }
   });
   return bad.load() ? NT_E_LETTER : NT_OK;
 }
@@ -466,7 +475,8 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
   const NtProgram& P = ctx->prog;
   const int np = P.n_pass, L = P.L, nh = P.n_hits;
   const int single = (P.n_pat == 1 && P.n_tvr == 0 && np == 2) ? 1 : 0;
-  const int fast6 = (single && P.pat[0].m == 6 && P.pat[0].onehot) ? 1 : 0;
+  const int one = (single && P.pat[0].onehot) ? 1 : 0;
+  const int m6 = (single && P.pat[0].m == 6) ? 1 : 0;
   NtBatch B{batch->planes, batch->blk_off, batch->len, batch->win_off,
             batch->exc_off, batch->exc_pos, batch->exc_code, batch->n_reads};
   NtOut O{out->win_counts, out->start, out->end, out->density, out->flags, out->hits};
@@ -506,7 +516,7 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
     const uint64_t bpc = std::min<uint64_t>(8, std::max<uint64_t>(1, (160u * 1024u) / per_wg));
     const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((batch->n_reads + 3) / 4, (uint64_t)ctx->cu_count * bpc));
     e = nt_dev_launch(ctx->prog_dev, (const uint32_t*)ctx->thr.p, &B, &O, tmask, 0u, (uint32_t)len_cap,
-                      single, fast6, 1, ww, nullptr, (int)grid, two ? 0 : (int)call_grid, ctx->stream);
+                      single, one, m6, 1, ww, nullptr, (int)grid, two ? 0 : (int)call_grid, ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, e, "launch nt_scan_kernel<lds>");
   }
   if (two) {
@@ -514,7 +524,7 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
     const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((batch->n_reads + 3) / 4, (uint64_t)ctx->cu_count * 2));
     if ((e = ctx->scratch.ensure(grid * 4 * (uint64_t)ww * 4)) != hipSuccess) return hip_fail(ctx, e, "hipMalloc(scratch)");
     e = nt_dev_launch(ctx->prog_dev, (const uint32_t*)ctx->thr.p, &B, &O, tmask, (uint32_t)len_cap, 0xFFFFFFFFu,
-                      single, 0, 0, ww, (uint32_t*)ctx->scratch.p, (int)grid, (int)call_grid, ctx->stream);
+                      single, 0, 0, 0, ww, (uint32_t*)ctx->scratch.p, (int)grid, (int)call_grid, ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, e, "launch nt_scan_kernel<global>");
   }
   return NT_OK;
@@ -596,6 +606,8 @@ int nt_analyze_host(nt_ctx* ctx, const char* const* seqs, const uint64_t* lens, 
   for (uint64_t r = 0; r < n_reads; ++r) {
     const uint8_t f = h_flags[r];
     if (!(f & NT_FLAG_DONE)) return fail(ctx, NT_E_HIP, "read " + std::to_string(r) + " not processed");
+    if (f & NT_FLAG_ERR_ALIGN)
+      return fail(ctx, NT_E_ARG, "read " + std::to_string(r) + ": blk_off must be even");
     if (f & NT_FLAG_ERR_RIGHT)
       return fail(ctx, NT_E_RIGHT_EMPTY,
                   "read " + std::to_string(r) + ": find_right_telo on a read without windows");
@@ -672,7 +684,7 @@ int nt_uniform_layout_device(nt_ctx* ctx, uint64_t n_reads, uint64_t read_len, i
                              uint64_t* blk_off_dev, uint32_t* len_dev, uint64_t* win_off_dev) {
   if (!ctx || read_len == 0 || read_len > 0xFFFFFFFFull) return NT_E_ARG;
   (void)hipSetDevice(ctx->device);
-  const uint64_t nblk = (read_len + 31) / 32;
+  const uint64_t nblk = read_blocks(read_len);
   const uint64_t nw = (uint64_t)window_count((int64_t)read_len, subseq_length);
   hipError_t e = nt_dev_launch_uniform_layout(n_reads, nblk, read_len, nw, blk_off_dev, len_dev,
                                               win_off_dev, ctx->stream);

@@ -25,6 +25,12 @@ def window_count(n, subseq_length=100):
     return lib().nt_window_count(int(n), int(subseq_length))
 
 
+def read_blocks(n):
+    """32-base blocks of a read's slot in the plane buffer (2*ceil(n/64));
+    slots start at even block offsets (16-byte segments)."""
+    return lib().nt_read_blocks(int(n))
+
+
 class NanoTel:
     """One GPU context + compiled --patterns/--tvr_patterns/flags."""
 

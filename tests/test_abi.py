@@ -98,7 +98,7 @@ def test_pack_reads_layout_and_rc():
     rc = L.nt_pack_count(ctypes.cast(ptrs, ctypes.c_void_p), lens.ctypes.data, n, 100,
                          ctypes.byref(tb), ctypes.byref(tw), ctypes.byref(te), ctypes.byref(ml),
                          ctypes.byref(bad))
-    assert rc == 0 and tb.value == 3 + 1 + 2 and te.value == 13 + 2 and ml.value == 65
+    assert rc == 0 and tb.value == 4 + 2 + 2 and te.value == 13 + 2 and ml.value == 65
     for rcflag in (0, 1):
         planes = np.zeros(2 * tb.value, np.uint32)
         blk = np.zeros(n, np.uint64)
@@ -117,6 +117,7 @@ def test_pack_reads_layout_and_rc():
             if rcflag:
                 ref = O.reverse_complement(ref)
             b0 = int(blk[r])
+            assert b0 % 2 == 0
             out = []
             exc = {int(ep[i]): int(ec[i]) for i in range(eo[r], eo[r + 1])}
             for pos in range(len(s)):

@@ -158,11 +158,12 @@ def test_error_behaviour():
 
 def test_device_synth_matches_host_generator():
     import torch
-    from nanotel_amd import NanoTel, synth_params, synth_read_ascii
+    from nanotel_amd import NanoTel, read_blocks, synth_params, synth_read_ascii
     sp = synth_params(read_len=5000, first_read=123)
     nt = NanoTel(patterns="TTAGGG")
     n = 16
-    nblk = (5000 + 31) // 32
+    nblk = read_blocks(5000)
+    assert nblk == 2 * 79
     planes = torch.zeros(n * nblk * 2, dtype=torch.int32, device="cuda")
     nt.synth_device(sp, n, planes.data_ptr())
     nt.synchronize()
