@@ -1,10 +1,12 @@
 """Throughput of the NanoTel hot path on MI355X (BASELINE.json metric).
 
-One step = one launch of the fused scan+call kernel over a device-resident
-batch of synthetic long reads (generated on the GPU by the counter-based
-generator of nt_rng.h; inputs resident in HBM before the timed region):
-  matchPattern TTAGGG exact + 1-mismatch (OOB rule), coverage, per-window
-  densities for both passes, telomere calling (A8-A12) and summary rows.
+One step = one nt_scan_call over a device-resident batch of synthetic long
+reads (generated on the GPU by the counter-based generator of nt_rng.h; inputs
+resident in HBM before the timed region): the scan kernel (matchPattern TTAGGG
+exact + 1-mismatch with the OOB rule, coverage, per-window counts of both
+passes, telomeric-window bitmasks) then the calling kernel (A8-A13 rows).
+roofline = the scan kernel (the dominant one), timed with HIP events recorded
+by the library on the launch stream around each kernel of every timed step.
 
 N GPUs: one process per GPU (torch.distributed, RCCL), each rank scans its own
 shard of reads (first_read = rank * reads) -> weak scaling, no data-path
@@ -34,12 +36,21 @@ CONFIGS = {
 }
 
 
-def algorithmic_bytes_per_read(read_len, n_pass, n_windows):
-    # planes (2 bits/base, 32-base blocks) + blk_off + len + win_off
-    # + window counts written (uint16 per window per pass)
-    # + row written: start/end int32 x3, density f64 x3, flags u8
-    blocks = (read_len + 31) // 32
-    return blocks * 8 + 8 + 4 + 8 + n_windows * n_pass * 2 + 3 * 4 * 2 + 3 * 8 + 1
+def scan_bytes_per_read(read_len, n_pass, n_windows, n_hits):
+    """Algorithmic HBM bytes of the SCAN kernel per read:
+    reads the 2-bit planes (ceil(n/4) B) + len (4) + blk_off (8) + win_off
+    (8); writes the uint16 window counts per pass, the telomeric-window
+    bitmask per pass (ceil(nw/64) u64) and the hit counters (u32)."""
+    planes = (read_len + 3) // 4
+    return (planes + 4 + 8 + 8 + n_windows * n_pass * 2 + n_pass * 8 * ((n_windows + 63) // 64)
+            + 4 * n_hits)
+
+
+def call_bytes_per_read(n_pass, n_windows):
+    """Algorithmic bytes of the CALLING kernel per read: len/blk_off/win_off,
+    the window bitmasks and counts it walks (upper bound: all of them), and
+    the row written (start/end int32 x3, density f64 x3, flags u8)."""
+    return 4 + 8 + 8 + n_pass * (8 * ((n_windows + 63) // 64) + 2 * n_windows) + 3 * (4 + 4 + 8) + 1
 
 
 def cpu_baseline(cfg, budget_s=12.0, max_reads=10 ** 9):
@@ -127,6 +138,7 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
+    nt.set_profiling(True)  # HIP events around each kernel, on the launch stream
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -142,7 +154,9 @@ def main():
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()
     wall = t1 - t0
-    kern_ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)]
+    step_ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)]
+    n_calls, scan_ms, call_ms = nt.kernel_times()
+    assert n_calls == args.steps
     if world > 1:
         t = torch.tensor([wall], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -151,14 +165,15 @@ def main():
     telo = int(((flags & 1) != 0).sum().item())
     total_bases = n * L * world * args.steps
     value = total_bases / wall / 1e9
-    avg_kern_s = sum(kern_ms) / len(kern_ms) / 1e3
-    bytes_per_launch = n * algorithmic_bytes_per_read(L, npass, nw)
-    achieved = bytes_per_launch / avg_kern_s / 1e9
+    scan_s = scan_ms / n_calls / 1e3
+    nh = nt.n_hits
+    scan_bytes = n * scan_bytes_per_read(L, npass, nw, nh)
+    achieved = scan_bytes / scan_s / 1e9
     traffic = None
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))
-            if tj.get("config") == args.config and tj.get("reads") == n:
+            if tj.get("config") == args.config and tj.get("reads") == n and tj.get("jit") == nt.jit:
                 traffic = tj.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
@@ -184,9 +199,14 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic,
-                         "kernel": "nt_scan_call_kernel<false>",
-                         "kernel_avg_ms": round(avg_kern_s * 1e3, 4),
-                         "algorithmic_bytes_per_launch": bytes_per_launch},
+                         "kernel": ("nt_scan_jit_lds (scan specialised for the patterns, hiprtc)" if nt.jit
+                                    else "nt::nt_scan_kernel (ahead-of-time scan)"),
+                         "kernel_avg_ms": round(scan_s * 1e3, 4),
+                         "algorithmic_bytes_per_launch": scan_bytes,
+                         "call_kernel": "nt::nt_call_kernel",
+                         "call_kernel_avg_ms": round(call_ms / n_calls, 4),
+                         "call_bytes_per_launch": n * call_bytes_per_read(npass, nw),
+                         "step_event_avg_ms": round(sum(step_ms) / len(step_ms), 4)},
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(cfg)

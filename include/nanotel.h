@@ -73,6 +73,8 @@ typedef struct {
   int32_t n_tvr;
   int32_t n_hits; /* hit counters per read: 2*n_pat + n_tvr */
   int32_t raw_p1; /* P1 keeps raw views (single fixed pattern) */
+  int32_t jit;    /* 1: the scan runs as a kernel specialised for these patterns (hiprtc);
+                     0: ahead-of-time kernels (NT_JIT=0 in the environment, or hiprtc failed) */
 } nt_program_info;
 
 /* Device-resident read batch (device pointers).  Layout: see DESIGN.md
@@ -141,6 +143,14 @@ int nt_pack_reads(const char* const* seqs, const uint64_t* lens, uint64_t n_read
 /* --- the hot path --------------------------------------------------------- */
 /* Asynchronous on the context stream.  max_len = longest read of the batch. */
 int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t max_len);
+
+/* Measurement: with profiling on, every nt_scan_call records HIP events on
+ * the context stream around its scan kernel(s) and its calling kernel.
+ * nt_kernel_times waits for them and returns the summed spans of the calls
+ * since the previous nt_kernel_times (or nt_set_profiling); returns the
+ * number of calls, or < 0. */
+int nt_set_profiling(nt_ctx* ctx, int on);
+int64_t nt_kernel_times(nt_ctx* ctx, double* scan_ms, double* call_ms);
 
 /* Host-buffer convenience: pack (+rc), upload, scan+call, download, sync.
  * win_counts/hits optional.  Returns the first per-read error, if any. */

@@ -12,7 +12,9 @@
 // Window counts: uint16 at win_counts[win_off[r]*n_pass + p*nw(r) + i]
 //   (covered bases of window i of pass p; nw = split_telo window count).
 #pragma once
+#ifndef __HIPCC_RTC__
 #include <stdint.h>
+#endif
 
 #define NT_MAX_PAT 8      // unique patterns per list (--patterns / --tvr_patterns)
 #define NT_MAX_M 18       // testit::assert(str_length(pattern) <= 18), NanoTel.R:589,647

@@ -1,8 +1,10 @@
 // nt_device.h -- gfx950 device primitives for the NanoTel scan (bit-sliced
 // matching on 2-bit planes, coverage spreading, exception fix-ups).
 #pragma once
+#ifndef __HIPCC_RTC__  // hiprtc (nt_jit.cpp) provides the HIP device runtime itself
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#endif
 
 #include "nt_common.h"
 

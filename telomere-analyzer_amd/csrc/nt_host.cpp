@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <cmath>
 #include <cstdio>
@@ -24,12 +25,20 @@ hipError_t nt_dev_launch(const NtProgram* prog, const uint32_t* thr, const NtBat
                          int single, int one, int m6, int lds, uint32_t wave_words, uint32_t* gscr,
                          int grid, int call_grid, hipStream_t stream);
 hipError_t nt_dev_set_lds_limit(uint32_t bytes);
+hipError_t nt_dev_launch_call(const NtProgram* prog, const NtBatch* B, const NtOut* O,
+                              const uint64_t* tmask, int call_grid, hipStream_t stream);
 hipError_t nt_dev_launch_synth(const NtSynth* S, uint32_t* planes, uint64_t n_reads,
                                hipStream_t stream);
 hipError_t nt_dev_launch_uniform_layout(uint64_t n_reads, uint64_t nblk, uint64_t read_len,
                                         uint64_t nw, uint64_t* blk_off, uint32_t* len,
                                         uint64_t* win_off, hipStream_t stream);
 }
+
+bool nt_jit_get(int device, const NtProgram& P, void** fn_lds, void** fn_gmem, std::string& err);
+hipError_t nt_jit_launch(void* fn, int grid, size_t lds_bytes, hipStream_t stream,
+                         const NtProgram* prog, const uint32_t* thr, const NtBatch* B,
+                         const NtOut* O, uint64_t* tmask, uint32_t len_lo, uint32_t len_hi,
+                         uint32_t wave_words, uint32_t* gscr);
 
 namespace {
 
@@ -182,6 +191,13 @@ struct nt_ctx {
   std::string err;
   bool compiled = false;
   bool lds_limit_set = false;
+  bool profile = false;  // HIP events around the scan and call kernels of every call
+  std::vector<std::array<hipEvent_t, 3>> ev;
+  size_t n_ev = 0;  // calls recorded since the last nt_kernel_times
+  bool jit = false;  // hiprtc-specialised scan kernels (nt_jit.cpp)
+  void* jit_lds = nullptr;
+  void* jit_gmem = nullptr;
+  std::string jit_err;
   NtProgram prog{};
   nt_params params{};
   NtProgram* prog_dev = nullptr;
@@ -238,6 +254,8 @@ void nt_destroy(nt_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->prog_dev) (void)hipFree(ctx->prog_dev);
+  for (auto& a : ctx->ev)
+    for (hipEvent_t ev : a) (void)hipEventDestroy(ev);
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
   delete ctx;
 }
@@ -350,12 +368,14 @@ int nt_compile(nt_ctx* ctx, const nt_params* prm, nt_program_info* info) {
   ctx->prog = P;
   ctx->params = *prm;
   ctx->compiled = true;
+  ctx->jit = nt_jit_get(ctx->device, P, &ctx->jit_lds, &ctx->jit_gmem, ctx->jit_err);
   if (info) {
     info->n_pass = P.n_pass;
     info->n_pat = P.n_pat;
     info->n_tvr = P.n_tvr;
     info->n_hits = P.n_hits;
     info->raw_p1 = P.raw_p1;
+    info->jit = ctx->jit ? 1 : 0;
   }
   return NT_OK;
 }
@@ -490,7 +510,8 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
   uint64_t* tmask = (uint64_t*)ctx->tmask.p;
   // per-wave window counters live in LDS up to the cap, in global scratch beyond
   const uint32_t max_nw = (uint32_t)window_count((int64_t)max_len, L);
-  auto wg_bytes = [&](uint32_t nwc) { return (uint64_t)nt_dev_wave_words(single, nh, np, nwc) * 4u * 4u; };
+  const int noslots = (single || ctx->jit) ? 1 : 0;  // register hit counters
+  auto wg_bytes = [&](uint32_t nwc) { return (uint64_t)nt_dev_wave_words(noslots, nh, np, nwc) * 4u * 4u; };
   uint32_t cap_nw = max_nw;
   uint64_t len_cap = max_len;
   if (wg_bytes(max_nw) > kLdsCapBytes) {
@@ -510,24 +531,74 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
   const uint64_t call_grid = std::max<uint64_t>(1, std::min<uint64_t>((batch->n_reads + 255) / 256,
                                                                       (uint64_t)ctx->cu_count * 64));
   const bool two = len_cap < max_len;
+  hipEvent_t* ev = nullptr;
+  if (ctx->profile) {
+    if (ctx->n_ev == ctx->ev.size()) {
+      std::array<hipEvent_t, 3> a{};
+      for (hipEvent_t& x : a)
+        if ((e = hipEventCreate(&x)) != hipSuccess) return hip_fail(ctx, e, "hipEventCreate");
+      ctx->ev.push_back(a);
+    }
+    ev = ctx->ev[ctx->n_ev++].data();
+    (void)hipEventRecord(ev[0], ctx->stream);
+  }
   {
-    const uint32_t ww = nt_dev_wave_words(single, nh, np, cap_nw);
+    const uint32_t ww = nt_dev_wave_words(noslots, nh, np, cap_nw);
     const uint64_t per_wg = std::max<uint64_t>((uint64_t)ww * 16u, 1);
     const uint64_t bpc = std::min<uint64_t>(8, std::max<uint64_t>(1, (160u * 1024u) / per_wg));
     const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((batch->n_reads + 3) / 4, (uint64_t)ctx->cu_count * bpc));
-    e = nt_dev_launch(ctx->prog_dev, (const uint32_t*)ctx->thr.p, &B, &O, tmask, 0u, (uint32_t)len_cap,
-                      single, one, m6, 1, ww, nullptr, (int)grid, two ? 0 : (int)call_grid, ctx->stream);
+    if (ctx->jit)
+      e = nt_jit_launch(ctx->jit_lds, (int)grid, (size_t)ww * 4u * 4u, ctx->stream, ctx->prog_dev,
+                        (const uint32_t*)ctx->thr.p, &B, &O, tmask, 0u, (uint32_t)len_cap, ww, nullptr);
+    else
+      e = nt_dev_launch(ctx->prog_dev, (const uint32_t*)ctx->thr.p, &B, &O, tmask, 0u, (uint32_t)len_cap,
+                        single, one, m6, 1, ww, nullptr, (int)grid, 0, ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, e, "launch nt_scan_kernel<lds>");
   }
   if (two) {
-    const uint32_t ww = nt_dev_wave_words(single, nh, np, max_nw);
+    const uint32_t ww = nt_dev_wave_words(noslots, nh, np, max_nw);
     const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((batch->n_reads + 3) / 4, (uint64_t)ctx->cu_count * 2));
     if ((e = ctx->scratch.ensure(grid * 4 * (uint64_t)ww * 4)) != hipSuccess) return hip_fail(ctx, e, "hipMalloc(scratch)");
-    e = nt_dev_launch(ctx->prog_dev, (const uint32_t*)ctx->thr.p, &B, &O, tmask, (uint32_t)len_cap, 0xFFFFFFFFu,
-                      single, 0, 0, 0, ww, (uint32_t*)ctx->scratch.p, (int)grid, (int)call_grid, ctx->stream);
+    if (ctx->jit)
+      e = nt_jit_launch(ctx->jit_gmem, (int)grid, 0, ctx->stream, ctx->prog_dev, (const uint32_t*)ctx->thr.p,
+                        &B, &O, tmask, (uint32_t)len_cap, 0xFFFFFFFFu, ww, (uint32_t*)ctx->scratch.p);
+    else
+      e = nt_dev_launch(ctx->prog_dev, (const uint32_t*)ctx->thr.p, &B, &O, tmask, (uint32_t)len_cap, 0xFFFFFFFFu,
+                        single, 0, 0, 0, ww, (uint32_t*)ctx->scratch.p, (int)grid, 0, ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, e, "launch nt_scan_kernel<global>");
   }
+  if (ev) (void)hipEventRecord(ev[1], ctx->stream);
+  e = nt_dev_launch_call(ctx->prog_dev, &B, &O, tmask, (int)call_grid, ctx->stream);
+  if (e != hipSuccess) return hip_fail(ctx, e, "launch nt_call_kernel");
+  if (ev) (void)hipEventRecord(ev[2], ctx->stream);
   return NT_OK;
+}
+
+int nt_set_profiling(nt_ctx* ctx, int on) {
+  if (!ctx) return NT_E_ARG;
+  ctx->profile = on != 0;
+  ctx->n_ev = 0;
+  return NT_OK;
+}
+
+int64_t nt_kernel_times(nt_ctx* ctx, double* scan_ms, double* call_ms) {
+  if (!ctx || !ctx->profile) return NT_E_STATE;
+  double a = 0.0, b = 0.0;
+  for (size_t i = 0; i < ctx->n_ev; ++i) {
+    hipEvent_t* ev = ctx->ev[i].data();
+    hipError_t e = hipEventSynchronize(ev[2]);
+    if (e != hipSuccess) return hip_fail(ctx, e, "hipEventSynchronize");
+    float x = 0.f, y = 0.f;
+    if ((e = hipEventElapsedTime(&x, ev[0], ev[1])) != hipSuccess) return hip_fail(ctx, e, "hipEventElapsedTime");
+    if ((e = hipEventElapsedTime(&y, ev[1], ev[2])) != hipSuccess) return hip_fail(ctx, e, "hipEventElapsedTime");
+    a += x;
+    b += y;
+  }
+  if (scan_ms) *scan_ms = a;
+  if (call_ms) *call_ms = b;
+  const int64_t n = (int64_t)ctx->n_ev;
+  ctx->n_ev = 0;
+  return n;
 }
 
 int nt_analyze_host(nt_ctx* ctx, const char* const* seqs, const uint64_t* lens, uint64_t n_reads,

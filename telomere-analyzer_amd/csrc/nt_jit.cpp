@@ -1,0 +1,154 @@
+// nt_jit.cpp -- run-time specialisation of the scan kernel (hiprtc).
+//
+// nt_compile() knows the pattern set; the scan's inner loop is dominated by
+// the per-letter tests, so the scan is recompiled for it: every letter
+// becomes a compile-time truth table over the 2-bit base (one v_bitop3 per
+// DISTINCT letter test per word, shared across letters and patterns), the
+// pattern lengths become compile-time (unrolled, 3-letter majority combine),
+// and the hit counters live in registers.  The source is nt_scan.h itself
+// (embedded at build time, nt_jit_src.inc) plus a generated pattern-set type.
+// Code objects are cached per (device, source) for the life of the process.
+// If hiprtc is unavailable the ahead-of-time kernels serve (NT_JIT=0 forces
+// that); nt_program_info.jit reports which one runs.
+#include <hip/hip_runtime.h>
+#include <hip/hiprtc.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "nt_common.h"
+
+namespace {
+
+#include "nt_jit_src.inc"  // kJitCommon, kJitDevice, kJitScan (raw string literals)
+
+struct JitEntry {
+  hipModule_t mod = nullptr;
+  hipFunction_t lds = nullptr, gmem = nullptr;
+  std::string err;
+};
+
+std::mutex g_mu;
+std::map<std::string, JitEntry> g_cache;
+
+std::string pat_type(const NtPat& P) {
+  std::string s = "nt::CtPat<" + std::to_string(P.m);
+  for (int j = 0; j < P.m; ++j) s += ", " + std::to_string((int)P.tt_scan[j]);
+  return s + ">";
+}
+
+std::string jit_source(const NtProgram& P) {
+  std::string pats, tvrs;
+  for (int i = 0; i < P.n_pat; ++i) pats += (i ? ", " : "") + pat_type(P.pat[i]);
+  for (int i = 0; i < P.n_tvr; ++i) tvrs += (i ? ", " : "") + pat_type(P.tvr[i]);
+  std::string s;
+  s += "typedef __hip_internal::uint8_t uint8_t;\n";
+  s += "typedef __hip_internal::uint16_t uint16_t;\n";
+  s += "typedef __hip_internal::uint32_t uint32_t;\n";
+  s += "typedef __hip_internal::uint64_t uint64_t;\n";
+  s += "typedef __hip_internal::int32_t int32_t;\n";
+  s += "typedef __hip_internal::int64_t int64_t;\n";
+  s += "#include \"nt_scan.h\"\n";
+  s += "using JitSet = nt::CtSet<nt::CtList<" + pats + ">, nt::CtList<" + tvrs + ">>;\n";
+  s += R"(
+extern "C" __global__ void __launch_bounds__(256)
+nt_scan_jit_lds(const NtProgram* __restrict__ prog, const uint32_t* __restrict__ thr, NtBatch B,
+                NtOut O, uint64_t* __restrict__ tmask, uint32_t len_lo, uint32_t len_hi,
+                uint32_t wave_words, uint32_t* __restrict__ gscr) {
+  extern __shared__ uint32_t smem[];
+  nt::scan_reads<JitSet, true>(prog, thr, B, O, tmask, len_lo, len_hi,
+                               smem + (threadIdx.x >> 6) * wave_words);
+}
+extern "C" __global__ void __launch_bounds__(256)
+nt_scan_jit_gmem(const NtProgram* __restrict__ prog, const uint32_t* __restrict__ thr, NtBatch B,
+                 NtOut O, uint64_t* __restrict__ tmask, uint32_t len_lo, uint32_t len_hi,
+                 uint32_t wave_words, uint32_t* __restrict__ gscr) {
+  const uint64_t gw = (uint64_t)blockIdx.x * nt::kNWaves + (threadIdx.x >> 6);
+  nt::scan_reads<JitSet, false>(prog, thr, B, O, tmask, len_lo, len_hi, gscr + gw * wave_words);
+}
+)";
+  return s;
+}
+
+bool compile(int device, const std::string& src, JitEntry& e) {
+  hiprtcProgram prog;
+  const char* hdrs[] = {kJitCommon, kJitDevice, kJitScan};
+  const char* names[] = {"nt_common.h", "nt_device.h", "nt_scan.h"};
+  if (hiprtcCreateProgram(&prog, src.c_str(), "nt_scan_jit.hip", 3, hdrs, names) != HIPRTC_SUCCESS) {
+    e.err = "hiprtcCreateProgram failed";
+    return false;
+  }
+  hipDeviceProp_t prop;
+  std::string arch = "--offload-arch=gfx950";
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess) {
+    std::string a = prop.gcnArchName;
+    arch = "--offload-arch=" + a.substr(0, a.find(':'));
+  }
+  const char* opts[] = {arch.c_str(), "-O3", "-std=c++17", "-ffp-contract=off"};
+  const hiprtcResult rc = hiprtcCompileProgram(prog, 4, opts);
+  if (rc != HIPRTC_SUCCESS) {
+    size_t n = 0;
+    hiprtcGetProgramLogSize(prog, &n);
+    std::string log(n + 1, '\0');
+    hiprtcGetProgramLog(prog, &log[0]);
+    e.err = std::string("hiprtc: ") + hiprtcGetErrorString(rc) + "\n" + log.c_str();
+    hiprtcDestroyProgram(&prog);
+    return false;
+  }
+  size_t n = 0;
+  hiprtcGetCodeSize(prog, &n);
+  std::vector<char> code(n);
+  hiprtcGetCode(prog, code.data());
+  hiprtcDestroyProgram(&prog);
+  hipError_t he = hipModuleLoadData(&e.mod, code.data());
+  if (he == hipSuccess) he = hipModuleGetFunction(&e.lds, e.mod, "nt_scan_jit_lds");
+  if (he == hipSuccess) he = hipModuleGetFunction(&e.gmem, e.mod, "nt_scan_jit_gmem");
+  if (he != hipSuccess) {
+    e.err = std::string("hipModuleLoadData: ") + hipGetErrorString(he);
+    return false;
+  }
+  return true;
+}
+
+}  // namespace
+
+// Returns true with the two kernels of the program's pattern set, false (and
+// a message) when specialisation is off or failed.
+bool nt_jit_get(int device, const NtProgram& P, void** fn_lds, void** fn_gmem, std::string& err) {
+  const char* env = std::getenv("NT_JIT");
+  if (env && env[0] == '0') {
+    err = "NT_JIT=0";
+    return false;
+  }
+  const std::string src = jit_source(P);
+  const std::string key = std::to_string(device) + "\n" + src;
+  std::lock_guard<std::mutex> lk(g_mu);
+  auto it = g_cache.find(key);
+  if (it == g_cache.end()) {
+    JitEntry e;
+    compile(device, src, e);
+    it = g_cache.emplace(key, e).first;
+  }
+  if (!it->second.lds) {
+    err = it->second.err;
+    return false;
+  }
+  *fn_lds = (void*)it->second.lds;
+  *fn_gmem = (void*)it->second.gmem;
+  return true;
+}
+
+hipError_t nt_jit_launch(void* fn, int grid, size_t lds_bytes, hipStream_t stream,
+                         const NtProgram* prog, const uint32_t* thr, const NtBatch* B,
+                         const NtOut* O, uint64_t* tmask, uint32_t len_lo, uint32_t len_hi,
+                         uint32_t wave_words, uint32_t* gscr) {
+  NtBatch b = *B;
+  NtOut o = *O;
+  void* args[] = {&prog, &thr, &b, &o, &tmask, &len_lo, &len_hi, &wave_words, &gscr};
+  return hipModuleLaunchKernel((hipFunction_t)fn, (unsigned)grid, 1, 1, 256, 1, 1,
+                               (unsigned)lds_bytes, stream, args, nullptr);
+}

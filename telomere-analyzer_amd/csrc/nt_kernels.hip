@@ -26,441 +26,23 @@
 #include "nt_common.h"
 #include "nt_device.h"
 #include "nt_rng.h"
+#include "nt_scan.h"
 
 namespace nt {
 
-// floor(p / L), 0 <= p < 2^31 (multiply-shift, exact; see nt_compile)
-struct DivL {
-  uint32_t m, s;
-};
-__device__ __forceinline__ int div_l(DivL d, int p) {
-  if (d.m == 0u) return p;  // L == 1
-  return (int)(__umulhi((uint32_t)p, d.m) >> d.s);
-}
-__device__ __forceinline__ int div_l(const NtProgram* prog, int p) {
-  return div_l(DivL{prog->div32_m, prog->div32_s}, p);
-}
-
-__device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// First uint64 of read r's telomeric bitmasks (pass p at + p * nmw):
-// tm_off(r) = (win_off[r] >> 6) + r never overlaps read r+1's block.
-__device__ __forceinline__ uint64_t tm_base(uint64_t win_off, uint64_t r, int np) {
-  return ((win_off >> 6) + r) * (uint64_t)np;
-}
-
-// ================================================================= scan
+// ============================================================ scan (AOT)
 //
-// Work split: one wave per read (grid-stride), the read cut into 64-base
-// SEGMENTS (two 32-base words A, B = one 16-byte load of the bit planes).
-// Chunk c of a read covers segments g0 = 63c - 1 ... g0 + 63: lane l holds
-// segment g0 + l; lanes 0..62 OWN theirs, lane 63 only lends its planes to
-// lane 62 (the matches starting in a segment read up to m-1 bases into the
-// next one).  Chunk 0 starts at segment -1 so that Biostrings' out-of-bound
-// start (-1, one mismatch) is an ordinary hit of lane 0's word B.
-//
-// Neighbour data moves with wave-wide DPP (wave_shl:1 / wave_shr:1); the
-// coverage a segment spills into the next one ("overflow") travels right
-// the same way, lane 62's overflow is carried into the next chunk's lane 0.
-// Window counts: the per-lane covered-base counts of passes 0 and 1 are
-// packed into one u32 (16+16 bit), prefix-summed across the wave with DPP
-// row_shr / row_bcast, and the lane holding a window boundary kL stores the
-// running count there (cum[k]); count(window k) = cum[k+1] - cum[k].  No
-// atomics, no zero-fill: every boundary belongs to exactly one owned lane.
-
-constexpr int kDppWaveShl1 = 0x130;  // lane i <- lane i+1
-constexpr int kDppWaveShr1 = 0x138;  // lane i <- lane i-1
-constexpr int kDppRowShr = 0x110;    // + n: row_shr:n
-constexpr int kDppRowBcast15 = 0x142;
-constexpr int kDppRowBcast31 = 0x143;
-
-// lane i <- lane i+1 (lane 63 <- 0)
-__device__ __forceinline__ uint32_t from_next_lane(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kDppWaveShl1, 0xf, 0xf, false);
-}
-// lane i <- lane i-1 (lane 0 <- lane0)
-__device__ __forceinline__ uint32_t from_prev_lane(uint32_t v, uint32_t lane0) {
-  return (uint32_t)__builtin_amdgcn_update_dpp((int)lane0, (int)v, kDppWaveShr1, 0xf, 0xf, false);
-}
-template <int kCtrl, int kRowMask>
-__device__ __forceinline__ uint32_t dpp0(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kCtrl, kRowMask, 0xf, false);
-}
-// inclusive prefix sum over the 64 lanes
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
-  v += dpp0<kDppRowShr + 1, 0xf>(v);
-  v += dpp0<kDppRowShr + 2, 0xf>(v);
-  v += dpp0<kDppRowShr + 4, 0xf>(v);
-  v += dpp0<kDppRowShr + 8, 0xf>(v);
-  v += dpp0<kDppRowBcast15, 0xa>(v);
-  v += dpp0<kDppRowBcast31, 0xc>(v);
-  return v;
-}
-
-__device__ __forceinline__ uint32_t maj3(uint32_t a, uint32_t b, uint32_t c) {
-  return (a & b) | (a & c) | (b & c);  // v_bitop3 0xe8
-}
-
-// Letter j of P against the 32 starts of a word: bit s set iff subject base
-// s+j matches (and is inside the read when kValid).
-template <bool kValid, bool kOne>
-__device__ __forceinline__ uint32_t letter_q(const NtPat& P, int j, uint32_t L0, uint32_t L1,
-                                             uint32_t H0, uint32_t H1, uint32_t V0, uint32_t V1) {
-  const uint32_t Ls = funnel(L1, L0, (uint32_t)j), Hs = funnel(H1, H0, (uint32_t)j);
-  uint32_t q;
-  if (kOne) {
-    q = (Ls ^ P.xl[j]) & (Hs ^ P.xh[j]);
-  } else {
-    const uint32_t* t = P.tm_scan[j];
-    q = bfi(Hs, bfi(Ls, t[3], t[2]), bfi(Ls, t[1], t[0]));
-  }
-  if (kValid) q &= funnel(V1, V0, (uint32_t)j);
-  return q;
-}
-
-// Hits of pattern P at the 32 starts of one word: a0 exact, a1 <= 1 mismatch
-// (matchPattern(max.mismatch = 0 / 1), out-of-read letters are mismatches).
-// kM > 0: letters combined three at a time -- all-3 (and3) and at-least-2-of-3
-// (majority) per group, then a1 = (a1 & all) | (a0 & maj), a0 &= all.
-template <bool kValid, bool kOne, int kM>
-__device__ __forceinline__ void word_hits(const NtPat& P, uint32_t L0, uint32_t L1, uint32_t H0,
-                                          uint32_t H1, uint32_t V0, uint32_t V1, uint32_t& a0,
-                                          uint32_t& a1) {
-  if constexpr (kM > 0) {
-    uint32_t q[kM];
-#pragma unroll
-    for (int j = 0; j < kM; ++j) q[j] = letter_q<kValid, kOne>(P, j, L0, L1, H0, H1, V0, V1);
-    uint32_t x0, x1;
-    int j;
-    if constexpr (kM >= 3) {
-      x0 = q[0] & q[1] & q[2];
-      x1 = maj3(q[0], q[1], q[2]);
-      j = 3;
-    } else if constexpr (kM == 2) {
-      x0 = q[0] & q[1];
-      x1 = q[0] | q[1];
-      j = 2;
-    } else {
-      x0 = q[0];
-      x1 = 0xFFFFFFFFu;
-      j = 1;
-    }
-#pragma unroll
-    for (; j + 3 <= kM; j += 3) {
-      const uint32_t all = q[j] & q[j + 1] & q[j + 2], two = maj3(q[j], q[j + 1], q[j + 2]);
-      x1 = (x1 & all) | (x0 & two);
-      x0 &= all;
-    }
-    if constexpr (kM >= 3 && kM % 3 == 2) {
-      const uint32_t all = q[kM - 2] & q[kM - 1], one = q[kM - 2] | q[kM - 1];
-      x1 = (x1 & all) | (x0 & one);
-      x0 &= all;
-    } else if constexpr (kM >= 3 && kM % 3 == 1) {
-      x1 = (x1 & q[kM - 1]) | x0;
-      x0 &= q[kM - 1];
-    }
-    a0 = x0;
-    a1 = x1;
-  } else {
-    uint32_t x0 = 0xFFFFFFFFu, x1 = 0xFFFFFFFFu;
-    for (int j = 0; j < P.m; ++j) {
-      const uint32_t q = letter_q<kValid, kOne>(P, j, L0, L1, H0, H1, V0, V1);
-      x1 = (x1 & q) | x0;
-      x0 &= q;
-    }
-    a0 = x0;
-    a1 = x1;
-  }
-  if (kValid && P.m <= 1) a1 &= V0;  // m <= k: no out-of-bound starts
-}
-
-// OR into (cA, cB, ov) the coverage of hit starts hA (word A) and hB (word
-// B): bit i covered iff a start in [i-m+1, i] (trim + IRanges::reduce).
-// ov = coverage spilling into the next segment's word A.  kM > 0: span
-// doubling on the 96-bit value (ov:B:A).
-template <int kM>
-__device__ __forceinline__ void seg_spread(uint32_t hA, uint32_t hB, int m, uint32_t& cA,
-                                           uint32_t& cB, uint32_t& ov) {
-  if constexpr (kM > 0) {
-    uint32_t w0 = hA, w1 = hB, w2 = 0u;
-#pragma unroll
-    for (int s = 1; s < kM;) {
-      const int t = 2 * s <= kM ? s : kM - s;
-      w2 |= funnel(w2, w1, (uint32_t)(32 - t));
-      w1 |= funnel(w1, w0, (uint32_t)(32 - t));
-      w0 |= w0 << t;
-      s += t;
-    }
-    cA |= w0;
-    cB |= w1;
-    ov |= w2;
-  } else {
-    cA |= hA;
-    cB |= hB;
-    for (int j = 1; j < m; ++j) {
-      cA |= hA << j;
-      cB |= funnel(hB, hA, (uint32_t)(32 - j));
-      ov |= hB >> (32 - j);
-    }
-  }
-}
-
-__device__ __forceinline__ uint4 load_seg_nc(const uint4* __restrict__ seg, int nseg, int g) {
-  const int gc = g < 0 ? 0 : (g >= nseg ? nseg - 1 : g);
-  const uint4 x = seg[gc];  // unconditional: counted s_waitcnt vmcnt(N) keeps the ring in flight
-  const bool ok = (g >= 0) & (g < nseg);
-  return make_uint4(ok ? x.x : 0u, ok ? x.y : 0u, ok ? x.z : 0u, ok ? x.w : 0u);
-}
-
-// Covered bases of (cA, cB) below segment offset o (0..63), packed like own.
-__device__ __forceinline__ uint32_t below(uint32_t cA0, uint32_t cB0, uint32_t cA1, uint32_t cB1, int o) {
-  const uint32_t mlo = o >= 32 ? 0xFFFFFFFFu : ((1u << (uint32_t)o) - 1u);
-  const uint32_t mhi = o >= 32 ? ((1u << (uint32_t)(o - 32)) - 1u) : 0u;
-  const uint32_t p0 = __builtin_popcount(cA0 & mlo) + __builtin_popcount(cB0 & mhi);
-  const uint32_t p1 = __builtin_popcount(cA1 & mlo) + __builtin_popcount(cB1 & mhi);
-  return p0 | (p1 << 16);
-}
-
-struct ScanState {
-  uint32_t ov0, ov1, ov2;  // overflow carried into the next chunk's lane 0
-  uint32_t T0, T1, T2;     // covered bases before this chunk, per pass
-  uint32_t acc0, acc1;     // single-pattern hit counters (per lane)
-};
-
-// One chunk (lane's segment g = g0 + lane).
-template <bool kSingle, bool kValid, bool kOne, int kM>
-__device__ __forceinline__ void scan_chunk(const NtProgram* __restrict__ prog, const ReadCtx& rc,
-                                           int g0, int lane, int np, int nw, int L, DivL div,
-                                           uint4 cur, uint2* cum01, uint32_t* cum2,
-                                           uint32_t* hitacc, ScanState& st) {
-  const int n = (int)rc.n;
-  const int g = g0 + lane, base = 64 * g;
-  const uint32_t LA = cur.x, HA = cur.y, LB = cur.z, HB = cur.w;
-  const uint32_t LN = from_next_lane(LA), HN = from_next_lane(HA);
-  uint32_t VA = 0xFFFFFFFFu, VB = 0xFFFFFFFFu, VN = 0xFFFFFFFFu;
-  if (kValid) {
-    VA = range_mask(base, 0, n - 1);
-    VB = range_mask(base + 32, 0, n - 1);
-    VN = range_mask(base + 64, 0, n - 1);
-  }
-  uint32_t cA0 = 0u, cB0 = 0u, ov0 = 0u, cA1 = 0u, cB1 = 0u, ov1 = 0u;
-  const int n_pat = kSingle ? 1 : prog->n_pat;
-  for (int p = 0; p < n_pat; ++p) {
-    const NtPat& P = prog->pat[p];
-    uint32_t a0A, a1A, a0B, a1B;
-    word_hits<kValid, kOne, kM>(P, LA, LB, HA, HB, VA, VB, a0A, a1A);
-    word_hits<kValid, kOne, kM>(P, LB, LN, HB, HN, VB, VN, a0B, a1B);
-    if (rc.n_exc) {
-      patch_exceptions(rc, base, 0, n - 1, P, false, a0A, a1A);
-      patch_exceptions(rc, base + 32, 0, n - 1, P, false, a0B, a1B);
-    }
-    // matchPattern hit counts (lane 63's are dropped in the final sum)
-    if (kSingle) {
-      st.acc0 += __builtin_popcount(a0A) + __builtin_popcount(a0B);
-      st.acc1 += __builtin_popcount(a1A) + __builtin_popcount(a1B);
-    } else {
-      hitacc[p * kWave + lane] += __builtin_popcount(a0A) + __builtin_popcount(a0B);
-      hitacc[(n_pat + p) * kWave + lane] += __builtin_popcount(a1A) + __builtin_popcount(a1B);
-    }
-    seg_spread<kM>(a0A, a0B, P.m, cA0, cB0, ov0);
-    seg_spread<kM>(a1A, a1B, P.m, cA1, cB1, ov1);
-  }
-  uint32_t cA2 = 0u, cB2 = 0u, ov2 = 0u;
-  if (!kSingle && np == 3) {  // P3 = P2 U exact TVR matches
-    cA2 = cA1;
-    cB2 = cB1;
-    ov2 = ov1;
-    for (int t = 0; t < prog->n_tvr; ++t) {
-      const NtPat& P = prog->tvr[t];
-      uint32_t a0A, a1A, a0B, a1B;
-      word_hits<kValid, false, 0>(P, LA, LB, HA, HB, VA, VB, a0A, a1A);
-      word_hits<kValid, false, 0>(P, LB, LN, HB, HN, VB, VN, a0B, a1B);
-      if (rc.n_exc) {
-        patch_exceptions(rc, base, 0, n - 1, P, false, a0A, a1A);
-        patch_exceptions(rc, base + 32, 0, n - 1, P, false, a0B, a1B);
-      }
-      hitacc[(2 * n_pat + t) * kWave + lane] += __builtin_popcount(a0A) + __builtin_popcount(a0B);
-      seg_spread<0>(a0A, a0B, P.m, cA2, cB2, ov2);
-    }
-  }
-  // coverage spilled from the previous segment (lane 0: previous chunk's lane 62)
-  cA0 |= from_prev_lane(ov0, st.ov0);
-  cA1 |= from_prev_lane(ov1, st.ov1);
-  st.ov0 = __builtin_amdgcn_readlane(ov0, kWave - 2);
-  st.ov1 = __builtin_amdgcn_readlane(ov1, kWave - 2);
-  if (!kSingle && np == 3) {
-    cA2 |= from_prev_lane(ov2, st.ov2);
-    st.ov2 = __builtin_amdgcn_readlane(ov2, kWave - 2);
-  }
-  if (kValid) {  // trim to [1, n]
-    cA0 &= VA; cB0 &= VB;
-    cA1 &= VA; cB1 &= VB;
-    cA2 &= VA; cB2 &= VB;
-  }
-  if (nw <= 0) return;
-  // ---- window accounting: packed prefix sum of passes 0 | 1 << 16
-  const uint32_t own = (__builtin_popcount(cA0) + __builtin_popcount(cB0)) |
-                       ((__builtin_popcount(cA1) + __builtin_popcount(cB1)) << 16);
-  const uint32_t excl = wave_incl_scan(own) - own;
-  const bool three = !kSingle && np == 3;
-  uint32_t excl2 = 0u;
-  if (three) {
-    const uint32_t own2 = __builtin_popcount(cA2) + __builtin_popcount(cB2);
-    excl2 = wave_incl_scan(own2) - own2;
-  }
-  // boundary k*L of this segment (o = offset in the segment): running counts
-  // of the bases before it go to cum01[k] (passes 0, 1) and cum2[k] (pass 2)
-  auto store = [&](int k, int o) {
-    const uint32_t t = (1u << (uint32_t)(o & 31)) - 1u;  // v_bfm_b32
-    const bool hi = o >= 32;
-    const uint32_t mlo = hi ? 0xFFFFFFFFu : t, mhi = hi ? t : 0u;
-    const uint32_t v = excl + ((__builtin_popcount(cA0 & mlo) + __builtin_popcount(cB0 & mhi)) |
-                               ((__builtin_popcount(cA1 & mlo) + __builtin_popcount(cB1 & mhi)) << 16));
-    cum01[k] = make_uint2(st.T0 + (v & 0xFFFFu), st.T1 + (v >> 16));
-    if (three)
-      cum2[k] = st.T2 + excl2 + __builtin_popcount(cA2 & mlo) + __builtin_popcount(cB2 & mhi);
-  };
-  if (g >= 0 && lane < kWave - 1) {
-    int k = div_l(div, base + L - 1);  // first window start >= base
-    if (L >= 64) {  // at most one boundary per segment
-      const int o = k * L - base;
-      if (k >= 1 && k < nw && o <= 63) store(k, o);
-    } else {
-      for (k = k < 1 ? 1 : k; k < nw && k * L - base <= 63; ++k) store(k, k * L - base);
-    }
-  }
-  const uint32_t tot = __builtin_amdgcn_readlane(excl + own, kWave - 2);
-  st.T0 += tot & 0xFFFFu;
-  st.T1 += tot >> 16;
-  if (three) {
-    const uint32_t own2 = __builtin_popcount(cA2) + __builtin_popcount(cB2);
-    st.T2 += __builtin_amdgcn_readlane(excl2 + own2, kWave - 2);
-  }
-}
-
-// LDS (kLds) or global scratch per wave: [n_hits][64] hit accumulators
-// (generic programs only), then the running window counts (cum01, cum2).
-template <bool kSingle, bool kLds, bool kOne, int kM>
+// Ahead-of-time scan kernels for run-time pattern sets (nt_scan.h); the
+// hiprtc-specialised twin is built by nt_jit.cpp.
+template <class S, bool kLds>
 __global__ void __launch_bounds__(kWG)
 nt_scan_kernel(const NtProgram* __restrict__ prog, const uint32_t* __restrict__ thr, NtBatch B,
                NtOut O, uint64_t* __restrict__ tmask, uint32_t len_lo, uint32_t len_hi,
                uint32_t wave_words, uint32_t* __restrict__ gscr) {
   extern __shared__ uint32_t smem[];
-  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x >> 6;
-  const uint64_t gw = (uint64_t)blockIdx.x * kNWaves + wave, GW = (uint64_t)gridDim.x * kNWaves;
-  const int np = prog->n_pass, nh = prog->n_hits, L = prog->L;
-  uint32_t* wmem = kLds ? smem + (uint64_t)wave * wave_words : gscr + gw * wave_words;
-  uint32_t* hitacc = wmem;
-  const int tsz = (int)prog->thr_size;
-  const DivL div{prog->div32_m, prog->div32_s};
-  const uint32_t thr_full = thr[L < tsz ? L : tsz - 1];
-
-  for (uint64_t r = gw; r < B.n_reads; r += GW) {
-    const uint32_t n32 = B.len[r];
-    if (n32 <= len_lo || n32 > len_hi) continue;
-    const uint64_t boff = B.blk_off[r];
-    if (boff & 1u) {  // layout contract: 16-byte aligned segments
-      if (lane == 0) O.flags[r] = NT_FLAG_ERR_ALIGN;
-      continue;
-    }
-    ReadCtx rc;
-    rc.n = n32;
-    rc.nblk = (int32_t)((n32 + 31u) >> 5);
-    rc.blk = reinterpret_cast<const uint2*>(B.planes) + boff;
-    rc.n_exc = 0;
-    rc.exc_pos = nullptr;
-    rc.exc_code = nullptr;
-    if (B.exc_off) {
-      const uint32_t e0 = B.exc_off[r], e1 = B.exc_off[r + 1];
-      rc.n_exc = (int32_t)(e1 - e0);
-      rc.exc_pos = B.exc_pos + e0;
-      rc.exc_code = B.exc_code + e0;
-    }
-    const int n = (int)n32;
-    const int nseg = (n + 63) >> 6;
-    const int nw = (int)split_window_count(n, L);
-    // running counts: uint2 {pass 0, pass 1} [nw+1], then pass 2 [nw+1]
-    uint2* cum01 = reinterpret_cast<uint2*>(wmem + (kSingle ? 0 : nh * kWave));
-    uint32_t* cum2 = reinterpret_cast<uint32_t*>(cum01 + (nw + 1));
-    if (!kSingle)
-      for (int c = 0; c < nh; ++c) hitacc[c * kWave + lane] = 0u;
-    // hitacc slots are per lane: no cross-lane sync needed before the scan
-
-    // ------------------------------------------------------------ scan
-    ScanState st{0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
-    {
-      const uint4* seg = reinterpret_cast<const uint4*>(rc.blk);
-      // 2-deep prefetch ring: this lane's segment of the next two chunks
-      uint4 nx1 = load_seg_nc(seg, nseg, lane - 1), nx2 = load_seg_nc(seg, nseg, kOwned - 1 + lane);
-      for (int g0 = -1; g0 < nseg; g0 += kOwned) {
-        const uint4 cur = nx1;
-        nx1 = nx2;
-        nx2 = load_seg_nc(seg, nseg, g0 + 2 * kOwned + lane);
-        if (g0 >= 0 && 64 * (g0 + kWave) <= n)
-          scan_chunk<kSingle, false, kOne, kM>(prog, rc, g0, lane, np, nw, L, div, cur, cum01, cum2,
-                                               hitacc, st);
-        else
-          scan_chunk<kSingle, true, kOne, kM>(prog, rc, g0, lane, np, nw, L, div, cur, cum01, cum2,
-                                              hitacc, st);
-      }
-    }
-    if (lane == 0 && nw > 0) {
-      cum01[0] = make_uint2(0u, 0u);
-      cum01[nw] = make_uint2(st.T0, st.T1);
-      if (np == 3 && !kSingle) {
-        cum2[0] = 0u;
-        cum2[nw] = st.T2;
-      }
-    }
-    wave_sync();
-
-    // ------------------------------------------------ window outputs
-    uint16_t* wout = O.win_counts + B.win_off[r] * np;
-    // telomeric window (class -5) iff !(count / width < min_density) iff
-    // count >= thr[width] (exact, host-computed); the last window may be wider
-    uint32_t thr_last = thr_full;
-    if (nw > 0) {
-      const int wl = n - (nw - 1) * L;
-      thr_last = thr[wl < tsz ? wl : tsz - 1];
-    }
-    const int nmw = (nw + 63) >> 6;
-    uint64_t* tmo = tmask + tm_base(B.win_off[r], r, np);
-    for (int p = 0; p < np; ++p) {
-      for (int ch = 0; ch < nmw; ++ch) {
-        const int i = ch * 64 + lane;
-        uint32_t cnt = 0u;
-        if (i < nw) {
-          if (p == 2) cnt = cum2[i + 1] - cum2[i];
-          else if (p == 1) cnt = cum01[i + 1].y - cum01[i].y;
-          else cnt = cum01[i + 1].x - cum01[i].x;
-          wout[p * nw + i] = (uint16_t)cnt;
-        }
-        const bool t = i < nw && cnt >= (i == nw - 1 ? thr_last : thr_full);
-        const uint64_t bal = __ballot(t);
-        if (lane == 0) tmo[p * nmw + ch] = bal;
-      }
-    }
-    if (O.hits) {
-      if (kSingle) {
-        const uint32_t h0 = wave_sum_u32(lane < kOwned ? st.acc0 : 0u);
-        const uint32_t h1 = wave_sum_u32(lane < kOwned ? st.acc1 : 0u);
-        if (lane == 0) {
-          O.hits[r * (uint64_t)nh] = h0;
-          O.hits[r * (uint64_t)nh + 1] = h1;
-        }
-      } else {
-        for (int c = 0; c < nh; ++c) {
-          const uint32_t v = wave_sum_u32(lane < kOwned ? hitacc[c * kWave + lane] : 0u);
-          if (lane == 0) O.hits[r * (uint64_t)nh + c] = v;
-        }
-      }
-    }
-    wave_sync();
-  }
+  const uint64_t gw = (uint64_t)blockIdx.x * kNWaves + (threadIdx.x >> 6);
+  uint32_t* wmem = kLds ? smem + (uint64_t)(threadIdx.x >> 6) * wave_words : gscr + gw * wave_words;
+  scan_reads<S, kLds>(prog, thr, B, O, tmask, len_lo, len_hi, wmem);
 }
 
 // ================================================================= call
@@ -914,6 +496,9 @@ nt_layout_kernel(uint64_t n_reads, uint64_t nblk, uint64_t read_len, uint64_t nw
 
 extern "C" {
 
+hipError_t nt_dev_launch_call(const NtProgram* prog, const NtBatch* B, const NtOut* O,
+                              const uint64_t* tmask, int call_grid, hipStream_t stream);
+
 // per-wave scan scratch words for reads with at most nw_cap windows
 uint32_t nt_dev_wave_words(int single, int n_hits, int np, uint32_t nw_cap) {
   const uint32_t w = (single ? 0u : (uint32_t)n_hits * 64u) + (uint32_t)(np < 2 ? 2 : np) * (nw_cap + 1u);
@@ -926,20 +511,25 @@ uint64_t nt_dev_tmask_words(uint64_t total_windows, uint64_t n_reads, int np) {
 }
 
 // (single, lds, one-hot, compile-time m): m = 6 covers TTAGGG-style motifs
-#define NT_SCAN_VARIANTS(X) \
-  X(true, true, true, 6)    \
-  X(true, true, false, 6)   \
-  X(true, true, true, 0)    \
-  X(true, true, false, 0)   \
-  X(true, false, false, 0)  \
-  X(false, true, false, 0)  \
-  X(false, false, false, 0)
+// AOT scan variants: (pattern set, LDS?, single, one-hot, m == 6)
+using nt::GenericSet;
+using nt::RtOneHot;
+using nt::RtTable;
+using nt::SingleSet;
+#define NT_SCAN_VARIANTS(X)                        \
+  X(SingleSet<RtOneHot<6>>, true, 1, 1, 1)         \
+  X(SingleSet<RtTable<6>>, true, 1, 0, 1)          \
+  X(SingleSet<RtOneHot<0>>, true, 1, 1, 0)         \
+  X(SingleSet<RtTable<0>>, true, 1, 0, 0)          \
+  X(SingleSet<RtTable<0>>, false, 1, -1, -1)       \
+  X(GenericSet, true, 0, -1, -1)                   \
+  X(GenericSet, false, 0, -1, -1)
 
 hipError_t nt_dev_set_lds_limit(uint32_t bytes) {
   hipError_t e = hipSuccess;
-#define NT_ATTR(S, G, O, M)                                                                    \
+#define NT_ATTR(S, G, SI, O, M)                                                                \
   if (G && e == hipSuccess)                                                                    \
-    e = hipFuncSetAttribute((const void*)nt::nt_scan_kernel<S, G, O, M>,                       \
+    e = hipFuncSetAttribute((const void*)nt::nt_scan_kernel<S, G>,                             \
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
   NT_SCAN_VARIANTS(NT_ATTR)
 #undef NT_ATTR
@@ -953,10 +543,9 @@ hipError_t nt_dev_launch(const NtProgram* prog, const uint32_t* thr, const NtBat
                          int grid, int call_grid, hipStream_t stream) {
   const size_t lds_bytes = lds ? (size_t)wave_words * 4u * nt::kNWaves : 0;
   bool done = false;
-#define NT_LAUNCH(S, G, O_, M)                                                                 \
-  if (!done && single == (int)S && lds == (int)G &&                                            \
-      (!S || !G || (one == (int)O_ && m6 == (M == 6)))) {                                      \
-    hipLaunchKernelGGL((nt::nt_scan_kernel<S, G, O_, M>), dim3(grid), dim3(nt::kWG), lds_bytes, \
+#define NT_LAUNCH(S, G, SI, O_, M)                                                             \
+  if (!done && single == SI && lds == (int)G && (O_ < 0 || one == O_) && (M < 0 || m6 == M)) { \
+    hipLaunchKernelGGL((nt::nt_scan_kernel<S, G>), dim3(grid), dim3(nt::kWG), lds_bytes,       \
                        stream, prog, thr, *B, *O, tmask, len_lo, len_hi, wave_words, gscr);    \
     done = true;                                                                               \
   }
@@ -965,6 +554,11 @@ hipError_t nt_dev_launch(const NtProgram* prog, const uint32_t* thr, const NtBat
   if (!done) return hipErrorInvalidValue;
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || call_grid <= 0) return e;
+  return nt_dev_launch_call(prog, B, O, tmask, call_grid, stream);
+}
+
+hipError_t nt_dev_launch_call(const NtProgram* prog, const NtBatch* B, const NtOut* O,
+                              const uint64_t* tmask, int call_grid, hipStream_t stream) {
   hipLaunchKernelGGL(nt::nt_call_kernel, dim3(call_grid), dim3(256), 0, stream, prog, *B, *O, tmask);
   return hipGetLastError();
 }

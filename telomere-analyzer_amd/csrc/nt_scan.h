@@ -1,0 +1,625 @@
+// nt_scan.h -- the streaming scan of the NanoTel hot path on gfx950.
+//
+// Computes, per read and pass (P1 exact, P2 <= 1 mismatch, P3 = P2 U exact
+// TVR matches), the covered-base count of every subseq_length window
+// (analyze_subtelos / get_density_iranges / get_sub_density, NanoTel.R:
+// 717-766, 308-397, 449-468), the telomeric-window bitmask (class -5,
+// NanoTel.R:749-758) and the matchPattern hit counts.
+//
+// Compiled twice: ahead of time (nt_kernels.hip) with the pattern set read
+// from NtProgram at run time, and at nt_compile() time through hiprtc
+// (nt_jit.cpp) with the pattern set baked in as compile-time truth tables, so
+// that every letter test is one v_bitop3 and identical letter tests and
+// shifts are shared across letters and patterns.
+//
+// Work split: one wave per read (grid-stride), the read cut into 64-base
+// SEGMENTS (two 32-base words A, B = one 16-byte load of the bit planes).
+// Chunk c of a read covers segments g0 = 63c - 1 ... g0 + 63: lane l holds
+// segment g0 + l; lanes 0..62 OWN theirs, lane 63 only lends its letter
+// tests to lane 62 (the matches starting in a segment read up to m-1 bases
+// into the next one).  Chunk 0 starts at segment -1 so that Biostrings'
+// out-of-bound start (-1, one mismatch) is an ordinary hit of lane 0.
+//
+// Neighbour data moves with wave-wide DPP (wave_shl:1 / wave_shr:1); the
+// coverage a segment spills into the next one ("overflow") travels right
+// the same way, lane 62's overflow is carried into the next chunk's lane 0.
+// Window counts: the per-lane covered-base counts of passes 0 and 1 are
+// packed into one u32 (16+16 bit), prefix-summed across the wave with DPP
+// row_shr / row_bcast, and the lane holding a window boundary kL stores the
+// running count there (cum[k]); count(window k) = cum[k+1] - cum[k].  No
+// atomics, no zero-fill: every boundary belongs to exactly one owned lane.
+#pragma once
+#include "nt_common.h"
+#include "nt_device.h"
+
+namespace nt {
+
+// floor(p / L), 0 <= p < 2^31 (multiply-shift, exact; see nt_compile)
+struct DivL {
+  uint32_t m, s;
+};
+__device__ __forceinline__ int div_l(DivL d, int p) {
+  if (d.m == 0u) return p;  // L == 1
+  return (int)(__umulhi((uint32_t)p, d.m) >> d.s);
+}
+__device__ __forceinline__ int div_l(const NtProgram* prog, int p) {
+  return div_l(DivL{prog->div32_m, prog->div32_s}, p);
+}
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// First uint64 of read r's telomeric bitmasks (pass p at + p * nmw):
+// tm_off(r) = (win_off[r] >> 6) + r never overlaps read r+1's block.
+__device__ __forceinline__ uint64_t tm_base(uint64_t win_off, uint64_t r, int np) {
+  return ((win_off >> 6) + r) * (uint64_t)np;
+}
+
+template <int I>
+struct IC {
+  static constexpr int value = I;
+};
+template <int I, int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(IC<I>{});
+    static_for<I + 1, N>(f);
+  }
+}
+
+// ------------------------------------------------------------------ DPP
+
+constexpr int kDppWaveShl1 = 0x130;  // lane i <- lane i+1
+constexpr int kDppWaveShr1 = 0x138;  // lane i <- lane i-1
+constexpr int kDppRowShr = 0x110;    // + n: row_shr:n
+constexpr int kDppRowBcast15 = 0x142;
+constexpr int kDppRowBcast31 = 0x143;
+
+// lane i <- lane i+1 (lane 63 <- 0)
+__device__ __forceinline__ uint32_t from_next_lane(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kDppWaveShl1, 0xf, 0xf, false);
+}
+// lane i <- lane i-1 (lane 0 <- lane0)
+__device__ __forceinline__ uint32_t from_prev_lane(uint32_t v, uint32_t lane0) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)lane0, (int)v, kDppWaveShr1, 0xf, 0xf, false);
+}
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ uint32_t dpp0(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kCtrl, kRowMask, 0xf, false);
+}
+// inclusive prefix sum over the 64 lanes
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+  v += dpp0<kDppRowShr + 1, 0xf>(v);
+  v += dpp0<kDppRowShr + 2, 0xf>(v);
+  v += dpp0<kDppRowShr + 4, 0xf>(v);
+  v += dpp0<kDppRowShr + 8, 0xf>(v);
+  v += dpp0<kDppRowBcast15, 0xa>(v);
+  v += dpp0<kDppRowBcast31, 0xc>(v);
+  return v;
+}
+
+// ------------------------------------------------------ letter tests
+
+// Bit i of the result: base (L_i, H_i) (A=00 C=01 G=10 T=11, H:L) is in the
+// 4-bit set tt (bit c = base c).  tt constant -> one v_bitop3 (or nothing).
+__device__ __forceinline__ uint32_t tt_test(int tt, uint32_t L, uint32_t H) {
+  switch (tt & 15) {
+    case 0: return 0u;
+    case 1: return ~(L | H);    // A
+    case 2: return L & ~H;      // C
+    case 3: return ~H;          // M = A|C
+    case 4: return ~L & H;      // G
+    case 5: return ~L;          // R = A|G
+    case 6: return L ^ H;       // S = C|G
+    case 7: return ~(L & H);    // V = A|C|G
+    case 8: return L & H;       // T
+    case 9: return ~(L ^ H);    // W = A|T
+    case 10: return L;          // Y = C|T
+    case 11: return L | ~H;     // H = A|C|T
+    case 12: return H;          // K = G|T
+    case 13: return ~L | H;     // D = A|G|T
+    case 14: return L | H;      // B = C|G|T
+    default: return 0xFFFFFFFFu;  // N
+  }
+}
+
+// Pattern descriptors: kM (compile-time length, 0 = run time), m(), and
+// E(j, L, H) = letter j of the pattern tested against the 32 bases (L, H).
+// Run-time one-hot letters: (L ^ xl) & (H ^ xh), two VALU ops.
+template <int M>
+struct RtOneHot {
+  static constexpr int kM = M;
+  const NtPat* P;
+  __device__ __forceinline__ int m() const { return M > 0 ? M : P->m; }
+  __device__ __forceinline__ uint32_t E(int j, uint32_t L, uint32_t H) const {
+    return (L ^ P->xl[j]) & (H ^ P->xh[j]);
+  }
+};
+// Run-time IUPAC letters (scan semantics): truth table as bit-select masks.
+template <int M>
+struct RtTable {
+  static constexpr int kM = M;
+  const NtPat* P;
+  __device__ __forceinline__ int m() const { return M > 0 ? M : P->m; }
+  __device__ __forceinline__ uint32_t E(int j, uint32_t L, uint32_t H) const {
+    const uint32_t* t = P->tm_scan[j];
+    return bfi(H, bfi(L, t[3], t[2]), bfi(L, t[1], t[0]));
+  }
+};
+
+__device__ __forceinline__ uint32_t maj3(uint32_t a, uint32_t b, uint32_t c) {
+  return (a & b) | (a & c) | (b & c);  // v_bitop3 0xe8
+}
+
+// a0 = AND of the kM letter words (exact), a1 = at most one zero (<= 1
+// mismatch): three letters at a time -- all-3 and at-least-2-of-3 per group,
+// then a1 = (a1 & all) | (a0 & two), a0 &= all.
+template <int kM, bool kExact>
+__device__ __forceinline__ void combine(const uint32_t* q, uint32_t& a0, uint32_t& a1) {
+  uint32_t x0 = q[0], x1 = 0xFFFFFFFFu;
+  if constexpr (kExact) {
+#pragma unroll
+    for (int j = 1; j < kM; ++j) x0 &= q[j];
+    a0 = x0;
+    a1 = 0u;
+    return;
+  }
+  int j = 1;
+  if constexpr (kM >= 3) {
+    x0 = q[0] & q[1] & q[2];
+    x1 = maj3(q[0], q[1], q[2]);
+    j = 3;
+  } else if constexpr (kM == 2) {
+    x0 = q[0] & q[1];
+    x1 = q[0] | q[1];
+    j = 2;
+  }
+#pragma unroll
+  for (; j + 3 <= kM; j += 3) {
+    const uint32_t all = q[j] & q[j + 1] & q[j + 2], two = maj3(q[j], q[j + 1], q[j + 2]);
+    x1 = (x1 & all) | (x0 & two);
+    x0 &= all;
+  }
+  if constexpr (kM >= 3 && kM % 3 == 2) {
+    const uint32_t all = q[kM - 2] & q[kM - 1], one = q[kM - 2] | q[kM - 1];
+    x1 = (x1 & all) | (x0 & one);
+    x0 &= all;
+  } else if constexpr (kM >= 3 && kM % 3 == 1) {
+    x1 = (x1 & q[kM - 1]) | x0;
+    x0 &= q[kM - 1];
+  }
+  a0 = x0;
+  a1 = x1;
+}
+
+// Planes and validity of one segment (word A, word B).
+struct Seg {
+  uint32_t LA, HA, LB, HB;
+  uint32_t VA, VB;  // positions inside the read (kValid chunks only)
+};
+
+// Hits of pattern d at the 64 starts of the segment: a0 exact, a1 <= 1
+// mismatch (matchPattern max.mismatch 0 / 1; letters outside the read are
+// mismatches).  Letter tests are made on the unshifted words and shifted by
+// j (v_alignbit); the next segment's word-A tests come from lane+1 by DPP.
+template <bool kValid, bool kExact, class D>
+__device__ __forceinline__ void seg_hits(const D& d, const Seg& s, uint32_t& a0A, uint32_t& a1A,
+                                         uint32_t& a0B, uint32_t& a1B) {
+  constexpr int kM = D::kM;
+  auto q = [&](int j, uint32_t& qA, uint32_t& qB) {
+    uint32_t eA = d.E(j, s.LA, s.HA), eB = d.E(j, s.LB, s.HB);
+    if (kValid) {
+      eA &= s.VA;
+      eB &= s.VB;
+    }
+    const uint32_t eN = from_next_lane(eA);
+    qA = funnel(eB, eA, (uint32_t)j);
+    qB = funnel(eN, eB, (uint32_t)j);
+  };
+  if constexpr (kM > 0) {
+    uint32_t qa[kM], qb[kM];
+#pragma unroll
+    for (int j = 0; j < kM; ++j) q(j, qa[j], qb[j]);
+    combine<kM, kExact>(qa, a0A, a1A);
+    combine<kM, kExact>(qb, a0B, a1B);
+  } else {
+    uint32_t x0A = 0xFFFFFFFFu, x1A = 0xFFFFFFFFu, x0B = 0xFFFFFFFFu, x1B = 0xFFFFFFFFu;
+    const int m = d.m();
+    for (int j = 0; j < m; ++j) {
+      uint32_t qA, qB;
+      q(j, qA, qB);
+      x1A = (x1A & qA) | x0A;
+      x0A &= qA;
+      x1B = (x1B & qB) | x0B;
+      x0B &= qB;
+    }
+    a0A = x0A;
+    a1A = kExact ? 0u : x1A;
+    a0B = x0B;
+    a1B = kExact ? 0u : x1B;
+  }
+  if (kValid && !kExact && d.m() <= 1) {  // m <= k: no out-of-bound starts
+    a1A &= s.VA;
+    a1B &= s.VB;
+  }
+}
+
+// OR into (cA, cB, ov) the coverage of hit starts hA (word A) and hB (word
+// B): bit i covered iff a start in [i-m+1, i] (trim + IRanges::reduce).
+// ov = coverage spilling into the next segment's word A.  kM > 0: span
+// doubling on the 96-bit value (ov:B:A).
+template <int kM>
+__device__ __forceinline__ void seg_spread(uint32_t hA, uint32_t hB, int m, uint32_t& cA,
+                                           uint32_t& cB, uint32_t& ov) {
+  if constexpr (kM > 0) {
+    uint32_t w0 = hA, w1 = hB, w2 = 0u;
+#pragma unroll
+    for (int s = 1; s < kM;) {
+      const int t = 2 * s <= kM ? s : kM - s;
+      w2 |= funnel(w2, w1, (uint32_t)(32 - t));
+      w1 |= funnel(w1, w0, (uint32_t)(32 - t));
+      w0 |= w0 << t;
+      s += t;
+    }
+    cA |= w0;
+    cB |= w1;
+    ov |= w2;
+  } else {
+    cA |= hA;
+    cB |= hB;
+    for (int j = 1; j < m; ++j) {
+      cA |= hA << j;
+      cB |= funnel(hB, hA, (uint32_t)(32 - j));
+      ov |= hB >> (32 - j);
+    }
+  }
+}
+
+// ------------------------------------------------------ pattern sets
+
+// Pattern-set policies: passes, hit counters and a visitor over the patterns
+// (f(index, descriptor)) and the TVRs.
+// kRegHits: hit counters in registers (else per-lane LDS/global slots).
+// Hit counter layout (per read): [exact per pattern][<=1 mismatch per
+// pattern][exact per TVR] (nt_program_info.n_hits = 2*n_pat + n_tvr).
+template <class D>
+struct SingleSet {  // --patterns with one unique pattern, no TVRs
+  static constexpr bool kRegHits = true;
+  static constexpr int kNPat = 1;
+  static constexpr int kNHits = 2;
+  static constexpr int kNPass = 2;  // 0 = read from the program
+  template <class F>
+  __device__ __forceinline__ static void for_pat(const NtProgram* prog, F&& f) {
+    f(0, D{&prog->pat[0]});
+  }
+  template <class F>
+  __device__ __forceinline__ static void for_tvr(const NtProgram*, F&&) {}
+};
+
+struct GenericSet {  // any program: run-time lists
+  static constexpr bool kRegHits = false;
+  static constexpr int kNPat = 0;
+  static constexpr int kNHits = 1;
+  static constexpr int kNPass = 0;
+  template <class F>
+  __device__ __forceinline__ static void for_pat(const NtProgram* prog, F&& f) {
+    for (int p = 0; p < prog->n_pat; ++p) f(p, RtTable<0>{&prog->pat[p]});
+  }
+  template <class F>
+  __device__ __forceinline__ static void for_tvr(const NtProgram* prog, F&& f) {
+    for (int t = 0; t < prog->n_tvr; ++t) f(t, RtTable<0>{&prog->tvr[t]});
+  }
+};
+
+// Compile-time pattern (JIT): the host generates JitPat<...> lists.
+template <int M, int... TT>
+struct CtPat {
+  static constexpr int kM = M;
+  const NtPat* P;  // run-time twin (exception fix-ups)
+  __device__ __forceinline__ int m() const { return M; }
+  __device__ __forceinline__ uint32_t E(int j, uint32_t L, uint32_t H) const {
+    constexpr int tt[] = {TT...};
+    return tt_test(tt[j], L, H);
+  }
+};
+template <class... P>
+struct CtList {
+  static constexpr int kN = sizeof...(P);
+};
+template <int I, class Head, class... Tail>
+struct CtAt {
+  using type = typename CtAt<I - 1, Tail...>::type;
+};
+template <class Head, class... Tail>
+struct CtAt<0, Head, Tail...> {
+  using type = Head;
+};
+template <class List>
+struct CtVisit;
+template <class... P>
+struct CtVisit<CtList<P...>> {
+  template <class F>
+  __device__ __forceinline__ static void run(const NtPat* base, F&& f) {
+    static_for<0, (int)sizeof...(P)>([&](auto i) {
+      constexpr int I = decltype(i)::value;
+      using D = typename CtAt<I, P...>::type;
+      f(I, D{base + I});
+    });
+  }
+};
+template <>
+struct CtVisit<CtList<>> {
+  template <class F>
+  __device__ __forceinline__ static void run(const NtPat*, F&&) {}
+};
+
+template <class Pats, class Tvrs>
+struct CtSet {
+  static constexpr int kNPat = Pats::kN, kNTvr = Tvrs::kN;
+  static constexpr bool kRegHits = true;
+  static constexpr int kNHits = 2 * kNPat + kNTvr;
+  static constexpr int kNPass = kNTvr > 0 ? 3 : 2;
+  template <class F>
+  __device__ __forceinline__ static void for_pat(const NtProgram* prog, F&& f) {
+    CtVisit<Pats>::run(prog->pat, f);
+  }
+  template <class F>
+  __device__ __forceinline__ static void for_tvr(const NtProgram* prog, F&& f) {
+    CtVisit<Tvrs>::run(prog->tvr, f);
+  }
+};
+
+// ------------------------------------------------------------ the scan
+
+__device__ __forceinline__ uint4 load_seg_nc(const uint4* __restrict__ seg, int nseg, int g) {
+  const int gc = g < 0 ? 0 : (g >= nseg ? nseg - 1 : g);
+  const uint4 x = seg[gc];  // unconditional: counted s_waitcnt vmcnt(N) keeps the ring in flight
+  const bool ok = (g >= 0) & (g < nseg);
+  return make_uint4(ok ? x.x : 0u, ok ? x.y : 0u, ok ? x.z : 0u, ok ? x.w : 0u);
+}
+
+template <int kNHits>
+struct ScanState {
+  uint32_t ov0, ov1, ov2;  // overflow carried into the next chunk's lane 0
+  uint32_t T0, T1, T2;     // covered bases before this chunk, per pass
+  uint32_t acc[kNHits];    // register hit counters (per lane)
+};
+
+// One chunk (lane's segment g = g0 + lane).
+template <class S, bool kValid>
+__device__ __forceinline__ void scan_chunk(const NtProgram* __restrict__ prog, const ReadCtx& rc,
+                                           int g0, int lane, int np, int nw, int L, DivL div,
+                                           uint4 cur, uint2* cum01, uint32_t* cum2,
+                                           uint32_t* hitacc, ScanState<S::kNHits>& st) {
+  const int n = (int)rc.n;
+  const int g = g0 + lane, base = 64 * g;
+  Seg s;
+  s.LA = cur.x;
+  s.HA = cur.y;
+  s.LB = cur.z;
+  s.HB = cur.w;
+  s.VA = s.VB = 0xFFFFFFFFu;
+  if (kValid) {
+    s.VA = range_mask(base, 0, n - 1);
+    s.VB = range_mask(base + 32, 0, n - 1);
+  }
+  const int n_pat = S::kRegHits ? S::kNPat : prog->n_pat;
+  uint32_t cA0 = 0u, cB0 = 0u, ov0 = 0u, cA1 = 0u, cB1 = 0u, ov1 = 0u;
+  S::for_pat(prog, [&](int p, auto d) {
+    uint32_t a0A, a1A, a0B, a1B;
+    seg_hits<kValid, false>(d, s, a0A, a1A, a0B, a1B);
+    if (rc.n_exc) {
+      patch_exceptions(rc, base, 0, n - 1, *d.P, false, a0A, a1A);
+      patch_exceptions(rc, base + 32, 0, n - 1, *d.P, false, a0B, a1B);
+    }
+    // matchPattern hit counts (lane 63's are dropped in the final sum)
+    const uint32_t h0 = __builtin_popcount(a0A) + __builtin_popcount(a0B);
+    const uint32_t h1 = __builtin_popcount(a1A) + __builtin_popcount(a1B);
+    if constexpr (S::kRegHits) {
+      st.acc[p] += h0;
+      st.acc[S::kNPat + p] += h1;
+    } else {
+      hitacc[p * kWave + lane] += h0;
+      hitacc[(n_pat + p) * kWave + lane] += h1;
+    }
+    seg_spread<decltype(d)::kM>(a0A, a0B, d.m(), cA0, cB0, ov0);
+    seg_spread<decltype(d)::kM>(a1A, a1B, d.m(), cA1, cB1, ov1);
+  });
+  const bool three = S::kNPass == 3 || (S::kNPass == 0 && np == 3);
+  uint32_t cA2 = 0u, cB2 = 0u, ov2 = 0u;
+  if (three) {  // P3 = P2 U exact TVR matches
+    cA2 = cA1;
+    cB2 = cB1;
+    ov2 = ov1;
+    S::for_tvr(prog, [&](int t, auto d) {
+      uint32_t a0A, a1A, a0B, a1B;
+      seg_hits<kValid, true>(d, s, a0A, a1A, a0B, a1B);
+      if (rc.n_exc) {
+        patch_exceptions(rc, base, 0, n - 1, *d.P, false, a0A, a1A);
+        patch_exceptions(rc, base + 32, 0, n - 1, *d.P, false, a0B, a1B);
+      }
+      const uint32_t h0 = __builtin_popcount(a0A) + __builtin_popcount(a0B);
+      if constexpr (S::kRegHits) st.acc[2 * S::kNPat + t] += h0;
+      else hitacc[(2 * n_pat + t) * kWave + lane] += h0;
+      seg_spread<decltype(d)::kM>(a0A, a0B, d.m(), cA2, cB2, ov2);
+    });
+  }
+  // coverage spilled from the previous segment (lane 0: previous chunk's lane 62)
+  cA0 |= from_prev_lane(ov0, st.ov0);
+  cA1 |= from_prev_lane(ov1, st.ov1);
+  st.ov0 = __builtin_amdgcn_readlane(ov0, kWave - 2);
+  st.ov1 = __builtin_amdgcn_readlane(ov1, kWave - 2);
+  if (three) {
+    cA2 |= from_prev_lane(ov2, st.ov2);
+    st.ov2 = __builtin_amdgcn_readlane(ov2, kWave - 2);
+  }
+  if (kValid) {  // trim to [1, n]
+    cA0 &= s.VA;
+    cB0 &= s.VB;
+    cA1 &= s.VA;
+    cB1 &= s.VB;
+    cA2 &= s.VA;
+    cB2 &= s.VB;
+  }
+  if (nw <= 0) return;
+  // ---- window accounting: packed prefix sum of passes 0 | 1 << 16
+  const uint32_t own = (__builtin_popcount(cA0) + __builtin_popcount(cB0)) |
+                       ((__builtin_popcount(cA1) + __builtin_popcount(cB1)) << 16);
+  const uint32_t excl = wave_incl_scan(own) - own;
+  uint32_t own2 = 0u, excl2 = 0u;
+  if (three) {
+    own2 = __builtin_popcount(cA2) + __builtin_popcount(cB2);
+    excl2 = wave_incl_scan(own2) - own2;
+  }
+  // boundary k*L of this segment (o = offset in the segment): running counts
+  // of the bases before it go to cum01[k] (passes 0, 1) and cum2[k] (pass 2)
+  auto store = [&](int k, int o) {
+    const uint32_t t = (1u << (uint32_t)(o & 31)) - 1u;  // v_bfm_b32
+    const bool hi = o >= 32;
+    const uint32_t mlo = hi ? 0xFFFFFFFFu : t, mhi = hi ? t : 0u;
+    const uint32_t v = excl + ((__builtin_popcount(cA0 & mlo) + __builtin_popcount(cB0 & mhi)) |
+                               ((__builtin_popcount(cA1 & mlo) + __builtin_popcount(cB1 & mhi)) << 16));
+    cum01[k] = make_uint2(st.T0 + (v & 0xFFFFu), st.T1 + (v >> 16));
+    if (three)
+      cum2[k] = st.T2 + excl2 + __builtin_popcount(cA2 & mlo) + __builtin_popcount(cB2 & mhi);
+  };
+  if (g >= 0 && lane < kWave - 1) {
+    int k = div_l(div, base + L - 1);  // first window start >= base
+    if (L >= 64) {  // at most one boundary per segment
+      const int o = k * L - base;
+      if (k >= 1 && k < nw && o <= 63) store(k, o);
+    } else {
+      for (k = k < 1 ? 1 : k; k < nw && k * L - base <= 63; ++k) store(k, k * L - base);
+    }
+  }
+  const uint32_t tot = __builtin_amdgcn_readlane(excl + own, kWave - 2);
+  st.T0 += tot & 0xFFFFu;
+  st.T1 += tot >> 16;
+  if (three) st.T2 += __builtin_amdgcn_readlane(excl2 + own2, kWave - 2);
+}
+
+// The whole scan of the reads with len in (len_lo, len_hi] (grid-stride, one
+// wave per read).  wmem: this wave's LDS (kLds) or global scratch:
+// [n_hits][64] hit slots (run-time sets only), then the running window counts
+// cum01 (uint2 {pass 0, pass 1} [nw+1]) and cum2 (pass 2 [nw+1]).
+template <class S, bool kLds>
+__device__ __forceinline__ void scan_reads(const NtProgram* __restrict__ prog,
+                                           const uint32_t* __restrict__ thr, const NtBatch& B,
+                                           const NtOut& O, uint64_t* __restrict__ tmask,
+                                           uint32_t len_lo, uint32_t len_hi, uint32_t* wmem) {
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x >> 6;
+  const uint64_t gw = (uint64_t)blockIdx.x * kNWaves + wave, GW = (uint64_t)gridDim.x * kNWaves;
+  const int np = S::kNPass ? S::kNPass : prog->n_pass;
+  const int nh = S::kRegHits ? S::kNHits : prog->n_hits, L = prog->L;
+  uint32_t* hitacc = wmem;
+  const int tsz = (int)prog->thr_size;
+  const DivL div{prog->div32_m, prog->div32_s};
+  const uint32_t thr_full = thr[L < tsz ? L : tsz - 1];
+
+  for (uint64_t r = gw; r < B.n_reads; r += GW) {
+    const uint32_t n32 = B.len[r];
+    if (n32 <= len_lo || n32 > len_hi) continue;
+    const uint64_t boff = B.blk_off[r];
+    if (boff & 1u) {  // layout contract: 16-byte aligned segments
+      if (lane == 0) O.flags[r] = NT_FLAG_ERR_ALIGN;
+      continue;
+    }
+    ReadCtx rc;
+    rc.n = n32;
+    rc.nblk = (int32_t)((n32 + 31u) >> 5);
+    rc.blk = reinterpret_cast<const uint2*>(B.planes) + boff;
+    rc.n_exc = 0;
+    rc.exc_pos = nullptr;
+    rc.exc_code = nullptr;
+    if (B.exc_off) {
+      const uint32_t e0 = B.exc_off[r], e1 = B.exc_off[r + 1];
+      rc.n_exc = (int32_t)(e1 - e0);
+      rc.exc_pos = B.exc_pos + e0;
+      rc.exc_code = B.exc_code + e0;
+    }
+    const int n = (int)n32;
+    const int nseg = (n + 63) >> 6;
+    const int nw = (int)split_window_count(n, L);
+    uint2* cum01 = reinterpret_cast<uint2*>(wmem + (S::kRegHits ? 0 : nh * kWave));
+    uint32_t* cum2 = reinterpret_cast<uint32_t*>(cum01 + (nw + 1));
+    if (!S::kRegHits)
+      for (int c = 0; c < nh; ++c) hitacc[c * kWave + lane] = 0u;  // per-lane slots
+
+    // ------------------------------------------------------------ scan
+    ScanState<S::kNHits> st;
+    st.ov0 = st.ov1 = st.ov2 = 0u;
+    st.T0 = st.T1 = st.T2 = 0u;
+#pragma unroll
+    for (int c = 0; c < S::kNHits; ++c) st.acc[c] = 0u;
+    {
+      const uint4* seg = reinterpret_cast<const uint4*>(rc.blk);
+      // 2-deep prefetch ring: this lane's segment of the next two chunks
+      uint4 nx1 = load_seg_nc(seg, nseg, lane - 1), nx2 = load_seg_nc(seg, nseg, kOwned - 1 + lane);
+      for (int g0 = -1; g0 < nseg; g0 += kOwned) {
+        const uint4 cur = nx1;
+        nx1 = nx2;
+        nx2 = load_seg_nc(seg, nseg, g0 + 2 * kOwned + lane);
+        if (g0 >= 0 && 64 * (g0 + kWave) <= n)
+          scan_chunk<S, false>(prog, rc, g0, lane, np, nw, L, div, cur, cum01, cum2, hitacc, st);
+        else
+          scan_chunk<S, true>(prog, rc, g0, lane, np, nw, L, div, cur, cum01, cum2, hitacc, st);
+      }
+    }
+    if (lane == 0 && nw > 0) {
+      cum01[0] = make_uint2(0u, 0u);
+      cum01[nw] = make_uint2(st.T0, st.T1);
+      if (np == 3) {
+        cum2[0] = 0u;
+        cum2[nw] = st.T2;
+      }
+    }
+    wave_sync();
+
+    // ------------------------------------------------ window outputs
+    uint16_t* wout = O.win_counts + B.win_off[r] * np;
+    // telomeric window (class -5) iff !(count / width < min_density) iff
+    // count >= thr[width] (exact, host-computed); the last window may be wider
+    uint32_t thr_last = thr_full;
+    if (nw > 0) {
+      const int wl = n - (nw - 1) * L;
+      thr_last = thr[wl < tsz ? wl : tsz - 1];
+    }
+    const int nmw = (nw + 63) >> 6;
+    uint64_t* tmo = tmask + tm_base(B.win_off[r], r, np);
+    for (int p = 0; p < np; ++p) {
+      for (int ch = 0; ch < nmw; ++ch) {
+        const int i = ch * 64 + lane;
+        uint32_t cnt = 0u;
+        if (i < nw) {
+          if (p == 2) cnt = cum2[i + 1] - cum2[i];
+          else if (p == 1) cnt = cum01[i + 1].y - cum01[i].y;
+          else cnt = cum01[i + 1].x - cum01[i].x;
+          wout[p * nw + i] = (uint16_t)cnt;
+        }
+        const bool t = i < nw && cnt >= (i == nw - 1 ? thr_last : thr_full);
+        const uint64_t bal = __ballot(t);
+        if (lane == 0) tmo[p * nmw + ch] = bal;
+      }
+    }
+    if (O.hits) {
+      if constexpr (S::kRegHits) {
+#pragma unroll
+        for (int c = 0; c < S::kNHits; ++c) {
+          const uint32_t v = wave_sum_u32(lane < kOwned ? st.acc[c] : 0u);
+          if (lane == 0) O.hits[r * (uint64_t)nh + c] = v;
+        }
+      } else {
+        for (int c = 0; c < nh; ++c) {
+          const uint32_t v = wave_sum_u32(lane < kOwned ? hitacc[c * kWave + lane] : 0u);
+          if (lane == 0) O.hits[r * (uint64_t)nh + c] = v;
+        }
+      }
+    }
+    wave_sync();
+  }
+}
+
+}  // namespace nt

@@ -46,7 +46,7 @@ class NtParams(ctypes.Structure):
 
 class NtProgramInfo(ctypes.Structure):
     _fields_ = [("n_pass", ctypes.c_int32), ("n_pat", ctypes.c_int32), ("n_tvr", ctypes.c_int32),
-                ("n_hits", ctypes.c_int32), ("raw_p1", ctypes.c_int32)]
+                ("n_hits", ctypes.c_int32), ("raw_p1", ctypes.c_int32), ("jit", ctypes.c_int32)]
 
 
 class NtBatch(ctypes.Structure):
@@ -90,6 +90,9 @@ SIGNATURES = {
     "nt_pack_reads": (ctypes.c_int, [_P, _P, ctypes.c_uint64, ctypes.c_int32, ctypes.c_int32, _P, _P,
                                      _P, _P, _P, _P, _P]),
     "nt_scan_call": (ctypes.c_int, [_P, ctypes.POINTER(NtBatch), ctypes.POINTER(NtOut), ctypes.c_uint64]),
+    "nt_set_profiling": (ctypes.c_int, [_P, ctypes.c_int]),
+    "nt_kernel_times": (ctypes.c_int64, [_P, ctypes.POINTER(ctypes.c_double),
+                                         ctypes.POINTER(ctypes.c_double)]),
     "nt_analyze_host": (ctypes.c_int, [_P, _P, _P, ctypes.c_uint64, _P, _P, _P, _P, _P, _P]),
     "nt_assign_serials": (ctypes.c_int64, [_P, ctypes.c_uint64, ctypes.POINTER(ctypes.c_double),
                                            ctypes.POINTER(ctypes.c_double), _P, _P]),

@@ -54,6 +54,9 @@ class NanoTel:
         self.n_tvr = info.n_tvr
         self.n_hits = info.n_hits
         self.raw_p1 = bool(info.raw_p1)
+        # scan kernel specialised for these patterns at run time (hiprtc), or
+        # the ahead-of-time kernels (NT_JIT=0 / hiprtc unavailable)
+        self.jit = bool(info.jit)
         self.subseq_length = int(subseq_length)
 
     # ------------------------------------------------------------------
@@ -80,6 +83,16 @@ class NanoTel:
 
     def set_stream(self, stream_handle):
         _check(lib().nt_set_stream(self._h, ctypes.c_void_p(stream_handle)), self._h)
+
+    def set_profiling(self, on=True):
+        _check(lib().nt_set_profiling(self._h, int(bool(on))), self._h)
+
+    def kernel_times(self):
+        """(calls, scan_ms, call_ms): summed HIP-event spans of the scan and the
+        calling kernels over the scan_call()s since the previous query."""
+        a, b = ctypes.c_double(), ctypes.c_double()
+        n = _check(lib().nt_kernel_times(self._h, ctypes.byref(a), ctypes.byref(b)), self._h)
+        return int(n), a.value, b.value
 
     def synchronize(self):
         _check(lib().nt_synchronize(self._h), self._h)

@@ -17,9 +17,20 @@ pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
-def _nt(**kw):
+def _nt(jit=True, **kw):
+    """NanoTel context; jit=False forces the ahead-of-time scan kernels."""
     from nanotel_amd import NanoTel
-    return NanoTel(**kw)
+    old = os.environ.get("NT_JIT")
+    os.environ["NT_JIT"] = "1" if jit else "0"
+    try:
+        nt = NanoTel(**kw)
+    finally:
+        if old is None:
+            del os.environ["NT_JIT"]
+        else:
+            os.environ["NT_JIT"] = old
+    assert nt.jit == jit, "hiprtc specialisation unavailable"
+    return nt
 
 
 def _example():
@@ -99,7 +110,8 @@ def test_synthetic_generator_reads():
     dict(patterns="TTRGGG CCCTAA", tvr_patterns="TYAGGG"),
     dict(patterns="TAGGGTTAGGGTTAGGGT"),
 ])
-def test_random_reads(cfg):
+@pytest.mark.parametrize("jit", [True, False], ids=["jit", "aot"])
+def test_random_reads(cfg, jit):
     rng = np.random.default_rng(zlib.crc32(str(sorted(cfg.items())).encode()))
     seqs = []
     right = cfg.get("check_right_edge", False)
@@ -110,32 +122,35 @@ def test_random_reads(cfg):
         where = ["left", "right", "mid"][i % 3]
         seqs.append(_telo_read(rng, n, motif=motif, where=where,
                                exc=0.002 if i % 5 == 0 else 0.0, lower=0.01 if i % 7 == 0 else 0.0))
-    nt = _nt(**cfg)
+    nt = _nt(jit=jit, **cfg)
     res = nt.analyze(seqs, want_windows=True, want_hits=True)
     orow = oracle_rows(seqs, cfg["patterns"], tvr=cfg.get("tvr_patterns"), L=cfg.get("subseq_length", 100),
                        min_density=cfg.get("min_density", 0.6), right_edge=right, rc=cfg.get("rc", False))
     compare(nt, res, orow)
 
 
-def test_iupac_subject_letters_and_tiny_reads():
+@pytest.mark.parametrize("jit", [True, False], ids=["jit", "aot"])
+def test_iupac_subject_letters_and_tiny_reads(jit):
     rng = np.random.default_rng(7)
     seqs = ["A", "T", "N", "TTAGGG", "TTAGG", "NNNNNNNNNN", "TTAGGGTTAGGGTTAGGGNNNN"]
     for n in range(1, 140, 3):
         seqs.append(_telo_read(rng, n, tract=(0, n), exc=0.05))
     for pats in ("TTAGGG", "YYAGGG", "TTAGGG TCAGGG", "NNNNNN"):
-        nt = _nt(patterns=pats, tvr_patterns="TGAGGG")
+        nt = _nt(jit=jit, patterns=pats, tvr_patterns="TGAGGG")
         res = nt.analyze(seqs, want_windows=True, want_hits=True)
         compare(nt, res, oracle_rows(seqs, pats, tvr="TGAGGG"))
 
 
-def test_long_reads_global_scratch_path():
+@pytest.mark.parametrize("jit", [True, False], ids=["jit", "aot"])
+def test_long_reads_global_scratch_path(jit):
     # reads beyond the LDS budget go through the global-scratch kernel
     rng = np.random.default_rng(11)
     seqs = [_telo_read(rng, 230000, tract=(5000, 20000)), _telo_read(rng, 1200, where="left"),
             _telo_read(rng, 181000, where="right", tract=(5000, 9000))]
-    nt = _nt(patterns="TTAGGG", tvr_patterns="TTGGGG")
-    res = nt.analyze(seqs, want_windows=True, want_hits=True)
-    compare(nt, res, oracle_rows(seqs, "TTAGGG", tvr="TTGGGG"))
+    for pats, tvr in (("TTAGGG", "TTGGGG"), ("TTAGGG", None)):
+        nt = _nt(jit=jit, patterns=pats, tvr_patterns=tvr)
+        res = nt.analyze(seqs, want_windows=True, want_hits=True)
+        compare(nt, res, oracle_rows(seqs, pats, tvr=tvr))
 
 
 def test_error_behaviour():
@@ -174,3 +189,71 @@ def test_device_synth_matches_host_generator():
         hi = np.unpackbits(np.ascontiguousarray(p[r, :, 1]).view(np.uint8), bitorder="little")[:5000]
         dev = "".join("ACGT"[c] for c in (lo + 2 * hi))
         assert dev == host
+
+
+def _device_batch(nt, sp, n, read_len, L=100):
+    """Synthetic reads generated on the device + the uniform layout (bench path)."""
+    import torch
+    from nanotel_amd import read_blocks, window_count
+    nblk = read_blocks(read_len)
+    nw = window_count(read_len, L)
+    t = dict(
+        planes=torch.zeros(n * nblk * 2, dtype=torch.int32, device="cuda"),
+        blk_off=torch.empty(n, dtype=torch.int64, device="cuda"),
+        lens=torch.empty(n, dtype=torch.int32, device="cuda"),
+        win_off=torch.empty(n, dtype=torch.int64, device="cuda"),
+        wc=torch.zeros(n * nw * nt.n_pass, dtype=torch.int16, device="cuda"),
+        start=torch.empty(n * 3, dtype=torch.int32, device="cuda"),
+        end=torch.empty(n * 3, dtype=torch.int32, device="cuda"),
+        dens=torch.empty(n * 3, dtype=torch.float64, device="cuda"),
+        flags=torch.zeros(n, dtype=torch.uint8, device="cuda"),
+        hits=torch.zeros(n * nt.n_hits, dtype=torch.int32, device="cuda"),
+    )
+    nt.synth_device(sp, n, t["planes"].data_ptr())
+    nt.uniform_layout_device(n, read_len, t["blk_off"].data_ptr(), t["lens"].data_ptr(),
+                             t["win_off"].data_ptr())
+    t["nw"] = nw
+    return t
+
+
+def _run_device(nt, t, n, read_len):
+    nt.scan_call_device(t["planes"].data_ptr(), t["blk_off"].data_ptr(), t["lens"].data_ptr(),
+                        t["win_off"].data_ptr(), n, n * t["nw"], read_len, t["start"].data_ptr(),
+                        t["end"].data_ptr(), t["dens"].data_ptr(), t["flags"].data_ptr(),
+                        t["wc"].data_ptr(), hits=t["hits"].data_ptr())
+    nt.synchronize()
+
+
+@pytest.mark.parametrize("jit", [True, False], ids=["jit", "aot"])
+def test_device_resident_path_matches_host_path(jit):
+    # the bench's device-resident batch (device generator + uniform layout)
+    # against the host-packed path and, on a sample, the oracle
+    from nanotel_amd import synth_params, synth_read_ascii
+    n, read_len = 96, 50000
+    sp = synth_params(read_len=read_len, first_read=5000)
+    nt = _nt(jit=jit, patterns="TTAGGG")
+    t = _device_batch(nt, sp, n, read_len)
+    _run_device(nt, t, n, read_len)
+    seqs = [synth_read_ascii(sp, i) for i in range(n)]
+    res = nt.analyze(seqs, want_windows=True, want_hits=True)
+    assert np.array_equal(t["start"].cpu().numpy().reshape(n, 3), res["start"])
+    assert np.array_equal(t["end"].cpu().numpy().reshape(n, 3), res["end"])
+    assert np.array_equal(t["dens"].cpu().numpy().reshape(n, 3).view(np.uint64),
+                          res["density"].view(np.uint64))
+    assert np.array_equal(t["flags"].cpu().numpy(), res["flags"])
+    assert np.array_equal(t["wc"].cpu().numpy().view(np.uint16), res["win_counts"])
+    assert np.array_equal(t["hits"].cpu().numpy().view(np.uint32).reshape(n, -1), res["hits"])
+    compare(nt, res, oracle_rows(seqs[:6], "TTAGGG"))
+
+
+def test_odd_block_offset_is_reported():
+    from nanotel_amd import synth_params
+    from nanotel_amd._lib import ROW_DONE, ROW_ERR_ALIGN
+    n, read_len = 8, 3000
+    nt = _nt(patterns="TTAGGG")
+    t = _device_batch(nt, synth_params(read_len=read_len), n, read_len)
+    t["blk_off"][3] += 1
+    _run_device(nt, t, n, read_len)
+    f = t["flags"].cpu().numpy()
+    assert f[3] == (ROW_DONE | ROW_ERR_ALIGN)
+    assert all((f[i] & ROW_ERR_ALIGN) == 0 for i in range(n) if i != 3)
