@@ -21,10 +21,12 @@ extern "C" {
 uint32_t nt_dev_wave_words(int single, int n_hits, int np, uint32_t nw_cap);
 uint64_t nt_dev_tmask_words(uint64_t total_windows, uint64_t n_reads, int np);
 hipError_t nt_dev_launch(const NtProgram* prog, const uint32_t* thr, const NtBatch* B,
-                         const NtOut* O, uint64_t* tmask, uint32_t len_lo, uint32_t len_hi,
+                         const NtOut* O, uint64_t* tmask, unsigned long long* queue,
+                         uint32_t len_lo, uint32_t len_hi,
                          int single, int one, int m6, int lds, uint32_t wave_words, uint32_t* gscr,
                          int grid, int call_grid, hipStream_t stream);
 hipError_t nt_dev_set_lds_limit(uint32_t bytes);
+int nt_dev_scan_blocks_per_cu(int single, int one, int m6, int lds, size_t lds_bytes);
 hipError_t nt_dev_launch_call(const NtProgram* prog, const NtBatch* B, const NtOut* O,
                               const uint64_t* tmask, int call_grid, hipStream_t stream);
 hipError_t nt_dev_launch_synth(const NtSynth* S, uint32_t* planes, uint64_t n_reads,
@@ -34,11 +36,12 @@ hipError_t nt_dev_launch_uniform_layout(uint64_t n_reads, uint64_t nblk, uint64_
                                         uint64_t* win_off, hipStream_t stream);
 }
 
+int nt_jit_blocks_per_cu(void* fn, size_t lds_bytes);
 bool nt_jit_get(int device, const NtProgram& P, void** fn_lds, void** fn_gmem, std::string& err);
 hipError_t nt_jit_launch(void* fn, int grid, size_t lds_bytes, hipStream_t stream,
                          const NtProgram* prog, const uint32_t* thr, const NtBatch* B,
-                         const NtOut* O, uint64_t* tmask, uint32_t len_lo, uint32_t len_hi,
-                         uint32_t wave_words, uint32_t* gscr);
+                         const NtOut* O, uint64_t* tmask, unsigned long long* queue,
+                         uint32_t len_lo, uint32_t len_hi, uint32_t wave_words, uint32_t* gscr);
 
 namespace {
 
@@ -203,7 +206,7 @@ struct nt_ctx {
   NtProgram* prog_dev = nullptr;
   int cu_count = 256;
   DevBuf planes, blk_off, len, win_off, exc_off, exc_pos, exc_code;
-  DevBuf wc, start, end, dens, flags, hits, scratch, tmask, thr;
+  DevBuf wc, start, end, dens, flags, hits, scratch, tmask, thr, queue;
 };
 
 static int fail(nt_ctx* ctx, int code, const std::string& msg) {
@@ -531,6 +534,9 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
   const uint64_t call_grid = std::max<uint64_t>(1, std::min<uint64_t>((batch->n_reads + 255) / 256,
                                                                       (uint64_t)ctx->cu_count * 64));
   const bool two = len_cap < max_len;
+  // read queues of the two scan launches (zeroed on the stream, 8 B each)
+  if ((e = ctx->queue.ensure(16)) != hipSuccess) return hip_fail(ctx, e, "hipMalloc(queue)");
+  unsigned long long* queue = (unsigned long long*)ctx->queue.p;
   hipEvent_t* ev = nullptr;
   if (ctx->profile) {
     if (ctx->n_ev == ctx->ev.size()) {
@@ -542,16 +548,21 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
     ev = ctx->ev[ctx->n_ev++].data();
     (void)hipEventRecord(ev[0], ctx->stream);
   }
+  if ((e = hipMemsetAsync(queue, 0, 16, ctx->stream)) != hipSuccess) return hip_fail(ctx, e, "hipMemsetAsync(queue)");
   {
     const uint32_t ww = nt_dev_wave_words(noslots, nh, np, cap_nw);
-    const uint64_t per_wg = std::max<uint64_t>((uint64_t)ww * 16u, 1);
-    const uint64_t bpc = std::min<uint64_t>(8, std::max<uint64_t>(1, (160u * 1024u) / per_wg));
+    const size_t lds_bytes = (size_t)ww * 4u * 4u;
+    // exactly the resident blocks (the waves stride over the reads): a grid
+    // beyond one resident round would start its tail blocks late
+    int bpc = ctx->jit ? nt_jit_blocks_per_cu(ctx->jit_lds, lds_bytes)
+                       : nt_dev_scan_blocks_per_cu(single, one, m6, 1, lds_bytes);
+    if (bpc <= 0) bpc = 1;
     const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((batch->n_reads + 3) / 4, (uint64_t)ctx->cu_count * bpc));
     if (ctx->jit)
-      e = nt_jit_launch(ctx->jit_lds, (int)grid, (size_t)ww * 4u * 4u, ctx->stream, ctx->prog_dev,
-                        (const uint32_t*)ctx->thr.p, &B, &O, tmask, 0u, (uint32_t)len_cap, ww, nullptr);
+      e = nt_jit_launch(ctx->jit_lds, (int)grid, lds_bytes, ctx->stream, ctx->prog_dev,
+                        (const uint32_t*)ctx->thr.p, &B, &O, tmask, queue, 0u, (uint32_t)len_cap, ww, nullptr);
     else
-      e = nt_dev_launch(ctx->prog_dev, (const uint32_t*)ctx->thr.p, &B, &O, tmask, 0u, (uint32_t)len_cap,
+      e = nt_dev_launch(ctx->prog_dev, (const uint32_t*)ctx->thr.p, &B, &O, tmask, queue, 0u, (uint32_t)len_cap,
                         single, one, m6, 1, ww, nullptr, (int)grid, 0, ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, e, "launch nt_scan_kernel<lds>");
   }
@@ -561,9 +572,9 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
     if ((e = ctx->scratch.ensure(grid * 4 * (uint64_t)ww * 4)) != hipSuccess) return hip_fail(ctx, e, "hipMalloc(scratch)");
     if (ctx->jit)
       e = nt_jit_launch(ctx->jit_gmem, (int)grid, 0, ctx->stream, ctx->prog_dev, (const uint32_t*)ctx->thr.p,
-                        &B, &O, tmask, (uint32_t)len_cap, 0xFFFFFFFFu, ww, (uint32_t*)ctx->scratch.p);
+                        &B, &O, tmask, queue + 1, (uint32_t)len_cap, 0xFFFFFFFFu, ww, (uint32_t*)ctx->scratch.p);
     else
-      e = nt_dev_launch(ctx->prog_dev, (const uint32_t*)ctx->thr.p, &B, &O, tmask, (uint32_t)len_cap, 0xFFFFFFFFu,
+      e = nt_dev_launch(ctx->prog_dev, (const uint32_t*)ctx->thr.p, &B, &O, tmask, queue + 1, (uint32_t)len_cap, 0xFFFFFFFFu,
                         single, 0, 0, 0, ww, (uint32_t*)ctx->scratch.p, (int)grid, 0, ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, e, "launch nt_scan_kernel<global>");
   }

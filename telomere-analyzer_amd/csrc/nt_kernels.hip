@@ -37,12 +37,12 @@ namespace nt {
 template <class S, bool kLds>
 __global__ void __launch_bounds__(kWG)
 nt_scan_kernel(const NtProgram* __restrict__ prog, const uint32_t* __restrict__ thr, NtBatch B,
-               NtOut O, uint64_t* __restrict__ tmask, uint32_t len_lo, uint32_t len_hi,
-               uint32_t wave_words, uint32_t* __restrict__ gscr) {
+               NtOut O, uint64_t* __restrict__ tmask, unsigned long long* __restrict__ queue,
+               uint32_t len_lo, uint32_t len_hi, uint32_t wave_words, uint32_t* __restrict__ gscr) {
   extern __shared__ uint32_t smem[];
   const uint64_t gw = (uint64_t)blockIdx.x * kNWaves + (threadIdx.x >> 6);
   uint32_t* wmem = kLds ? smem + (uint64_t)(threadIdx.x >> 6) * wave_words : gscr + gw * wave_words;
-  scan_reads<S, kLds>(prog, thr, B, O, tmask, len_lo, len_hi, wmem);
+  scan_reads<S, kLds>(prog, thr, B, O, tmask, queue, len_lo, len_hi, wmem);
 }
 
 // ================================================================= call
@@ -538,7 +538,8 @@ hipError_t nt_dev_set_lds_limit(uint32_t bytes) {
 
 // single: 1 pattern, no TVR; one: one-hot letters; m6: 6 letters
 hipError_t nt_dev_launch(const NtProgram* prog, const uint32_t* thr, const NtBatch* B,
-                         const NtOut* O, uint64_t* tmask, uint32_t len_lo, uint32_t len_hi,
+                         const NtOut* O, uint64_t* tmask, unsigned long long* queue,
+                         uint32_t len_lo, uint32_t len_hi,
                          int single, int one, int m6, int lds, uint32_t wave_words, uint32_t* gscr,
                          int grid, int call_grid, hipStream_t stream) {
   const size_t lds_bytes = lds ? (size_t)wave_words * 4u * nt::kNWaves : 0;
@@ -546,7 +547,8 @@ hipError_t nt_dev_launch(const NtProgram* prog, const uint32_t* thr, const NtBat
 #define NT_LAUNCH(S, G, SI, O_, M)                                                             \
   if (!done && single == SI && lds == (int)G && (O_ < 0 || one == O_) && (M < 0 || m6 == M)) { \
     hipLaunchKernelGGL((nt::nt_scan_kernel<S, G>), dim3(grid), dim3(nt::kWG), lds_bytes,       \
-                       stream, prog, thr, *B, *O, tmask, len_lo, len_hi, wave_words, gscr);    \
+                       stream, prog, thr, *B, *O, tmask, queue, len_lo, len_hi, wave_words,    \
+                       gscr);                                                                  \
     done = true;                                                                               \
   }
   NT_SCAN_VARIANTS(NT_LAUNCH)
@@ -555,6 +557,22 @@ hipError_t nt_dev_launch(const NtProgram* prog, const uint32_t* thr, const NtBat
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || call_grid <= 0) return e;
   return nt_dev_launch_call(prog, B, O, tmask, call_grid, stream);
+}
+
+// resident 256-thread blocks per CU of the scan variant (grid sizing)
+int nt_dev_scan_blocks_per_cu(int single, int one, int m6, int lds, size_t lds_bytes) {
+  int nb = 0;
+  bool done = false;
+#define NT_OCC(S, G, SI, O_, M)                                                                \
+  if (!done && single == SI && lds == (int)G && (O_ < 0 || one == O_) && (M < 0 || m6 == M)) { \
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, nt::nt_scan_kernel<S, G>, nt::kWG,   \
+                                                     lds_bytes) != hipSuccess)                 \
+      nb = 0;                                                                                  \
+    done = true;                                                                               \
+  }
+  NT_SCAN_VARIANTS(NT_OCC)
+#undef NT_OCC
+  return nb;
 }
 
 hipError_t nt_dev_launch_call(const NtProgram* prog, const NtBatch* B, const NtOut* O,

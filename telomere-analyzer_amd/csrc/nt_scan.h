@@ -509,9 +509,9 @@ template <class S, bool kLds>
 __device__ __forceinline__ void scan_reads(const NtProgram* __restrict__ prog,
                                            const uint32_t* __restrict__ thr, const NtBatch& B,
                                            const NtOut& O, uint64_t* __restrict__ tmask,
+                                           unsigned long long* __restrict__ queue,
                                            uint32_t len_lo, uint32_t len_hi, uint32_t* wmem) {
-  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x >> 6;
-  const uint64_t gw = (uint64_t)blockIdx.x * kNWaves + wave, GW = (uint64_t)gridDim.x * kNWaves;
+  const int lane = threadIdx.x & (kWave - 1);
   const int np = S::kNPass ? S::kNPass : prog->n_pass;
   const int nh = S::kRegHits ? S::kNHits : prog->n_hits, L = prog->L;
   uint32_t* hitacc = wmem;
@@ -519,7 +519,22 @@ __device__ __forceinline__ void scan_reads(const NtProgram* __restrict__ prog,
   const DivL div{prog->div32_m, prog->div32_s};
   const uint32_t thr_full = thr[L < tsz ? L : tsz - 1];
 
-  for (uint64_t r = gw; r < B.n_reads; r += GW) {
+  // dynamic read queue: each wave claims kClaim reads at a time (the next
+  // claim is issued before the current reads are scanned), so waves that
+  // start late or draw short reads simply take fewer
+  constexpr uint64_t kClaim = 4;
+  auto claim = [&]() -> uint64_t {
+    unsigned long long v = 0;
+    if (lane == 0) v = atomicAdd(queue, (unsigned long long)kClaim);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+  };
+  uint64_t cur = claim();
+  while (cur < B.n_reads) {
+  const uint64_t nxt = claim();
+  const uint64_t r_end = cur + kClaim < B.n_reads ? cur + kClaim : B.n_reads;
+  for (uint64_t r = cur; r < r_end; ++r) {
     const uint32_t n32 = B.len[r];
     if (n32 <= len_lo || n32 > len_hi) continue;
     const uint64_t boff = B.blk_off[r];
@@ -619,6 +634,8 @@ __device__ __forceinline__ void scan_reads(const NtProgram* __restrict__ prog,
       }
     }
     wave_sync();
+  }
+  cur = nxt;
   }
 }
 
