@@ -387,8 +387,14 @@ __device__ void call_pass(const Lane& c, int& out_s, int& out_e, double& out_d, 
   out_d = sub_density(c, tp.s, tp.e);
 }
 
-// One lane per read (grid-stride over reads).
-__global__ void __launch_bounds__(256)
+// One lane per read (grid-stride over reads).  The kernel is memory-latency
+// bound: NT_CALL_WAVES_PER_EU caps the VGPRs for occupancy (4 waves/SIMD
+// measured best: 1.96 -> 1.57 ms at c50k; 3: 1.71, 5: 1.76).
+#ifndef NT_CALL_WAVES_PER_EU
+#define NT_CALL_WAVES_PER_EU 4
+#endif
+#define NT_CALL_ATTR __attribute__((amdgpu_waves_per_eu(NT_CALL_WAVES_PER_EU)))
+__global__ void __launch_bounds__(256) NT_CALL_ATTR
 nt_call_kernel(const NtProgram* __restrict__ prog, NtBatch B, NtOut O,
                const uint64_t* __restrict__ tmask) {
   const int np = prog->n_pass, L = prog->L;
