@@ -1,0 +1,107 @@
+"""Multi-GPU sharding of NanoTel's chunk stream.
+
+The reference reads its input as a stream of `nrec`-record chunks
+(run_future_worker_chuncks, NanoTel.R:2171-2268); reads are independent, so
+chunks are dealt round-robin to ranks (one process per GPU) and scanned with no
+collective on the data path.  The only cross-chunk dependency of the output is
+the Serial column (A15):
+
+  * inside a chunk, serials are offsets from the chunk's serial_start that
+    depend only on that chunk's telomeric flags (the 8-way split,
+    NanoTel.R:2234-2254) -- nt_assign_serials with serial_start = 0;
+  * serial_start(chunk k+1) = max(Serial of chunks <= k) + 1, which is -Inf
+    while no row exists yet (max(numeric(0)), NanoTel.R:2258).
+
+So each rank publishes, per chunk it owns, the chunk's largest relative serial
+(-Inf for a chunk without rows); one all-reduce(MAX) of that n_chunks vector
+(8 bytes per chunk; every other rank contributes -Inf) gives every rank all of
+them, and the serial_starts follow from a sequential scan that reproduces the
+reference's fp64 arithmetic exactly.  Rows then go to rank 0 in chunk order.
+"""
+import numpy as np
+
+from .api import assign_serials
+
+NEG_INF = float("-inf")
+
+
+def owner(chunk, world):
+    """Rank that scans chunk `chunk` (round-robin)."""
+    return chunk % world
+
+
+def local_chunks(n_chunks, rank, world):
+    return list(range(rank, n_chunks, world))
+
+
+def chunk_relative(is_telo):
+    """Serials of one chunk relative to serial_start = 0.
+
+    Returns (rel_serials (n,) float64, NaN for non-telomeric reads;
+    row_order (rows,) int64 -- the reference's group-major row order;
+    rel_max float: largest relative serial, -Inf without rows)."""
+    ser, order, _, mx = assign_serials(is_telo, serial_start=0.0, max_serial=NEG_INF)
+    return ser, order, mx
+
+
+def serial_starts(rel_max):
+    """serial_start of every chunk from the chunks' relative maxima, in chunk
+    order: S_0 = 1; M_k = max(M_{k-1}, S_k + rel_max_k); S_{k+1} = M_k + 1.
+    Same fp64 operations as the reference's running max(Serial) + 1."""
+    starts = np.empty(len(rel_max), np.float64)
+    s, m = 1.0, NEG_INF
+    for k, r in enumerate(rel_max):
+        starts[k] = s
+        v = s + r
+        if v > m:
+            m = v
+        s = m + 1.0
+    return starts
+
+
+def exchange_rel_max(local, n_chunks, group=None, device=None):
+    """All ranks' per-chunk relative maxima: local = {chunk: rel_max} for the
+    chunks this rank owns.  One all_reduce(MAX) over an n_chunks float64
+    vector (gloo on CPU tensors, RCCL on device tensors)."""
+    import torch
+    import torch.distributed as dist
+    t = torch.full((n_chunks,), NEG_INF, dtype=torch.float64,
+                   device=device if device is not None else "cpu")
+    for k, v in local.items():
+        t[k] = v
+    if dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return t.cpu().numpy()
+
+
+def assign_chunk_serials(rel, start):
+    """Absolute serials of one chunk: start + relative offsets (NaN stays)."""
+    return start + rel
+
+
+def gather_rows(local_rows, group=None, dst=0):
+    """Gather {chunk: rows} from every rank to dst; returns the rows
+    concatenated in chunk order on dst (None elsewhere)."""
+    import torch.distributed as dist
+    if not (dist.is_initialized() and dist.get_world_size(group) > 1):
+        return [r for _, rows in sorted(local_rows.items()) for r in rows]
+    world = dist.get_world_size(group)
+    out = [None] * world if dist.get_rank(group) == dst else None
+    dist.gather_object(local_rows, out, dst=dst, group=group)
+    if out is None:
+        return None
+    merged = {}
+    for part in out:
+        merged.update(part)
+    return [r for _, rows in sorted(merged.items()) for r in rows]
+
+
+def sequential_serials(flags_per_chunk):
+    """Reference recurrence run chunk by chunk in one process (the oracle for
+    the sharded path): list of per-chunk absolute serial arrays."""
+    ss, mx = 1.0, NEG_INF
+    out = []
+    for f in flags_per_chunk:
+        ser, _, ss, mx = assign_serials(f, serial_start=ss, max_serial=mx)
+        out.append(ser)
+    return out
