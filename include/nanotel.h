@@ -164,6 +164,22 @@ int nt_analyze_host(nt_ctx* ctx, const char* const* seqs, const uint64_t* lens, 
 int64_t nt_assign_serials(const uint8_t* is_telo, uint64_t n, double* serial_start_io,
                           double* max_serial_io, double* serial_out, int64_t* order_out);
 
+/* --- host ingest: FASTA/FASTQ(.gz) in nrec-record chunks ------------------ */
+/* readDNAStringSet(open_input_files(path), nrec, format) (NanoTel.R:2171-2216):
+ * path = a file or a directory (files listed recursively, sorted, read as one
+ * record stream); format 0 = fasta, 1 = fastq; gzip transparent.  A chunk's
+ * names/sequences stay valid until the next nt_reader_next / close.
+ * Returns the number of records (0 at the end) or < 0 (nt_reader_error). */
+typedef struct nt_reader nt_reader;
+int nt_reader_open(const char* path, int format, nt_reader** out);
+void nt_reader_close(nt_reader* r);
+uint64_t nt_reader_file_count(const nt_reader* r);
+const char* nt_reader_file(const nt_reader* r, uint64_t i);
+const char* nt_reader_error(const nt_reader* r);
+int64_t nt_reader_next(nt_reader* r, uint64_t nrec, const char* const** names,
+                       const uint64_t** name_lens, const char* const** seqs,
+                       const uint64_t** seq_lens);
+
 /* --- synthetic long reads (bench / tests) --------------------------------- */
 int nt_synth_device(nt_ctx* ctx, const nt_synth_params* sp, uint64_t n_reads, uint32_t* planes_dev);
 int nt_uniform_layout_device(nt_ctx* ctx, uint64_t n_reads, uint64_t read_len, int32_t subseq_length,

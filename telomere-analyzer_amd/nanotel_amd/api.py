@@ -108,6 +108,15 @@ class NanoTel:
         """
         bseqs = [s.encode() if isinstance(s, str) else bytes(s) for s in seqs]
         n = len(bseqs)
+        ptrs = (ctypes.c_char_p * max(1, n))(*bseqs)
+        lens = np.array([len(b) for b in bseqs], np.uint64)
+        return self._analyze(ctypes.addressof(ptrs), lens, n, want_windows, want_hits)
+
+    def analyze_chunk(self, chunk, want_windows=False, want_hits=False):
+        """analyze() of an io.Reader chunk, zero-copy (the reader's buffers)."""
+        return self._analyze(chunk.seq_ptrs, chunk.lengths, chunk.n, want_windows, want_hits)
+
+    def _analyze(self, ptrs_addr, lens, n, want_windows, want_hits):
         out = {
             "start": np.full((n, 3), -1, np.int32),
             "end": np.full((n, 3), -1, np.int32),
@@ -118,8 +127,7 @@ class NanoTel:
             out["width"] = np.zeros((0, 3), np.int64)
             out["telomeric"] = np.zeros(0, bool)
             return out
-        ptrs = (ctypes.c_char_p * n)(*bseqs)
-        lens = np.array([len(b) for b in bseqs], np.uint64)
+        lens = np.ascontiguousarray(lens, np.uint64)
         wc = None
         if want_windows:
             nw = np.array([window_count(int(x), self.subseq_length) for x in lens], np.int64)
@@ -130,7 +138,7 @@ class NanoTel:
             out["n_windows"] = nw
         hits = np.zeros((n, max(1, self.n_hits)), np.uint32) if want_hits else None
         rc = lib().nt_analyze_host(
-            self._h, ctypes.cast(ptrs, ctypes.c_void_p), lens.ctypes.data, n,
+            self._h, ctypes.c_void_p(ptrs_addr), lens.ctypes.data, n,
             out["start"].ctypes.data, out["end"].ctypes.data, out["density"].ctypes.data,
             out["flags"].ctypes.data, None if wc is None else wc.ctypes.data,
             None if hits is None else hits.ctypes.data)

@@ -1,0 +1,82 @@
+"""Command line of the MI355X NanoTel: the flags of NanoTel.R's optparse
+block (NanoTel.R:30-93) and its argument checks (NanoTel.R:104-137).
+
+    python -m nanotel_amd -i reads.fastq.gz --save_path out --patterns "TTAGGG"
+
+Multi-GPU: launch one process per GPU with torch.distributed.run; chunks are
+dealt round-robin to the ranks (driver.py / shard.py), rank 0 writes the
+summary.  --use_filter, --analysis and the plots are not part of this build.
+"""
+import argparse
+import os
+import sys
+
+from .driver import VERSION, run
+
+
+def parser():
+    ap = argparse.ArgumentParser(prog="nanotel_amd", description="Telomere Analyzer (MI355X hot path)")
+    ap.add_argument("-i", "--input_path", default=None, help="Path to input files.( dir or single file)")
+    ap.add_argument("--save_path", default=None, help="A path to a directory for storing the output files.")
+    ap.add_argument("--format", default="fastq",
+                    help='input files format (Either "fastq" (the default) or "fasta", gzip is supported)')
+    ap.add_argument("-n", "--nrec", type=int, default=10000,
+                    help="The maximum of number of records to read in to memory for each iteration.")
+    ap.add_argument("-r", "--rc", action="store_true", help="Should we do reverse complement on the given reads.")
+    ap.add_argument("--patterns", default=None, help="Space separated list of pattern(s).")
+    ap.add_argument("--min_density", type=float, default=0.6,
+                    help="Minimal density to consider a subsequence as a pattern region.")
+    ap.add_argument("--subseq_length", type=int, default=100, help="The length of the sub-sequence.")
+    ap.add_argument("--use_filter", action="store_true", help="Filter reads accoding to the edge.")
+    ap.add_argument("--check_right_edge", action="store_true",
+                    help="The expected telomere is at the right edge of the reads.")
+    ap.add_argument("--tvr_patterns", default=None,
+                    help="Space separated list of additional pattern(s) for Telomere variant repeats.")
+    ap.add_argument("--version", action="store_true", help="Print version information and exit")
+    ap.add_argument("--analysis", action="store_true", help="Post-processing (not part of this build).")
+    # build-specific
+    ap.add_argument("--device", type=int, default=None, help="GPU index (default: LOCAL_RANK or 0)")
+    ap.add_argument("--no_reads", action="store_true", help="do not write reads/<serial>.fasta.gz")
+    ap.add_argument("--legacy_no_ext", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--readr_sci_threshold", type=float, default=None, help=argparse.SUPPRESS)
+    return ap
+
+
+def main(argv=None):
+    a = parser().parse_args(argv)
+    if a.version:
+        print(VERSION)
+        return 0
+    if a.patterns is None:
+        sys.exit("Error: Missing required parameter:  --patterns")
+    if a.save_path is None:
+        sys.exit("Error: Missing required parameter:  --save_path")
+    if a.input_path is None:
+        sys.exit("Error: Missing required parameter:  --input_path")
+    if a.format not in ("fasta", "fastq"):
+        sys.exit("Error: Format should be a string fastq or fasta")
+    if a.use_filter or a.analysis:
+        sys.exit("Error: --use_filter / --analysis are not supported by this build")
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = a.device if a.device is not None else local
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(dev)
+        dist.init_process_group("nccl")
+    try:
+        run(a.input_path, a.save_path, a.patterns, fmt=a.format, nrec=a.nrec, rc=a.rc,
+            min_density=a.min_density, subseq_length=a.subseq_length,
+            check_right_edge=a.check_right_edge, tvr_patterns=a.tvr_patterns,
+            legacy_no_ext=a.legacy_no_ext, device=dev, write_reads=not a.no_reads,
+            sci_threshold=a.readr_sci_threshold)
+    finally:
+        if world > 1:
+            import torch.distributed as dist
+            dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,190 @@
+"""The NanoTel run driver over the MI355X hot path.
+
+Mirrors run_future_worker_chuncks + the main script of NanoTel.R
+(NanoTel.R:2171-2268, 2304-2433): stream the input in `nrec`-record chunks,
+scan + call every chunk on the GPU (one nt_analyze_host per chunk, which
+replaces the 8 forked search_patterns of NanoTel.R:2234-2258), assign serials
+(A15), write reads/<serial>.fasta.gz for telomeric reads (NanoTel.R:1869-1873),
+then <basename>_summary.csv, reads_ids.txt and run.log (NanoTel.R:2340-2433).
+
+With torch.distributed initialised (one process per GPU), chunks are dealt
+round-robin to ranks and the serials are fixed by one all_reduce (shard.py);
+rank 0 writes the summary.  Plots, --analysis and --use_filter are out of
+scope of this build.
+"""
+import os
+import time
+
+import numpy as np
+
+from . import shard
+from .api import NanoTel
+from .io import Reader, csv_field, format_double, format_int, r_as_character, write_fasta_gz
+
+VERSION = "Telomere Analyzer  version v1.1.9-beta 2026-02-19"
+
+BASE_COLUMNS = ["Serial", "sequence_ID", "sequence_length", "telo_density", "Telomere_start",
+                "Telomere_end", "Telomere_length", "telo_density_mismatch", "Telomere_start_mismatch",
+                "Telomere_end_mismatch", "Telomere_length_mismatch"]
+TVR_COLUMNS = ["telo_density_mismatch_tvr", "Telomere_start_mismatch_tvr", "Telomere_end_mismatch_tvr",
+               "Telomere_length_mismatch_tvr"]
+
+_COMP = bytes.maketrans(b"ACGTMRWSYKVHDBNacgtmrwsykvhdbn", b"TGCAKYWSRMBDHVNtgcakywsrmbdhvn")
+
+
+def reverse_complement(seq):
+    """Biostrings reverseComplement on bytes (A14; the written reads are the
+    RC'd reads under --rc, NanoTel.R:2219-2221)."""
+    return seq.translate(_COMP)[::-1]
+
+
+def columns(tvr):
+    return BASE_COLUMNS + (TVR_COLUMNS if tvr else [])
+
+
+def chunk_rows(res, names, lengths, serials, order, n_pass):
+    """Summary rows of one chunk in the reference's row order (analyze_read's
+    row, NanoTel.R:1920-1974): per pass start/end/length/density, NA when the
+    pass found no telomere (start == -1)."""
+    rows = []
+    for j in order:
+        j = int(j)
+        row = [float(serials[j]), names[j], int(lengths[j])]
+        for p in range(n_pass):
+            s, e = int(res["start"][j, p]), int(res["end"][j, p])
+            if s == -1:
+                row += [None, None, None, None]
+            else:
+                row += [float(res["density"][j, p]), s, e, e - s + 1]
+        rows.append(row)
+    return rows
+
+
+def format_row(row, sci_threshold=None):
+    out = [format_double(row[0], sci_threshold), csv_field(row[1]), format_int(row[2])]
+    for k in range(3, len(row), 4):
+        d, s, e, w = row[k:k + 4]
+        out += [format_double(d) if d is not None else "NA", format_int(s), format_int(e), format_int(w)]
+    return ",".join(out)
+
+
+def write_summary_csv(path, rows, tvr, sci_threshold=None):
+    """write_csv(df_summary, <basename>_summary.csv) (NanoTel.R:2430-2432)."""
+    with open(path, "w", newline="") as f:
+        f.write(",".join(columns(tvr)) + "\n")
+        for r in rows:
+            f.write(format_row(r, sci_threshold) + "\n")
+
+
+def _summary_stats(v):
+    """R summary(): Min, 1st Qu., Median, Mean, 3rd Qu., Max (type-7 quantiles)."""
+    v = np.asarray([x for x in v if x is not None], np.float64)
+    if v.size == 0:
+        return "no values"
+    q = np.quantile(v, [0, 0.25, 0.5, 0.75, 1.0])
+    return (f"Min. {q[0]:g}  1st Qu. {q[1]:g}  Median {q[2]:g}  Mean {v.mean():g}  "
+            f"3rd Qu. {q[3]:g}  Max. {q[4]:g}")
+
+
+def run(input_path, save_path, patterns, fmt="fastq", nrec=10000, rc=False, min_density=0.6,
+        subseq_length=100, check_right_edge=False, tvr_patterns=None, legacy_no_ext=False,
+        device=0, write_reads=True, sci_threshold=None, log=print):
+    """Run the pipeline; returns (summary rows, all read lengths) on rank 0."""
+    import torch.distributed as dist
+    dist_on = dist.is_available() and dist.is_initialized()
+    rank = dist.get_rank() if dist_on else 0
+    world = dist.get_world_size() if dist_on else 1
+    os.makedirs(save_path, exist_ok=True)
+    reads_dir = os.path.join(save_path, "reads")
+    os.makedirs(reads_dir, exist_ok=True)
+    nt = NanoTel(patterns=patterns, tvr_patterns=tvr_patterns, subseq_length=subseq_length,
+                 min_density=min_density, check_right_edge=check_right_edge, rc=rc,
+                 legacy_no_ext=legacy_no_ext, device=device)
+    tvr = tvr_patterns is not None
+    rdr = Reader(input_path, fmt)
+    files = rdr.files()
+    lengths_all = []
+    local_rows = {}
+    k = 0  # global chunk index
+    s_next, m_run = 1.0, shard.NEG_INF  # serial_start of the next chunk, running max(Serial)
+    t0 = time.time()
+    # rounds of `world` chunks: rank r scans chunk r of the round; one
+    # all_reduce per round fixes the serial_starts, so the stream is processed
+    # with O(1) state (every rank parses the stream to stay in step)
+    while True:
+        own = None
+        n_round = 0
+        for r in range(world):
+            ch = rdr.next_chunk(nrec)
+            if ch is None:
+                break
+            n_round += 1
+            lengths_all.append(ch.lengths.copy())
+            if r == rank:
+                log(f"processing chunk {k + r + 1} ...")
+                res = nt.analyze_chunk(ch)
+                rel, order, rmax = shard.chunk_relative(res["telomeric"])
+                seqs = {int(j): ch.seq(int(j)) for j in order} if write_reads else {}
+                own = (r, rel, order, rmax, res, ch.names(), ch.lengths.copy(), seqs)
+        if n_round == 0:
+            break
+        maxima = shard.exchange_rel_max({own[0]: own[3]} if own else {}, n_round)
+        starts = np.empty(n_round, np.float64)
+        for r in range(n_round):  # the reference's recurrence, chunk by chunk
+            starts[r] = s_next
+            v = s_next + maxima[r]
+            if v > m_run:
+                m_run = v
+            s_next = m_run + 1.0
+        if own is not None:
+            r, rel, order, _, res, names, lens, seqs = own
+            ser = shard.assign_chunk_serials(rel, starts[r])
+            local_rows[k + r] = chunk_rows(res, names, lens, ser, order, nt.n_pass)
+            if write_reads:
+                for j in order:
+                    j = int(j)
+                    seq = reverse_complement(seqs[j]) if rc else seqs[j]
+                    write_fasta_gz(os.path.join(reads_dir, f"{r_as_character(float(ser[j]))}.fasta.gz"),
+                                   names[j], seq)
+        k += n_round
+        if n_round < world:
+            break
+    rows = shard.gather_rows(local_rows)
+    rdr.close()
+    nt.close()
+    if rank != 0:
+        return None, None
+    lengths = np.concatenate(lengths_all) if lengths_all else np.zeros(0, np.uint64)
+    barcode = os.path.basename(os.path.normpath(os.path.abspath(input_path)))
+    write_summary_csv(os.path.join(save_path, f"{barcode}_summary.csv"), rows, tvr, sci_threshold)
+    with open(os.path.join(save_path, "reads_ids.txt"), "w") as f:
+        for r in rows:
+            f.write(r[1] + "\n")
+    with open(os.path.join(save_path, "run.log"), "w") as f:
+        f.write(VERSION + "\n")
+        f.write(f"Work started at: {time.strftime('%Y-%m-%d %H:%M:%S', time.localtime(t0))}\n")
+        f.write("############### The input argumetns for this run: ################\n")
+        if rc:
+            f.write("Reverse complement was applied on the input reads.\n")
+        f.write(f"The patterns to search: {patterns}\n")
+        f.write(f"The sub-sequence length  is: {subseq_length}\n")
+        f.write(f"The minimal density for a telomeric subseq: {min_density}\n")
+        if tvr:
+            f.write(f"Additional Telomere variant repeats patterns were added: {tvr_patterns}\n")
+        f.write("##################################################################\n")
+        f.write("The input files:\n")
+        for p in files:
+            f.write(p + "\n")
+        f.write(f"Total reads in sample: {lengths.size}\n")
+        f.write(f"Summary statistics of the sample reads length: {_summary_stats(lengths)}\n")
+        f.write(f"Number of reads which identified as Telomeric: {len(rows)}\n")
+        pct = round(100 * len(rows) / lengths.size, 2) if lengths.size else float("nan")
+        f.write(f"% of total reads: {pct}%\n")
+        f.write(f"Telomere length: {_summary_stats([r[6] for r in rows])}\n")
+        f.write(f"Telomere length with 1 mismatch allowed: {_summary_stats([r[10] for r in rows])}\n")
+        if tvr:
+            f.write("Telomere length with 1 mismatch allowed + tvr patterns.: "
+                    f"{_summary_stats([r[14] for r in rows])}\n")
+        f.write(f"Work ended at: {time.strftime('%Y-%m-%d %H:%M:%S')} "
+                f"({time.time() - t0:.1f} s, {world} GPU(s))\n")
+    return rows, lengths

@@ -1,0 +1,161 @@
+"""Host ingest and outputs of the NanoTel driver.
+
+* `Reader`: FASTA/FASTQ(.gz) records in `nrec` chunks through the library's
+  C++ reader (nt_reader_*; open_input_files + readDNAStringSet(nrec),
+  NanoTel.R:2171-2216).  A chunk hands the read pointers straight to
+  nt_analyze_host (no Python copies of the sequences).
+* `format_double` / `write_summary_csv`: the summary.csv writer (write_csv,
+  NanoTel.R:2430-2432).  readr 2.1.4's number formatting is not available
+  offline: doubles are written as the shortest round-trip decimal, integral
+  values without a fraction ("1", not "1.0"), NA as "NA" -- which reproduces
+  Example_output/summary.csv byte for byte; the scientific switch for large
+  integral doubles (readr may write 1e5 as "1e5") is `sci_threshold`.
+* `r_as_character`: R's as.character()/toString() of a double (15
+  significant digits, fixed unless the scientific form is narrower), used for
+  the reads/<serial>.fasta.gz file names (NanoTel.R:1871).
+* `write_fasta_gz`: writeXStringSet(..., compress = TRUE): 80-column FASTA.
+"""
+import ctypes
+import gzip
+import math
+import os
+
+import numpy as np
+
+from ._lib import NanoTelError, lib
+
+
+class Chunk:
+    """One nt_reader_next() chunk; valid until the reader advances."""
+
+    def __init__(self, n, names_p, name_lens_p, seqs_p, seq_lens_p):
+        self.n = int(n)
+        self._names_p = names_p
+        self._name_lens = np.ctypeslib.as_array(ctypes.cast(name_lens_p, ctypes.POINTER(ctypes.c_uint64)),
+                                                shape=(self.n,)) if self.n else np.zeros(0, np.uint64)
+        self.seq_ptrs = seqs_p.value or 0  # address of const char*[n]
+        self.seq_lens_addr = seq_lens_p.value or 0
+        self.lengths = np.ctypeslib.as_array(ctypes.cast(seq_lens_p, ctypes.POINTER(ctypes.c_uint64)),
+                                             shape=(self.n,)) if self.n else np.zeros(0, np.uint64)
+        self._np = ctypes.cast(names_p, ctypes.POINTER(ctypes.c_void_p))
+        self._sp = ctypes.cast(seqs_p, ctypes.POINTER(ctypes.c_void_p))
+
+    def name(self, i):
+        return ctypes.string_at(self._np[i], int(self._name_lens[i])).decode("utf-8", "replace")
+
+    def names(self):
+        return [self.name(i) for i in range(self.n)]
+
+    def seq(self, i):
+        return ctypes.string_at(self._sp[i], int(self.lengths[i]))
+
+
+class Reader:
+    def __init__(self, path, fmt="fastq"):
+        if fmt not in ("fasta", "fastq"):
+            raise ValueError("Format should be a string fastq or fasta")
+        h = ctypes.c_void_p()
+        rc = lib().nt_reader_open(os.fsencode(path), 0 if fmt == "fasta" else 1, ctypes.byref(h))
+        if rc != 0:
+            raise NanoTelError(rc, f"cannot open input {path!r}")
+        self._h = h
+
+    def files(self):
+        L = lib()
+        return [L.nt_reader_file(self._h, i).decode() for i in range(L.nt_reader_file_count(self._h))]
+
+    def next_chunk(self, nrec):
+        a, b, c, d = (ctypes.c_void_p() for _ in range(4))
+        n = lib().nt_reader_next(self._h, int(nrec), ctypes.byref(a), ctypes.byref(b), ctypes.byref(c),
+                                 ctypes.byref(d))
+        if n < 0:
+            raise NanoTelError(int(n), lib().nt_reader_error(self._h).decode())
+        if n == 0:
+            return None
+        return Chunk(n, a, b, c, d)
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            lib().nt_reader_close(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+
+# ---------------------------------------------------------------- formatting
+
+def format_double(x, sci_threshold=None):
+    """write_csv formatting of a double: shortest round-trip digits; integral
+    values without '.0'; NA/NaN -> "NA".  sci_threshold: integral values with
+    |x| >= threshold and trailing zeros are written as "<digits>e<exp>"
+    (readr/grisu style, parity unpinned); None keeps them fixed."""
+    if x is None or (isinstance(x, float) and math.isnan(x)):
+        return "NA"
+    if math.isinf(x):
+        return "Inf" if x > 0 else "-Inf"
+    if x == int(x) and abs(x) < 1e15:
+        i = int(x)
+        if sci_threshold is not None and abs(i) >= sci_threshold and i % 10 == 0:
+            s = str(abs(i)).rstrip("0")
+            e = len(str(abs(i))) - len(s)
+            return ("-" if i < 0 else "") + f"{s}e{e}"
+        return str(i)
+    r = repr(float(x))
+    if "e" in r:
+        m, e = r.split("e")
+        r = f"{m}e{int(e)}"
+    return r
+
+
+def format_int(x):
+    return "NA" if x is None else str(int(x))
+
+
+def csv_field(s):
+    """readr quoting: quote when the field holds the delimiter, a quote or a
+    line break (quotes doubled)."""
+    if any(c in s for c in ',"\n\r'):
+        return '"' + s.replace('"', '""') + '"'
+    return s
+
+
+def r_as_character(x):
+    """as.character(<double>) in R: up to 15 significant digits, fixed
+    notation unless the scientific one is strictly narrower (scipen = 0)."""
+    if math.isnan(x):
+        return "NA"
+    if math.isinf(x):
+        return "Inf" if x > 0 else "-Inf"
+    if x == 0:
+        return "0"
+    # minimal significant digits (<= 15) that reproduce x at 15 digits
+    ref = float(f"{x:.15g}")
+    for d in range(1, 16):
+        if float(f"{x:.{d}g}") == ref:
+            break
+    sci = f"{x:.{d - 1}e}"
+    mant, exp = sci.split("e")
+    e = int(exp)
+    sci_s = f"{mant}e{'-' if e < 0 else '+'}{abs(e):02d}"
+    # fixed: digits after the point needed for d significant digits
+    nd = max(0, d - 1 - e)
+    fixed_s = f"{x:.{nd}f}"
+    return fixed_s if len(fixed_s) <= len(sci_s) else sci_s
+
+
+def write_fasta_gz(path, name, seq, width=80):
+    """writeXStringSet(x, path, compress = TRUE): '>' name, 80-column lines."""
+    with gzip.open(path, "wb") as f:
+        f.write(b">" + name.encode() + b"\n")
+        for i in range(0, len(seq), width):
+            f.write(seq[i:i + width] + b"\n")

@@ -6,6 +6,7 @@ Run in the build container (where /root/reference exists):
 Outputs (all *data*, no reference source):
   sample.fasta                    -- Example/sample.fasta (the C1 input, 4 reads)
   example_summary.csv             -- Example/Example_output/summary.csv (2023 code version)
+  reads/{1..4}.fasta              -- Example/Example_output/reads/*.fasta (written telomeric reads)
   example_window_counts.json      -- per-window covered-base counts for P1 (exact)
                                      and P2 (1 mismatch), decoded from the density
                                      polygons of Example_output/single_read_plots_adj/read*.eps
@@ -81,6 +82,11 @@ def main():
     shutil.copyfile(os.path.join(REF, "sample.fasta"), os.path.join(HERE, "sample.fasta"))
     shutil.copyfile(os.path.join(REF, "Example_output", "summary.csv"),
                     os.path.join(HERE, "example_summary.csv"))
+    # the telomeric reads as the reference wrote them (reads/<serial>.fasta, 2023 version)
+    os.makedirs(os.path.join(HERE, "reads"), exist_ok=True)
+    for serial in range(1, 5):
+        shutil.copyfile(os.path.join(REF, "Example_output", "reads", f"{serial}.fasta"),
+                        os.path.join(HERE, "reads", f"{serial}.fasta"))
     names, seqs = read_fasta(os.path.join(REF, "sample.fasta"))
     L = 100
     result = {"L": L, "min_density": 0.6, "patterns": "TTAGGG", "reads": []}

@@ -1,0 +1,69 @@
+"""End to end on the GPU: the command line (python -m nanotel_amd) reading
+FASTA/FASTQ(.gz), scanning on the MI355X and writing summary.csv,
+reads_ids.txt and reads/<serial>.fasta.gz.
+
+* Example/sample.fasta in legacy mode (the 2023 code that produced
+  Example_output) -> byte-identical summary.csv and reads/*.fasta;
+* a multi-file, multi-chunk FASTQ(.gz) input -> the same files as the
+  oracle-driven driver (tests/test_driver.py's stand-in).
+"""
+import gzip
+import os
+import shutil
+
+import numpy as np
+import pytest
+
+import _oracle as O
+from test_driver import OracleNanoTel, _make_input, _outputs
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def test_cli_example_legacy_byte_identical(tmp_path):
+    from nanotel_amd.cli import main
+    inp = tmp_path / "sample.fasta"
+    shutil.copyfile(os.path.join(GOLD, "sample.fasta"), inp)
+    out = tmp_path / "out"
+    assert main(["-i", str(inp), "--save_path", str(out), "--format", "fasta", "--patterns", "TTAGGG",
+                 "--legacy_no_ext"]) == 0
+    assert (out / "sample.fasta_summary.csv").read_bytes() == open(
+        os.path.join(GOLD, "example_summary.csv"), "rb").read()
+    for i in range(1, 5):
+        assert gzip.open(out / "reads" / f"{i}.fasta.gz").read() == open(
+            os.path.join(GOLD, "reads", f"{i}.fasta"), "rb").read()
+    names, _ = O.read_fasta(os.path.join(GOLD, "sample.fasta"))
+    assert (out / "reads_ids.txt").read_text().splitlines() == names
+
+
+def test_cli_example_current_code(tmp_path):
+    # current code (edge extension on): SURVEY §8(c) predicted rows
+    from nanotel_amd.cli import main
+    inp = tmp_path / "sample.fasta"
+    shutil.copyfile(os.path.join(GOLD, "sample.fasta"), inp)
+    out = tmp_path / "out"
+    assert main(["-i", str(inp), "--save_path", str(out), "--format", "fasta", "--patterns", "TTAGGG"]) == 0
+    lines = (out / "sample.fasta_summary.csv").read_text().splitlines()
+    assert lines[2].endswith("0.9630518234165067,12070,20405,8336,0.9743309666848716,11251,20405,9155")
+    assert lines[3].endswith("0.9837031219320637,49241,59426,10186,0.9906408174959411,48956,59426,10471")
+    assert lines[4].endswith("0.9705955437753665,3805,15877,12073,0.9874927524227616,3805,15877,12073")
+
+
+@pytest.mark.parametrize("rc", [False, True])
+def test_driver_gpu_matches_oracle_driver(tmp_path, rc):
+    from nanotel_amd import driver
+    inp = _make_input(str(tmp_path), rc)
+    gpu_out, ora_out = str(tmp_path / "gpu"), str(tmp_path / "ora")
+    driver.run(inp, gpu_out, "TTAGGG", fmt="fasta", nrec=4, rc=rc, log=lambda *a: None)
+    real = driver.NanoTel
+    try:
+        driver.NanoTel = OracleNanoTel
+        driver.run(inp, ora_out, "TTAGGG", fmt="fasta", nrec=4, rc=rc, log=lambda *a: None)
+    finally:
+        driver.NanoTel = real
+    a, b = _outputs(gpu_out), _outputs(ora_out)
+    assert a == b
+    assert len(a["in_summary.csv"].splitlines()) > 5
+    assert np.all([k.endswith(".fasta.gz") or k in ("in_summary.csv", "reads_ids.txt") for k in a])

@@ -1,0 +1,139 @@
+"""Host ingest and output writers, CPU only.
+
+* the C++ reader (nt_reader_*) against a plain Python parse, over FASTA,
+  FASTQ, gzip, a nested directory stream and chunks that span files;
+* the summary.csv writer: the oracle's rows for Example/sample.fasta
+  (legacy mode) are written byte-identical to the committed
+  Example_output/summary.csv;
+* reads/<serial>.fasta.gz: the written reads equal Example_output/reads/*.fasta;
+* R's as.character() of doubles for the file names.
+"""
+import gzip
+import os
+
+import numpy as np
+import pytest
+
+import _oracle as O
+from _parity import oracle_rows
+from nanotel_amd import assign_serials
+from nanotel_amd.driver import chunk_rows, reverse_complement, write_summary_csv
+from nanotel_amd.io import Reader, format_double, r_as_character, write_fasta_gz
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _chunks(path, fmt, nrec):
+    out = []
+    with Reader(path, fmt) as r:
+        while True:
+            ch = r.next_chunk(nrec)
+            if ch is None:
+                break
+            out.append([(ch.name(i), ch.seq(i).decode()) for i in range(ch.n)])
+    return out
+
+
+def test_reader_fasta_matches_python_parse():
+    names, seqs = O.read_fasta(os.path.join(GOLD, "sample.fasta"))
+    got = _chunks(os.path.join(GOLD, "sample.fasta"), "fasta", 10000)
+    assert len(got) == 1 and got[0] == list(zip(names, seqs))
+    got3 = _chunks(os.path.join(GOLD, "sample.fasta"), "fasta", 3)
+    assert [len(c) for c in got3] == [3, 1]
+    assert sum(got3, []) == list(zip(names, seqs))
+
+
+def _write_fastq(path, recs, gz=False, crlf=False):
+    nl = "\r\n" if crlf else "\n"
+    txt = "".join(f"@{n}{nl}{s}{nl}+{nl}{'I' * len(s)}{nl}" for n, s in recs)
+    if gz:
+        with gzip.open(path, "wt", newline="") as f:
+            f.write(txt)
+    else:
+        with open(path, "w", newline="") as f:
+            f.write(txt)
+
+
+def test_reader_fastq_gz_directory_stream(tmp_path):
+    rng = np.random.default_rng(3)
+
+    def rec(i):
+        return (f"read_{i} runid=abc ch={i}", "".join(rng.choice(list("ACGTN"), int(rng.integers(1, 300)))))
+
+    recs = [rec(i) for i in range(17)]
+    d = tmp_path / "in"
+    (d / "sub").mkdir(parents=True)
+    # sorted full paths: in/a.fastq, in/b.fastq.gz, in/sub/c.fastq
+    _write_fastq(d / "a.fastq", recs[:5])
+    _write_fastq(d / "b.fastq.gz", recs[5:12], gz=True, crlf=True)
+    _write_fastq(d / "sub" / "c.fastq", recs[12:])
+    with Reader(str(d), "fastq") as r:
+        assert [os.path.relpath(p, d) for p in r.files()] == ["a.fastq", "b.fastq.gz", "sub/c.fastq"]
+    for nrec in (1, 4, 7, 100):
+        got = _chunks(str(d), "fastq", nrec)
+        assert [len(c) for c in got] == [min(nrec, 17 - i) for i in range(0, 17, nrec)]
+        assert sum(got, []) == recs
+
+
+def test_reader_fasta_wrapped_blank_lines(tmp_path):
+    p = tmp_path / "x.fa.gz"
+    with gzip.open(p, "wt") as f:
+        f.write(">r1 desc words\nACGT\nTTAG\n\nGG\n>r2\n\nNNNN\n>r3\n")
+    assert _chunks(str(p), "fasta", 10) == [[("r1 desc words", "ACGTTTAGGG"), ("r2", "NNNN"), ("r3", "")]]
+
+
+def test_reader_errors(tmp_path):
+    from nanotel_amd import NanoTelError
+    with pytest.raises(NanoTelError):
+        Reader(str(tmp_path / "missing.fq"), "fastq")
+    p = tmp_path / "bad.fq"
+    p.write_text("not a fastq\n")
+    with pytest.raises(NanoTelError):
+        _chunks(str(p), "fastq", 10)
+
+
+def test_r_as_character():
+    cases = {1.0: "1", 2.0: "2", 100.0: "100", 1e5: "1e+05", 2e5: "2e+05", 123456.0: "123456",
+             110000.0: "110000", 1e15: "1e+15", 0.1: "0.1", 1 / 3: "0.333333333333333",
+             1234567.0: "1234567", 0.00001: "1e-05", 123.5: "123.5"}
+    for x, s in cases.items():
+        assert r_as_character(x) == s, (x, r_as_character(x), s)
+
+
+def test_format_double():
+    assert format_double(1.0) == "1"
+    assert format_double(0.9919354838709677) == "0.9919354838709677"
+    assert format_double(float("nan")) == "NA"
+    assert format_double(100000.0) == "100000"
+    assert format_double(100000.0, sci_threshold=1e5) == "1e5"
+
+
+def test_summary_csv_from_oracle_rows_is_byte_identical():
+    # the legacy (2023) code produced Example_output/summary.csv
+    names, seqs = O.read_fasta(os.path.join(GOLD, "sample.fasta"))
+    orows = oracle_rows(seqs, "TTAGGG", legacy=True, want_windows=False, want_hits=False)
+    n = len(seqs)
+    res = {"start": np.array([r["start"] + [-1] for r in orows]),
+           "end": np.array([r["end"] + [-1] for r in orows]),
+           "density": np.array([r["density"] + [0.0] for r in orows])}
+    telo = np.array([r["telomeric"] for r in orows], np.uint8)
+    ser, order, _, _ = assign_serials(telo)
+    rows = chunk_rows(res, names, [len(s) for s in seqs], ser, order, 2)
+    out = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"nt_summary_{os.getpid()}.csv")
+    write_summary_csv(out, rows, tvr=False)
+    assert open(out, "rb").read() == open(os.path.join(GOLD, "example_summary.csv"), "rb").read()
+    os.remove(out)
+    assert n == 4
+
+
+def test_written_reads_match_reference(tmp_path):
+    names, seqs = O.read_fasta(os.path.join(GOLD, "sample.fasta"))
+    for i, (nm, s) in enumerate(zip(names, seqs), start=1):
+        p = tmp_path / f"{r_as_character(float(i))}.fasta.gz"
+        write_fasta_gz(str(p), nm, s.encode())
+        assert gzip.open(p, "rb").read() == open(os.path.join(GOLD, "reads", f"{i}.fasta"), "rb").read()
+
+
+def test_reverse_complement_matches_oracle():
+    s = "ACGTNRYKMSWBDHVacgtn"
+    assert reverse_complement(s.encode()).decode().upper() == O.reverse_complement(s).upper()
