@@ -40,17 +40,19 @@ def scan_bytes_per_read(read_len, n_pass, n_windows, n_hits):
     """Algorithmic HBM bytes of the SCAN kernel per read:
     reads the 2-bit planes (ceil(n/4) B) + len (4) + blk_off (8) + win_off
     (8); writes the uint16 window counts per pass, the telomeric-window
-    bitmask per pass (ceil(nw/64) u64) and the hit counters (u32)."""
+    bitmask per pass (ceil(nw/64) u64), the running counts at every 16th
+    window (u32, for the calling kernel) and the hit counters (u32)."""
     planes = (read_len + 3) // 4
     return (planes + 4 + 8 + 8 + n_windows * n_pass * 2 + n_pass * 8 * ((n_windows + 63) // 64)
-            + 4 * n_hits)
+            + n_pass * 4 * (n_windows // 16 + 1) + 4 * n_hits)
 
 
 def call_bytes_per_read(n_pass, n_windows):
     """Algorithmic bytes of the CALLING kernel per read: len/blk_off/win_off,
     the window bitmasks and counts it walks (upper bound: all of them), and
     the row written (start/end int32 x3, density f64 x3, flags u8)."""
-    return 4 + 8 + 8 + n_pass * (8 * ((n_windows + 63) // 64) + 2 * n_windows) + 3 * (4 + 4 + 8) + 1
+    return (4 + 8 + 8 + n_pass * (8 * ((n_windows + 63) // 64) + 4 * (n_windows // 16 + 1) + 2 * n_windows)
+            + 3 * (4 + 4 + 8) + 1)
 
 
 def cpu_baseline(cfg, budget_s=12.0, max_reads=10 ** 9):

@@ -8,6 +8,7 @@
 #include <atomic>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <thread>
@@ -194,6 +195,8 @@ struct nt_ctx {
   std::string err;
   bool compiled = false;
   bool lds_limit_set = false;
+  hipStream_t call_stream = nullptr;  // sub-batched calling kernels (NT_SUBBATCH > 1)
+  hipEvent_t ev_scan = nullptr, ev_call = nullptr;
   bool profile = false;  // HIP events around the scan and call kernels of every call
   std::vector<std::array<hipEvent_t, 3>> ev;
   size_t n_ev = 0;  // calls recorded since the last nt_kernel_times
@@ -256,7 +259,11 @@ void nt_destroy(nt_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->call_stream) (void)hipStreamSynchronize(ctx->call_stream);
   if (ctx->prog_dev) (void)hipFree(ctx->prog_dev);
+  if (ctx->ev_scan) (void)hipEventDestroy(ctx->ev_scan);
+  if (ctx->ev_call) (void)hipEventDestroy(ctx->ev_call);
+  if (ctx->call_stream) (void)hipStreamDestroy(ctx->call_stream);
   for (auto& a : ctx->ev)
     for (hipEvent_t ev : a) (void)hipEventDestroy(ev);
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
@@ -531,11 +538,24 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
     }
     len_cap = a;
   }
-  const uint64_t call_grid = std::max<uint64_t>(1, std::min<uint64_t>((batch->n_reads + 255) / 256,
-                                                                      (uint64_t)ctx->cu_count * 64));
   const bool two = len_cap < max_len;
-  // read queues of the two scan launches (zeroed on the stream, 8 B each)
-  if ((e = ctx->queue.ensure(16)) != hipSuccess) return hip_fail(ctx, e, "hipMalloc(queue)");
+  // Sub-batches: the calling kernel of sub-batch k runs on a second stream
+  // while the scan of sub-batch k+1 runs (NT_SUBBATCH, default 1 = serial);
+  // NT_SCAN_WAVES caps the scan's blocks per CU to leave room for it.
+  uint64_t nsub = 1;
+  if (const char* v = std::getenv("NT_SUBBATCH")) nsub = std::max<uint64_t>(1, std::strtoull(v, nullptr, 10));
+  nsub = std::min<uint64_t>(nsub, std::max<uint64_t>(1, batch->n_reads / 256));
+  int bpc_cap = 0;
+  if (const char* v = std::getenv("NT_SCAN_WAVES")) bpc_cap = std::atoi(v);
+  if (nsub > 1 && !ctx->call_stream) {
+    if ((e = hipStreamCreateWithFlags(&ctx->call_stream, hipStreamNonBlocking)) != hipSuccess)
+      return hip_fail(ctx, e, "hipStreamCreate(call)");
+    if ((e = hipEventCreateWithFlags(&ctx->ev_scan, hipEventDisableTiming)) != hipSuccess ||
+        (e = hipEventCreateWithFlags(&ctx->ev_call, hipEventDisableTiming)) != hipSuccess)
+      return hip_fail(ctx, e, "hipEventCreate");
+  }
+  // read queues: two per sub-batch (LDS and global-scratch launches), zeroed on the stream
+  if ((e = ctx->queue.ensure(16 * nsub)) != hipSuccess) return hip_fail(ctx, e, "hipMalloc(queue)");
   unsigned long long* queue = (unsigned long long*)ctx->queue.p;
   hipEvent_t* ev = nullptr;
   if (ctx->profile) {
@@ -548,39 +568,74 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
     ev = ctx->ev[ctx->n_ev++].data();
     (void)hipEventRecord(ev[0], ctx->stream);
   }
-  if ((e = hipMemsetAsync(queue, 0, 16, ctx->stream)) != hipSuccess) return hip_fail(ctx, e, "hipMemsetAsync(queue)");
-  {
-    const uint32_t ww = nt_dev_wave_words(noslots, nh, np, cap_nw);
-    const size_t lds_bytes = (size_t)ww * 4u * 4u;
-    // exactly the resident blocks (the waves stride over the reads): a grid
-    // beyond one resident round would start its tail blocks late
-    int bpc = ctx->jit ? nt_jit_blocks_per_cu(ctx->jit_lds, lds_bytes)
-                       : nt_dev_scan_blocks_per_cu(single, one, m6, 1, lds_bytes);
-    if (bpc <= 0) bpc = 1;
-    const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((batch->n_reads + 3) / 4, (uint64_t)ctx->cu_count * bpc));
+  if ((e = hipMemsetAsync(queue, 0, 16 * nsub, ctx->stream)) != hipSuccess) return hip_fail(ctx, e, "hipMemsetAsync(queue)");
+  const uint32_t ww_lds = nt_dev_wave_words(noslots, nh, np, cap_nw);
+  const size_t lds_bytes = (size_t)ww_lds * 4u * 4u;
+  // exactly the resident blocks (the waves take reads from a queue)
+  int bpc = ctx->jit ? nt_jit_blocks_per_cu(ctx->jit_lds, lds_bytes)
+                     : nt_dev_scan_blocks_per_cu(single, one, m6, 1, lds_bytes);
+  if (bpc <= 0) bpc = 1;
+  if (bpc_cap > 0) bpc = std::min(bpc, bpc_cap);
+  const uint32_t ww_g = nt_dev_wave_words(noslots, nh, np, max_nw);
+  const uint64_t grid_g = std::max<uint64_t>(1, std::min<uint64_t>((batch->n_reads + 3) / 4, (uint64_t)ctx->cu_count * 2));
+  if (two && (e = ctx->scratch.ensure(grid_g * 4 * (uint64_t)ww_g * 4)) != hipSuccess)
+    return hip_fail(ctx, e, "hipMalloc(scratch)");
+  for (uint64_t k = 0; k < nsub; ++k) {
+    const uint64_t r0 = batch->n_reads * k / nsub, r1 = batch->n_reads * (k + 1) / nsub;
+    const uint64_t nr = r1 - r0;
+    // the sub-batch: pointers advanced by r0 (win_off / blk_off / exc_off stay absolute);
+    // the telomeric-mask base is per batch-global read index (tm_base), so shift it too
+    NtBatch Bk = B;
+    Bk.blk_off += r0;
+    Bk.len += r0;
+    Bk.win_off += r0;
+    if (Bk.exc_off) Bk.exc_off += r0;
+    Bk.n_reads = nr;
+    NtOut Ok = O;
+    Ok.start += 3 * r0;
+    Ok.end += 3 * r0;
+    Ok.density += 3 * r0;
+    Ok.flags += r0;
+    if (Ok.hits) Ok.hits += (uint64_t)nh * r0;
+    uint64_t* tmk = tmask + 2 * r0 * (uint64_t)np;  // aux_base(win_off, r, np) of the global read index
+    unsigned long long* q = queue + 2 * k;
+    const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((nr + 3) / 4, (uint64_t)ctx->cu_count * bpc));
     if (ctx->jit)
       e = nt_jit_launch(ctx->jit_lds, (int)grid, lds_bytes, ctx->stream, ctx->prog_dev,
-                        (const uint32_t*)ctx->thr.p, &B, &O, tmask, queue, 0u, (uint32_t)len_cap, ww, nullptr);
+                        (const uint32_t*)ctx->thr.p, &Bk, &Ok, tmk, q, 0u, (uint32_t)len_cap, ww_lds, nullptr);
     else
-      e = nt_dev_launch(ctx->prog_dev, (const uint32_t*)ctx->thr.p, &B, &O, tmask, queue, 0u, (uint32_t)len_cap,
-                        single, one, m6, 1, ww, nullptr, (int)grid, 0, ctx->stream);
+      e = nt_dev_launch(ctx->prog_dev, (const uint32_t*)ctx->thr.p, &Bk, &Ok, tmk, q, 0u, (uint32_t)len_cap,
+                        single, one, m6, 1, ww_lds, nullptr, (int)grid, 0, ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, e, "launch nt_scan_kernel<lds>");
+    if (two) {
+      if (ctx->jit)
+        e = nt_jit_launch(ctx->jit_gmem, (int)grid_g, 0, ctx->stream, ctx->prog_dev, (const uint32_t*)ctx->thr.p,
+                          &Bk, &Ok, tmk, q + 1, (uint32_t)len_cap, 0xFFFFFFFFu, ww_g, (uint32_t*)ctx->scratch.p);
+      else
+        e = nt_dev_launch(ctx->prog_dev, (const uint32_t*)ctx->thr.p, &Bk, &Ok, tmk, q + 1, (uint32_t)len_cap,
+                          0xFFFFFFFFu, single, 0, 0, 0, ww_g, (uint32_t*)ctx->scratch.p, (int)grid_g, 0,
+                          ctx->stream);
+      if (e != hipSuccess) return hip_fail(ctx, e, "launch nt_scan_kernel<global>");
+    }
+    const uint64_t call_grid = std::max<uint64_t>(1, std::min<uint64_t>((nr + 255) / 256, (uint64_t)ctx->cu_count * 64));
+    if (nsub == 1) {
+      if (ev) (void)hipEventRecord(ev[1], ctx->stream);
+      e = nt_dev_launch_call(ctx->prog_dev, &Bk, &Ok, tmk, (int)call_grid, ctx->stream);
+    } else {
+      // calling kernel of this sub-batch on the call stream, after its scan
+      if ((e = hipEventRecord(ctx->ev_scan, ctx->stream)) != hipSuccess ||
+          (e = hipStreamWaitEvent(ctx->call_stream, ctx->ev_scan, 0)) != hipSuccess)
+        return hip_fail(ctx, e, "stream dependency");
+      e = nt_dev_launch_call(ctx->prog_dev, &Bk, &Ok, tmk, (int)call_grid, ctx->call_stream);
+    }
+    if (e != hipSuccess) return hip_fail(ctx, e, "launch nt_call_kernel");
   }
-  if (two) {
-    const uint32_t ww = nt_dev_wave_words(noslots, nh, np, max_nw);
-    const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((batch->n_reads + 3) / 4, (uint64_t)ctx->cu_count * 2));
-    if ((e = ctx->scratch.ensure(grid * 4 * (uint64_t)ww * 4)) != hipSuccess) return hip_fail(ctx, e, "hipMalloc(scratch)");
-    if (ctx->jit)
-      e = nt_jit_launch(ctx->jit_gmem, (int)grid, 0, ctx->stream, ctx->prog_dev, (const uint32_t*)ctx->thr.p,
-                        &B, &O, tmask, queue + 1, (uint32_t)len_cap, 0xFFFFFFFFu, ww, (uint32_t*)ctx->scratch.p);
-    else
-      e = nt_dev_launch(ctx->prog_dev, (const uint32_t*)ctx->thr.p, &B, &O, tmask, queue + 1, (uint32_t)len_cap, 0xFFFFFFFFu,
-                        single, 0, 0, 0, ww, (uint32_t*)ctx->scratch.p, (int)grid, 0, ctx->stream);
-    if (e != hipSuccess) return hip_fail(ctx, e, "launch nt_scan_kernel<global>");
+  if (nsub > 1) {
+    if (ev) (void)hipEventRecord(ev[1], ctx->stream);  // end of the last scan
+    if ((e = hipEventRecord(ctx->ev_call, ctx->call_stream)) != hipSuccess ||
+        (e = hipStreamWaitEvent(ctx->stream, ctx->ev_call, 0)) != hipSuccess)
+      return hip_fail(ctx, e, "stream join");
   }
-  if (ev) (void)hipEventRecord(ev[1], ctx->stream);
-  e = nt_dev_launch_call(ctx->prog_dev, &B, &O, tmask, (int)call_grid, ctx->stream);
-  if (e != hipSuccess) return hip_fail(ctx, e, "launch nt_call_kernel");
   if (ev) (void)hipEventRecord(ev[2], ctx->stream);
   return NT_OK;
 }

@@ -57,6 +57,7 @@ struct Lane {
   const NtProgram* prog;
   const uint16_t* cnt;   // this pass's window counts
   const uint64_t* tm;    // this pass's telomeric-window bitmask
+  const uint32_t* ck;    // this pass's running counts at every 16th window boundary
   int n, nw, nmw, L;
   int k;         // 0 for P1, 1 for P2/P3
   bool use_tvr;  // P3
@@ -132,6 +133,18 @@ __device__ int cov_count(const Lane& c, int x, int y) {
 
 // sum(width(intersect(IRanges(a1, b1), ranges))): window counts for whole
 // windows, recomputed coverage for the partial windows at the two ends.
+// Covered bases of windows [0, k) (0 <= k <= nw): the scan's checkpoint at
+// window 16*(k/16) plus at most 15 window counts (independent loads).
+__device__ __forceinline__ int cnt_before(const Lane& c, int k) {
+  const int r = k & 15;
+  const uint16_t* w = c.cnt + (k - r);
+  int t = (int)c.ck[k >> 4];
+#pragma unroll
+  for (int i = 0; i < 15; ++i)
+    if (i < r) t += w[i];
+  return t;
+}
+
 __device__ int range_count(const Lane& c, int a1, int b1) {
   const int a = (a1 < 1 ? 1 : a1) - 1, b = (b1 > c.n ? c.n : b1) - 1;
   if (a > b) return 0;
@@ -139,11 +152,12 @@ __device__ int range_count(const Lane& c, int a1, int b1) {
   const int L = c.L;
   const int ka = min(div_l(c.prog, a), c.nw - 1), kb = min(div_l(c.prog, b), c.nw - 1);
   const int ws_a = ka * L, we_b = kb == c.nw - 1 ? c.n - 1 : (kb + 1) * L - 1;
-  if (ka == kb) return (a == ws_a && b == we_b) ? wcount(c, ka) : cov_count(c, a, b);
-  const int we_a = (ka + 1) * L - 1, ws_b = kb * L;
-  int tot = a == ws_a ? wcount(c, ka) : cov_count(c, a, we_a);
-  for (int k = ka + 1; k < kb; ++k) tot += wcount(c, k);
-  tot += b == we_b ? wcount(c, kb) : cov_count(c, ws_b, b);
+  const bool a_whole = a == ws_a, b_whole = b == we_b;
+  if (ka == kb) return (a_whole && b_whole) ? wcount(c, ka) : cov_count(c, a, b);
+  // whole windows from the running counts, partial end windows from coverage
+  int tot = cnt_before(c, b_whole ? kb + 1 : kb) - cnt_before(c, a_whole ? ka : ka + 1);
+  if (!a_whole) tot += cov_count(c, a, (ka + 1) * L - 1);
+  if (!b_whole) tot += cov_count(c, kb * L, b);
   return tot;
 }
 
@@ -355,15 +369,24 @@ __device__ int search_left(const Lane& c, int start_index) {
 // find_telo_position_wraper (NanoTel.R:1080-1155) + density (NanoTel.R:1840).
 __device__ void call_pass(const Lane& c, int& out_s, int& out_e, double& out_d, uint32_t& err) {
   Pos tp = find_telo_position(c, 3, 2.0);
+#ifdef NT_DBG_NO_WRAP
+  const double telo_density = 1.0;
+#else
   const double telo_density = sub_density(c, tp.s, tp.e);
+#endif
   const int num_rows = (tp.e - tp.s + 1) / c.L;
   if (telo_density < 0.85 && num_rows > 5) {
     const int min_rows = num_rows <= 7 ? num_rows - 2 : 7;
     const double min_density = 0.6 * (double)min_rows;
     tp = find_telo_position(c, min_rows, min_density);
   }
+#ifdef NT_DBG_NO_ACC  // timing experiments only (wrong results)
+  const int s_acc = tp.s;
+  int e_acc = tp.e;
+#else
   const int s_acc = accurate_start(c, tp.s);
   int e_acc = accurate_end(c, tp.e);
+#endif
   if (s_acc > e_acc) e_acc = s_acc;
   tp = Pos{s_acc, e_acc};
   if (tp.e - tp.s + 1 < 100) {
@@ -375,7 +398,11 @@ __device__ void call_pass(const Lane& c, int& out_s, int& out_e, double& out_d, 
       tp = find_left_telo(c);
     }
   }
+#ifdef NT_DBG_NO_EXT
+  if (false) {
+#else
   if (!c.prog->legacy_no_ext) {
+#endif
     int e2 = tp.e, s2 = tp.s;
     if (tp.e < c.n) e2 = search_right(c, tp.e + 1);
     if (tp.s > 1) s2 = search_left(c, tp.s - 1);
@@ -384,7 +411,11 @@ __device__ void call_pass(const Lane& c, int& out_s, int& out_e, double& out_d, 
   if (tp.e < tp.s - 1) { err |= NT_FLAG_ERR_WIDTH; out_s = -1; out_e = -1; out_d = 0.0; return; }
   out_s = tp.s;
   out_e = tp.e;
+#ifdef NT_DBG_NO_FINAL
+  out_d = 0.5;
+#else
   out_d = sub_density(c, tp.s, tp.e);
+#endif
 }
 
 // One lane per read (grid-stride over reads).  The kernel is memory-latency
@@ -429,12 +460,14 @@ nt_call_kernel(const NtProgram* __restrict__ prog, NtBatch B, NtOut O,
     c.nw = (int)split_window_count(c.n, L);
     c.nmw = (c.nw + 63) >> 6;
     const uint64_t woff = B.win_off[r];
-    const uint64_t* tmr = tmask + tm_base(woff, r, np);
+    const uint64_t* tmr = tmask + aux_base(woff, r, np);
+    const uint32_t* ckr = reinterpret_cast<const uint32_t*>(tmr + np * aux_nmw(c.nw));
     int maxw = INT_MIN;
     uint32_t flags = NT_FLAG_DONE;
     for (int p = 0; p < np; ++p) {
       c.cnt = O.win_counts + woff * np + (uint64_t)p * c.nw;
       c.tm = tmr + p * c.nmw;
+      c.ck = ckr + p * aux_nck(c.nw);
       c.k = p == 0 ? 0 : 1;
       c.use_tvr = p == 2;
       c.raw = p == 0 && prog->raw_p1;
@@ -513,7 +546,7 @@ uint32_t nt_dev_wave_words(int single, int n_hits, int np, uint32_t nw_cap) {
 
 // uint64 words of the telomeric-bitmask scratch for a batch
 uint64_t nt_dev_tmask_words(uint64_t total_windows, uint64_t n_reads, int np) {
-  return ((total_windows >> 6) + n_reads + 1) * (uint64_t)np;
+  return ((total_windows >> 4) + 2 * n_reads + 2) * (uint64_t)np;  // aux_base blocks
 }
 
 // (single, lds, one-hot, compile-time m): m = 6 covers TTAGGG-style motifs

@@ -52,11 +52,17 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// First uint64 of read r's telomeric bitmasks (pass p at + p * nmw):
-// tm_off(r) = (win_off[r] >> 6) + r never overlaps read r+1's block.
-__device__ __forceinline__ uint64_t tm_base(uint64_t win_off, uint64_t r, int np) {
-  return ((win_off >> 6) + r) * (uint64_t)np;
+// Per-read auxiliary block of the scan for the calling kernel, in uint64
+// units from aux_base(): the telomeric-window bitmasks (pass p at p * nmw,
+// nmw = ceil(nw / 64)), then the running covered-base counts at every 16th
+// window boundary as uint32 (pass p at p * nck, nck = nw / 16 + 1):
+// cnt16[p][j] = covered bases before window 16 j.  Block size <=
+// np * (nw / 16 + 2) words, and (win_off >> 4) + 2 r never reaches read r+1's.
+__device__ __forceinline__ uint64_t aux_base(uint64_t win_off, uint64_t r, int np) {
+  return ((win_off >> 4) + 2 * r) * (uint64_t)np;
 }
+__device__ __forceinline__ int aux_nmw(int nw) { return (nw + 63) >> 6; }
+__device__ __forceinline__ int aux_nck(int nw) { return (nw >> 4) + 1; }
 
 template <int I>
 struct IC {
@@ -602,9 +608,14 @@ __device__ __forceinline__ void scan_reads(const NtProgram* __restrict__ prog,
       const int wl = n - (nw - 1) * L;
       thr_last = thr[wl < tsz ? wl : tsz - 1];
     }
-    const int nmw = (nw + 63) >> 6;
-    uint64_t* tmo = tmask + tm_base(B.win_off[r], r, np);
+    const int nmw = aux_nmw(nw), nck = aux_nck(nw);
+    uint64_t* tmo = tmask + aux_base(B.win_off[r], r, np);
+    uint32_t* cko = reinterpret_cast<uint32_t*>(tmo + np * nmw);
     for (int p = 0; p < np; ++p) {
+      for (int j = lane; j < nck; j += kWave) {
+        const int i = 16 * j;  // i <= nw
+        cko[p * nck + j] = nw == 0 ? 0u : (p == 2 ? cum2[i] : (p == 1 ? cum01[i].y : cum01[i].x));
+      }
       for (int ch = 0; ch < nmw; ++ch) {
         const int i = ch * 64 + lane;
         uint32_t cnt = 0u;

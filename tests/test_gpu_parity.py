@@ -257,3 +257,25 @@ def test_odd_block_offset_is_reported():
     f = t["flags"].cpu().numpy()
     assert f[3] == (ROW_DONE | ROW_ERR_ALIGN)
     assert all((f[i] & ROW_ERR_ALIGN) == 0 for i in range(n) if i != 3)
+
+
+@pytest.mark.parametrize("jit", [True, False], ids=["jit", "aot"])
+def test_subbatched_overlap_matches_serial(jit):
+    # NT_SUBBATCH > 1: the calling kernel of sub-batch k runs on a second
+    # stream beside the scan of sub-batch k+1; outputs must not change
+    from nanotel_amd import synth_params
+    n, read_len = 1100, 7000
+    sp = synth_params(read_len=read_len, first_read=77)
+    nt = _nt(jit=jit, patterns="TTAGGG", tvr_patterns="TTGGGG")
+    outs = []
+    for sub in ("1", "3"):
+        os.environ["NT_SUBBATCH"] = sub
+        try:
+            t = _device_batch(nt, sp, n, read_len)
+            _run_device(nt, t, n, read_len)
+        finally:
+            del os.environ["NT_SUBBATCH"]
+        outs.append({k: t[k].cpu().numpy() for k in ("start", "end", "dens", "flags", "wc", "hits")})
+    for k in outs[0]:
+        assert np.array_equal(outs[0][k], outs[1][k]), k
+    assert (outs[0]["flags"] & 1).sum() > 100
