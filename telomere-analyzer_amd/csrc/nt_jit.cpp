@@ -55,7 +55,12 @@ std::string jit_source(const NtProgram& P) {
   s += "#include \"nt_scan.h\"\n";
   s += "using JitSet = nt::CtSet<nt::CtList<" + pats + ">, nt::CtList<" + tvrs + ">>;\n";
   s += R"(
-extern "C" __global__ void __launch_bounds__(256)
+#ifdef NT_SCAN_WAVES_EU
+#define NT_SCAN_ATTR __attribute__((amdgpu_waves_per_eu(NT_SCAN_WAVES_EU)))
+#else
+#define NT_SCAN_ATTR
+#endif
+extern "C" __global__ void __launch_bounds__(256) NT_SCAN_ATTR
 nt_scan_jit_lds(const NtProgram* __restrict__ prog, const uint32_t* __restrict__ thr, NtBatch B,
                 NtOut O, uint64_t* __restrict__ tmask, unsigned long long* __restrict__ queue,
                 uint32_t len_lo, uint32_t len_hi, uint32_t wave_words, uint32_t* __restrict__ gscr) {
@@ -89,8 +94,22 @@ bool compile(int device, const std::string& src, JitEntry& e) {
     std::string a = prop.gcnArchName;
     arch = "--offload-arch=" + a.substr(0, a.find(':'));
   }
-  const char* opts[] = {arch.c_str(), "-O3", "-std=c++17", "-ffp-contract=off"};
-  const hiprtcResult rc = hiprtcCompileProgram(prog, 4, opts);
+  std::vector<std::string> extra;  // NT_JIT_OPTS: extra compiler options (tuning experiments)
+  if (const char* v = std::getenv("NT_JIT_OPTS")) {
+    std::string t;
+    for (const char* p = v;; ++p) {
+      if (*p == ' ' || *p == 0) {
+        if (!t.empty()) extra.push_back(t);
+        t.clear();
+        if (*p == 0) break;
+      } else {
+        t += *p;
+      }
+    }
+  }
+  std::vector<const char*> opts = {arch.c_str(), "-O3", "-std=c++17", "-ffp-contract=off"};
+  for (const std::string& x : extra) opts.push_back(x.c_str());
+  const hiprtcResult rc = hiprtcCompileProgram(prog, (int)opts.size(), opts.data());
   if (rc != HIPRTC_SUCCESS) {
     size_t n = 0;
     hiprtcGetProgramLogSize(prog, &n);
@@ -126,7 +145,8 @@ bool nt_jit_get(int device, const NtProgram& P, void** fn_lds, void** fn_gmem, s
     return false;
   }
   const std::string src = jit_source(P);
-  const std::string key = std::to_string(device) + "\n" + src;
+  const char* xo = std::getenv("NT_JIT_OPTS");
+  const std::string key = std::to_string(device) + "\n" + (xo ? xo : "") + "\n" + src;
   std::lock_guard<std::mutex> lk(g_mu);
   auto it = g_cache.find(key);
   if (it == g_cache.end()) {

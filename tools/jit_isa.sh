@@ -19,10 +19,21 @@ nt_scan_jit_lds(const NtProgram* __restrict__ prog, const uint32_t* __restrict__
 }
 EOT
 cd "$out"
-/opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -I"$here/telomere-analyzer_amd/csrc" \
+/opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -DNT_ISA_MARKS -I"$here/telomere-analyzer_amd/csrc" \
   -c --save-temps -Rpass-analysis=kernel-resource-usage j.hip -o j.o 2>&1 | grep -E "VGPRs:|SGPRs:|Occupancy" | sed 's/.*remark: //'
 python3 - <<'EOT'
 s=open('j-hip-amdgcn-amd-amdhsa-gfx950.s').read()
 i=s.index('nt_scan_jit_lds:'); j=s.index('.Lfunc_end',i)
 open('k.s','w').write(s[i:j])
+EOT
+# instruction mix between the chunk markers (both the edge and the interior instances)
+python3 - <<'EOT'
+import re
+s=open('k.s').read().split('\n')
+marks=[i for i,l in enumerate(s) if 'NT_CHUNK_BEGIN' in l or 'NT_CHUNK_END' in l]
+pairs=[(marks[i],marks[i+1]) for i in range(0,len(marks)-1,2)]
+for a,b in pairs:
+    body=[l.strip() for l in s[a:b] if l.strip() and not l.strip().startswith(';') and not l.strip().startswith('.')]
+    v=sum(1 for l in body if l.startswith('v_')); sa=sum(1 for l in body if l.startswith('s_') and not l.startswith('s_nop')); ds=sum(1 for l in body if l.startswith('ds_'))
+    print(f"chunk region lines {a}-{b}: VALU {v} SALU {sa} LDS {ds} (static, all paths)")
 EOT
