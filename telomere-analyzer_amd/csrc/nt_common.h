@@ -21,6 +21,12 @@
 #define NT_MAX_TVR_M 32   // TVRs are only length-limited by the 32-bit start words
 #define NT_MAX_PASS 3
 
+// Scan read queues (see scan_reads): per launch, NT_QUEUES u64 counters
+// NT_QUEUE_STRIDE u64 apart (own 256-byte line each), zeroed before the launch
+#define NT_QUEUES 8
+#define NT_QUEUE_STRIDE 32
+#define NT_QUEUE_WORDS (NT_QUEUES * NT_QUEUE_STRIDE)
+
 // Per-read flag bits (rows.flags)
 #define NT_FLAG_TELOMERIC 0x01   // row emitted (max width >= 30), NanoTel.R:1847-1868
 #define NT_FLAG_NA_SHIFT 1       // bit 1+p: pass p start == -1 (NA columns)

@@ -23,7 +23,7 @@ uint32_t nt_dev_wave_words(int single, int n_hits, int np, uint32_t nw_cap);
 uint64_t nt_dev_tmask_words(uint64_t total_windows, uint64_t n_reads, int np);
 hipError_t nt_dev_launch(const NtProgram* prog, const uint32_t* thr, const NtBatch* B,
                          const NtOut* O, uint64_t* tmask, unsigned long long* queue,
-                         uint32_t len_lo, uint32_t len_hi,
+                         uint32_t len_lo, uint32_t len_hi, uint32_t claim, uint32_t nstatic,
                          int single, int one, int m6, int lds, uint32_t wave_words, uint32_t* gscr,
                          int grid, int call_grid, hipStream_t stream);
 hipError_t nt_dev_set_lds_limit(uint32_t bytes);
@@ -42,7 +42,7 @@ bool nt_jit_get(int device, const NtProgram& P, void** fn_lds, void** fn_gmem, s
 hipError_t nt_jit_launch(void* fn, int grid, size_t lds_bytes, hipStream_t stream,
                          const NtProgram* prog, const uint32_t* thr, const NtBatch* B,
                          const NtOut* O, uint64_t* tmask, unsigned long long* queue,
-                         uint32_t len_lo, uint32_t len_hi, uint32_t wave_words, uint32_t* gscr);
+                         uint32_t len_lo, uint32_t len_hi, uint32_t claim, uint32_t nstatic, uint32_t wave_words, uint32_t* gscr);
 
 namespace {
 
@@ -494,6 +494,24 @@ int nt_pack_reads(const char* const* seqs, const uint64_t* lens, uint64_t n_read
   return bad.load() ? NT_E_LETTER : NT_OK;
 }
 
+// Read distribution of the scan (scan_reads): the 8 per-XCD queues, ~64 kb
+// per claim and >= ~8 claims per wave.  NT_STATIC_FRAC (a static share
+// before the queues, measured slower) and NT_CLAIM override (tuning).
+struct QueuePlan {
+  uint32_t claim, nstatic;
+};
+static QueuePlan queue_plan(uint64_t n_reads, uint64_t mean_len, uint64_t waves) {
+  waves = std::max<uint64_t>(waves, 1);
+  double frac = 0.0;
+  if (const char* v = std::getenv("NT_STATIC_FRAC")) frac = std::min(1.0, std::max(0.0, std::atof(v)));
+  const uint64_t nst = (uint64_t)(frac * (double)(n_reads / waves));
+  const uint64_t dyn = n_reads - nst * waves;
+  uint64_t c = (64000 + std::max<uint64_t>(mean_len, 1) / 2) / std::max<uint64_t>(mean_len, 1);
+  c = std::min<uint64_t>(c, dyn / (8 * waves));
+  if (const char* v = std::getenv("NT_CLAIM")) c = (uint64_t)std::max(1, std::atoi(v));
+  return {(uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(c, 64)), (uint32_t)nst};
+}
+
 int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t max_len) {
   if (!ctx || !batch || !out) return NT_E_ARG;
   if (!ctx->compiled) return fail(ctx, NT_E_STATE, "nt_compile() not called");
@@ -555,7 +573,7 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
       return hip_fail(ctx, e, "hipEventCreate");
   }
   // read queues: two per sub-batch (LDS and global-scratch launches), zeroed on the stream
-  if ((e = ctx->queue.ensure(16 * nsub)) != hipSuccess) return hip_fail(ctx, e, "hipMalloc(queue)");
+  if ((e = ctx->queue.ensure(2 * NT_QUEUE_WORDS * 8 * nsub)) != hipSuccess) return hip_fail(ctx, e, "hipMalloc(queue)");
   unsigned long long* queue = (unsigned long long*)ctx->queue.p;
   hipEvent_t* ev = nullptr;
   if (ctx->profile) {
@@ -568,7 +586,7 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
     ev = ctx->ev[ctx->n_ev++].data();
     (void)hipEventRecord(ev[0], ctx->stream);
   }
-  if ((e = hipMemsetAsync(queue, 0, 16 * nsub, ctx->stream)) != hipSuccess) return hip_fail(ctx, e, "hipMemsetAsync(queue)");
+  if ((e = hipMemsetAsync(queue, 0, 2 * NT_QUEUE_WORDS * 8 * nsub, ctx->stream)) != hipSuccess) return hip_fail(ctx, e, "hipMemsetAsync(queue)");
   const uint32_t ww_lds = nt_dev_wave_words(noslots, nh, np, cap_nw);
   const size_t lds_bytes = (size_t)ww_lds * 4u * 4u;
   // exactly the resident blocks (the waves take reads from a queue)
@@ -598,22 +616,24 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
     Ok.flags += r0;
     if (Ok.hits) Ok.hits += (uint64_t)nh * r0;
     uint64_t* tmk = tmask + 2 * r0 * (uint64_t)np;  // aux_base(win_off, r, np) of the global read index
-    unsigned long long* q = queue + 2 * k;
+    unsigned long long* q = queue + 2 * NT_QUEUE_WORDS * k;
     const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((nr + 3) / 4, (uint64_t)ctx->cu_count * bpc));
+    const QueuePlan qp = queue_plan(nr, batch->n_windows * (uint64_t)L / batch->n_reads, grid * 4);
+    const uint32_t claim = qp.claim, nstatic = qp.nstatic;
     if (ctx->jit)
       e = nt_jit_launch(ctx->jit_lds, (int)grid, lds_bytes, ctx->stream, ctx->prog_dev,
-                        (const uint32_t*)ctx->thr.p, &Bk, &Ok, tmk, q, 0u, (uint32_t)len_cap, ww_lds, nullptr);
+                        (const uint32_t*)ctx->thr.p, &Bk, &Ok, tmk, q, 0u, (uint32_t)len_cap, claim, nstatic, ww_lds, nullptr);
     else
-      e = nt_dev_launch(ctx->prog_dev, (const uint32_t*)ctx->thr.p, &Bk, &Ok, tmk, q, 0u, (uint32_t)len_cap,
+      e = nt_dev_launch(ctx->prog_dev, (const uint32_t*)ctx->thr.p, &Bk, &Ok, tmk, q, 0u, (uint32_t)len_cap, claim, nstatic,
                         single, one, m6, 1, ww_lds, nullptr, (int)grid, 0, ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, e, "launch nt_scan_kernel<lds>");
     if (two) {
       if (ctx->jit)
         e = nt_jit_launch(ctx->jit_gmem, (int)grid_g, 0, ctx->stream, ctx->prog_dev, (const uint32_t*)ctx->thr.p,
-                          &Bk, &Ok, tmk, q + 1, (uint32_t)len_cap, 0xFFFFFFFFu, ww_g, (uint32_t*)ctx->scratch.p);
+                          &Bk, &Ok, tmk, q + NT_QUEUE_WORDS, (uint32_t)len_cap, 0xFFFFFFFFu, 1u, 0u, ww_g, (uint32_t*)ctx->scratch.p);
       else
-        e = nt_dev_launch(ctx->prog_dev, (const uint32_t*)ctx->thr.p, &Bk, &Ok, tmk, q + 1, (uint32_t)len_cap,
-                          0xFFFFFFFFu, single, 0, 0, 0, ww_g, (uint32_t*)ctx->scratch.p, (int)grid_g, 0,
+        e = nt_dev_launch(ctx->prog_dev, (const uint32_t*)ctx->thr.p, &Bk, &Ok, tmk, q + NT_QUEUE_WORDS, (uint32_t)len_cap,
+                          0xFFFFFFFFu, 1u, 0u, single, 0, 0, 0, ww_g, (uint32_t*)ctx->scratch.p, (int)grid_g, 0,
                           ctx->stream);
       if (e != hipSuccess) return hip_fail(ctx, e, "launch nt_scan_kernel<global>");
     }

@@ -63,17 +63,17 @@ std::string jit_source(const NtProgram& P) {
 extern "C" __global__ void __launch_bounds__(256) NT_SCAN_ATTR
 nt_scan_jit_lds(const NtProgram* __restrict__ prog, const uint32_t* __restrict__ thr, NtBatch B,
                 NtOut O, uint64_t* __restrict__ tmask, unsigned long long* __restrict__ queue,
-                uint32_t len_lo, uint32_t len_hi, uint32_t wave_words, uint32_t* __restrict__ gscr) {
+                uint32_t len_lo, uint32_t len_hi, uint32_t claim, uint32_t nstatic, uint32_t wave_words, uint32_t* __restrict__ gscr) {
   extern __shared__ uint32_t smem[];
-  nt::scan_reads<JitSet, true>(prog, thr, B, O, tmask, queue, len_lo, len_hi,
+  nt::scan_reads<JitSet, true>(prog, thr, B, O, tmask, queue, len_lo, len_hi, claim, nstatic,
                                smem + (threadIdx.x >> 6) * wave_words);
 }
 extern "C" __global__ void __launch_bounds__(256)
 nt_scan_jit_gmem(const NtProgram* __restrict__ prog, const uint32_t* __restrict__ thr, NtBatch B,
                  NtOut O, uint64_t* __restrict__ tmask, unsigned long long* __restrict__ queue,
-                 uint32_t len_lo, uint32_t len_hi, uint32_t wave_words, uint32_t* __restrict__ gscr) {
+                 uint32_t len_lo, uint32_t len_hi, uint32_t claim, uint32_t nstatic, uint32_t wave_words, uint32_t* __restrict__ gscr) {
   const uint64_t gw = (uint64_t)blockIdx.x * nt::kNWaves + (threadIdx.x >> 6);
-  nt::scan_reads<JitSet, false>(prog, thr, B, O, tmask, queue, len_lo, len_hi,
+  nt::scan_reads<JitSet, false>(prog, thr, B, O, tmask, queue, len_lo, len_hi, claim, nstatic,
                                 gscr + gw * wave_words);
 }
 )";
@@ -166,10 +166,10 @@ bool nt_jit_get(int device, const NtProgram& P, void** fn_lds, void** fn_gmem, s
 hipError_t nt_jit_launch(void* fn, int grid, size_t lds_bytes, hipStream_t stream,
                          const NtProgram* prog, const uint32_t* thr, const NtBatch* B,
                          const NtOut* O, uint64_t* tmask, unsigned long long* queue,
-                         uint32_t len_lo, uint32_t len_hi, uint32_t wave_words, uint32_t* gscr) {
+                         uint32_t len_lo, uint32_t len_hi, uint32_t claim, uint32_t nstatic, uint32_t wave_words, uint32_t* gscr) {
   NtBatch b = *B;
   NtOut o = *O;
-  void* args[] = {&prog, &thr, &b, &o, &tmask, &queue, &len_lo, &len_hi, &wave_words, &gscr};
+  void* args[] = {&prog, &thr, &b, &o, &tmask, &queue, &len_lo, &len_hi, &claim, &nstatic, &wave_words, &gscr};
   return hipModuleLaunchKernel((hipFunction_t)fn, (unsigned)grid, 1, 1, 256, 1, 1,
                                (unsigned)lds_bytes, stream, args, nullptr);
 }

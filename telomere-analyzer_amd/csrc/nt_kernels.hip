@@ -38,11 +38,11 @@ template <class S, bool kLds>
 __global__ void __launch_bounds__(kWG)
 nt_scan_kernel(const NtProgram* __restrict__ prog, const uint32_t* __restrict__ thr, NtBatch B,
                NtOut O, uint64_t* __restrict__ tmask, unsigned long long* __restrict__ queue,
-               uint32_t len_lo, uint32_t len_hi, uint32_t wave_words, uint32_t* __restrict__ gscr) {
+               uint32_t len_lo, uint32_t len_hi, uint32_t claim, uint32_t nstatic, uint32_t wave_words, uint32_t* __restrict__ gscr) {
   extern __shared__ uint32_t smem[];
   const uint64_t gw = (uint64_t)blockIdx.x * kNWaves + (threadIdx.x >> 6);
   uint32_t* wmem = kLds ? smem + (uint64_t)(threadIdx.x >> 6) * wave_words : gscr + gw * wave_words;
-  scan_reads<S, kLds>(prog, thr, B, O, tmask, queue, len_lo, len_hi, wmem);
+  scan_reads<S, kLds>(prog, thr, B, O, tmask, queue, len_lo, len_hi, claim, nstatic, wmem);
 }
 
 // ================================================================= call
@@ -578,7 +578,7 @@ hipError_t nt_dev_set_lds_limit(uint32_t bytes) {
 // single: 1 pattern, no TVR; one: one-hot letters; m6: 6 letters
 hipError_t nt_dev_launch(const NtProgram* prog, const uint32_t* thr, const NtBatch* B,
                          const NtOut* O, uint64_t* tmask, unsigned long long* queue,
-                         uint32_t len_lo, uint32_t len_hi,
+                         uint32_t len_lo, uint32_t len_hi, uint32_t claim, uint32_t nstatic,
                          int single, int one, int m6, int lds, uint32_t wave_words, uint32_t* gscr,
                          int grid, int call_grid, hipStream_t stream) {
   const size_t lds_bytes = lds ? (size_t)wave_words * 4u * nt::kNWaves : 0;
@@ -586,7 +586,7 @@ hipError_t nt_dev_launch(const NtProgram* prog, const uint32_t* thr, const NtBat
 #define NT_LAUNCH(S, G, SI, O_, M)                                                             \
   if (!done && single == SI && lds == (int)G && (O_ < 0 || one == O_) && (M < 0 || m6 == M)) { \
     hipLaunchKernelGGL((nt::nt_scan_kernel<S, G>), dim3(grid), dim3(nt::kWG), lds_bytes,       \
-                       stream, prog, thr, *B, *O, tmask, queue, len_lo, len_hi, wave_words,    \
+                       stream, prog, thr, *B, *O, tmask, queue, len_lo, len_hi, claim, nstatic, wave_words,    \
                        gscr);                                                                  \
     done = true;                                                                               \
   }

@@ -531,12 +531,34 @@ __device__ __forceinline__ void scan_chunk(const NtProgram* __restrict__ prog, c
 #endif
 constexpr int kRing = NT_RING;  // prefetch depth in chunks (tuning knob)
 
+struct ReadMeta {
+  uint32_t len;
+  uint64_t boff, woff;  // block offset (uniform), window offset
+  uint32_t e0, e1;      // exception list range (0, 0 without exceptions)
+};
+
+// The per-read metadata, all loads independent (one memory round trip).
+__device__ __forceinline__ ReadMeta load_meta(const NtBatch& B, uint64_t r) {
+  ReadMeta m;
+  m.len = B.len[r];
+  const uint64_t b = B.blk_off[r];
+  m.boff = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) << 32) |
+           __builtin_amdgcn_readfirstlane((uint32_t)b);  // uniform: SGPR base
+  m.woff = B.win_off[r];
+  m.e0 = m.e1 = 0u;
+  if (B.exc_off) {
+    m.e0 = B.exc_off[r];
+    m.e1 = B.exc_off[r + 1];
+  }
+  return m;
+}
+
 template <class S, bool kLds>
 __device__ __forceinline__ void scan_reads(const NtProgram* __restrict__ prog,
                                            const uint32_t* __restrict__ thr, const NtBatch& B,
                                            const NtOut& O, uint64_t* __restrict__ tmask,
                                            unsigned long long* __restrict__ queue,
-                                           uint32_t len_lo, uint32_t len_hi, uint32_t* wmem) {
+                                           uint32_t len_lo, uint32_t len_hi, uint32_t claim, uint32_t nstatic, uint32_t* wmem) {
   const int lane = threadIdx.x & (kWave - 1);
   const int np = S::kNPass ? S::kNPass : prog->n_pass;
   const int nh = S::kRegHits ? S::kNHits : prog->n_hits, L = prog->L;
@@ -545,42 +567,71 @@ __device__ __forceinline__ void scan_reads(const NtProgram* __restrict__ prog,
   const DivL div{prog->div32_m, prog->div32_s};
   const uint32_t thr_full = thr[L < tsz ? L : tsz - 1];
 
-  // dynamic read queue: each wave claims kClaim reads at a time (the next
-  // claim is issued before the current reads are scanned), so waves that
-  // start late or draw short reads simply take fewer
-  constexpr uint64_t kClaim = 4;
-  auto claim = [&]() -> uint64_t {
-    unsigned long long v = 0;
-    if (lane == 0) v = atomicAdd(queue, (unsigned long long)kClaim);
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
-    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-    return ((uint64_t)hi << 32) | lo;
-  };
-  uint64_t cur = claim();
-  while (cur < B.n_reads) {
-  const uint64_t nxt = claim();
-  const uint64_t r_end = cur + kClaim < B.n_reads ? cur + kClaim : B.n_reads;
-  for (uint64_t r = cur; r < r_end; ++r) {
-    const uint32_t n32 = B.len[r];
-    if (n32 <= len_lo || n32 > len_hi) continue;
-    const uint64_t boff = B.blk_off[r];
-    if (boff & 1u) {  // layout contract: 16-byte aligned segments
-      if (lane == 0) O.flags[r] = NT_FLAG_ERR_ALIGN;
-      continue;
+  // Read distribution: 8 queues, one per XCD (blocks are dealt round-robin
+  // to the XCDs), each over an eighth of the reads and claimed `claim` reads
+  // at a time; a wave whose queue is drained moves on to the next one.  A
+  // single device-scope counter serialises near 13 ns per claim across the
+  // chip, which bound the scan of short reads (1M x 10 kb: 3.2 ms at 4 reads
+  // per claim, 1.18 ms with the 8 queues).  A static round-robin share of
+  // the reads before the queues (`nstatic` per wave, tuning) measured slower
+  // at every fraction tried (1M x 50 kb: 5.1 ms at 3/4 static, 3.8 ms at 0).
+  const uint64_t nR = B.n_reads;
+  const uint64_t W = (uint64_t)gridDim.x * kNWaves;
+  const uint64_t w = (uint64_t)blockIdx.x * kNWaves + __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const uint64_t st_n = (uint64_t)nstatic * W < nR ? nstatic : nR / W;
+  const uint64_t D0 = st_n * W, Dn = nR - D0;
+  const uint64_t kc = claim ? claim : 1u;
+  uint32_t qi = blockIdx.x % NT_QUEUES, qtried = 0;
+  // next range [lo, hi) of reads from the queues, hi == lo == nR when drained
+  auto claim_next = [&](uint64_t& lo, uint64_t& hi) {
+    while (qtried < NT_QUEUES) {
+      const uint64_t q0 = D0 + Dn * qi / NT_QUEUES, q1 = D0 + Dn * (qi + 1) / NT_QUEUES;
+      unsigned long long v = 0;
+      if (lane == 0) v = atomicAdd(queue + qi * NT_QUEUE_STRIDE, (unsigned long long)kc);
+      const uint64_t o = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
+                         __builtin_amdgcn_readfirstlane((uint32_t)v);
+      if (o < q1 - q0) {
+        lo = q0 + o;
+        hi = q1 - q0 - o > kc ? lo + kc : q1;
+        return;
+      }
+      qi = qi + 1 == NT_QUEUES ? 0 : qi + 1;
+      ++qtried;
     }
+    lo = hi = nR;
+  };
+  // Read sequence: the current range [aLo, aHi) step aStep and the one
+  // claimed ahead [bLo, bHi).  While read r is scanned, the metadata of the next read is
+  // already in flight, and the ring's last loads are its first two chunks.
+  uint64_t aLo = w, aHi = D0, aStep = W, bLo, bHi;
+  if (st_n == 0) {
+    claim_next(aLo, aHi);
+    aStep = 1;
+  }
+  claim_next(bLo, bHi);
+  uint64_t r = aLo;
+  ReadMeta m = r < nR ? load_meta(B, r) : ReadMeta{};
+  uint4 nx1 = make_uint4(0u, 0u, 0u, 0u), nx2 = nx1;
+  bool ring_ok = false;  // nx1/nx2 hold chunks 0 and 1 of read r
+  while (r < nR) {
+    const bool cross = r + aStep >= aHi;
+    const uint64_t rn = cross ? bLo : r + aStep;  // next read (>= nR: none)
+    ReadMeta mn{};
+    if (rn < nR) mn = load_meta(B, rn);
+    const bool skip = m.len <= len_lo || m.len > len_hi;
+    const bool skip_n = rn >= nR || mn.len <= len_lo || mn.len > len_hi || (mn.boff & 1u);
+    if (!skip && (m.boff & 1u)) {  // layout contract: 16-byte aligned segments
+      if (lane == 0) O.flags[r] = NT_FLAG_ERR_ALIGN;
+    } else if (!skip) {
+    const uint32_t n32 = m.len;
+    const uint64_t boff = m.boff;
     ReadCtx rc;
     rc.n = n32;
     rc.nblk = (int32_t)((n32 + 31u) >> 5);
     rc.blk = reinterpret_cast<const uint2*>(B.planes) + boff;
-    rc.n_exc = 0;
-    rc.exc_pos = nullptr;
-    rc.exc_code = nullptr;
-    if (B.exc_off) {
-      const uint32_t e0 = B.exc_off[r], e1 = B.exc_off[r + 1];
-      rc.n_exc = (int32_t)(e1 - e0);
-      rc.exc_pos = B.exc_pos + e0;
-      rc.exc_code = B.exc_code + e0;
-    }
+    rc.n_exc = (int32_t)(m.e1 - m.e0);
+    rc.exc_pos = B.exc_off ? B.exc_pos + m.e0 : nullptr;
+    rc.exc_code = B.exc_off ? B.exc_code + m.e0 : nullptr;
     const int n = (int)n32;
     const int nseg = (n + 63) >> 6;
     const int nw = (int)split_window_count(n, L);
@@ -596,21 +647,33 @@ __device__ __forceinline__ void scan_reads(const NtProgram* __restrict__ prog,
 #pragma unroll
     for (int c = 0; c < S::kNHits; ++c) st.acc[c] = 0u;
     {
+      // 2-deep prefetch ring over the chunk stream of this read and the next
+      // one: the ring's last two loads of this read are the next read's
+      // chunks 0 and 1 (when both reads have >= 2 chunks), so no wave waits
+      // on a cold load at a read boundary
       const uint4* seg = reinterpret_cast<const uint4*>(rc.blk);
-      // prefetch ring: this lane's segment of the next kRing chunks
-      uint4 ring[kRing];
-#pragma unroll
-      for (int i = 0; i < kRing; ++i) ring[i] = load_seg(seg, nseg, i * kOwned - 1 + lane);
-      for (int g0 = -1; g0 < nseg; g0 += kOwned) {
-        const uint4 cur = ring[0];
-#pragma unroll
-        for (int i = 0; i + 1 < kRing; ++i) ring[i] = ring[i + 1];
-        ring[kRing - 1] = load_seg(seg, nseg, g0 + kRing * kOwned + lane);
+      const int K = (nseg + kOwned) / kOwned;  // chunks: g0 = -1, 62, ... < nseg
+      const uint4* segn = reinterpret_cast<const uint4*>(B.planes) + (mn.boff >> 1);
+      const int nsegn = ((int)mn.len + 63) >> 6;
+      const bool pf = !skip_n && K >= 2 && (nsegn + kOwned) / kOwned >= 2;
+      if (!ring_ok) {
+        nx1 = load_seg(seg, nseg, lane - 1);
+        nx2 = load_seg(seg, nseg, kOwned - 1 + lane);
+      }
+      int c = 0;
+      for (int g0 = -1; g0 < nseg; g0 += kOwned, ++c) {
+        const uint4 cur = nx1;
+        nx1 = nx2;
+        const int t = c + 2;  // stream position loaded now
+        const bool own_t = t < K || !pf;
+        nx2 = load_seg(own_t ? seg : segn, own_t ? nseg : nsegn,
+                       (own_t ? g0 + 2 * kOwned : (t - K) * kOwned - 1) + lane);
         if (g0 >= 0 && 64 * (g0 + kWave) <= n)
           scan_chunk<S, false>(prog, rc, g0, lane, np, nw, L, div, cur, cum01, cum2, hitacc, st);
         else
           scan_chunk<S, true>(prog, rc, g0, lane, np, nw, L, div, cur, cum01, cum2, hitacc, st);
       }
+      ring_ok = pf;
     }
     if (lane == 0 && nw > 0) {
       cum01[0] = make_uint2(0u, 0u);
@@ -623,7 +686,7 @@ __device__ __forceinline__ void scan_reads(const NtProgram* __restrict__ prog,
     wave_sync();
 
     // ------------------------------------------------ window outputs
-    uint16_t* wout = O.win_counts + B.win_off[r] * np;
+    uint16_t* wout = O.win_counts + m.woff * np;
     // telomeric window (class -5) iff !(count / width < min_density) iff
     // count >= thr[width] (exact, host-computed); the last window may be wider
     uint32_t thr_last = thr_full;
@@ -632,7 +695,7 @@ __device__ __forceinline__ void scan_reads(const NtProgram* __restrict__ prog,
       thr_last = thr[wl < tsz ? wl : tsz - 1];
     }
     const int nmw = aux_nmw(nw), nck = aux_nck(nw);
-    uint64_t* tmo = tmask + aux_base(B.win_off[r], r, np);
+    uint64_t* tmo = tmask + aux_base(m.woff, r, np);
     uint32_t* cko = reinterpret_cast<uint32_t*>(tmo + np * nmw);
     for (int p = 0; p < np; ++p) {
       for (int j = lane; j < nck; j += kWave) {
@@ -668,8 +731,16 @@ __device__ __forceinline__ void scan_reads(const NtProgram* __restrict__ prog,
       }
     }
     wave_sync();
-  }
-  cur = nxt;
+    }  // scanned read
+    if (skip || (m.boff & 1u)) ring_ok = false;
+    if (cross) {
+      aLo = bLo;
+      aHi = bHi;
+      aStep = 1;
+      if (aLo < nR) claim_next(bLo, bHi);
+    }
+    r = rn;
+    m = mn;
   }
 }
 

@@ -279,3 +279,31 @@ def test_subbatched_overlap_matches_serial(jit):
     for k in outs[0]:
         assert np.array_equal(outs[0][k], outs[1][k]), k
     assert (outs[0]["flags"] & 1).sum() > 100
+
+
+@pytest.mark.parametrize("plan", [("1.0", "3"), ("0.5", "1"), ("0.0", "7"), ("0.9", "64")])
+def test_read_distribution_plans(plan):
+    # static runs + 8 per-XCD queues (scan_reads): every read scanned exactly
+    # once whatever the split between the static part and the claims
+    frac, claim = plan
+    rng = np.random.default_rng(11)
+    lens = rng.integers(1, 3000, 20000)
+    lens[::97] = rng.integers(3000, 40000, lens[::97].size)
+    alpha = np.frombuffer(b"ACGTTAGGG", dtype=np.uint8)
+    seqs = [alpha[rng.integers(0, alpha.size, int(n))].tobytes().decode() for n in lens]
+    for i in range(0, len(seqs), 13):
+        seqs[i] = "TTAGGG" * (len(seqs[i]) // 6) + seqs[i][: len(seqs[i]) % 6]
+    nt = _nt(patterns="TTAGGG")
+    ref = nt.analyze(seqs, want_windows=True, want_hits=True)
+    os.environ["NT_STATIC_FRAC"], os.environ["NT_CLAIM"] = frac, claim
+    try:
+        res = nt.analyze(seqs, want_windows=True, want_hits=True)
+    finally:
+        del os.environ["NT_STATIC_FRAC"], os.environ["NT_CLAIM"]
+    for k in ("start", "end", "flags", "win_counts", "hits"):
+        assert np.array_equal(ref[k], res[k]), k
+    assert np.array_equal(ref["density"].view(np.uint64), res["density"].view(np.uint64))
+    assert (res["flags"] & 1).sum() > 1000
+    idx = list(range(0, len(seqs), 997))
+    compare(nt, {k: v[idx] if isinstance(v, np.ndarray) and v.shape[:1] == (len(seqs),) else v
+                 for k, v in res.items()}, oracle_rows([seqs[i] for i in idx], "TTAGGG"), check_windows=False)

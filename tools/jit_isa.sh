@@ -1,6 +1,6 @@
 #!/bin/bash
 # Offline ISA of the hiprtc-specialised scan for a pattern set (for reading
-# the inner loop): tools/jit_isa.sh OUTDIR "nt::CtPat<6,8,8,1,4,4,4>" ["tvr list"]
+# the inner loop): [ISA_DEFS=-D..] tools/jit_isa.sh OUTDIR "nt::CtPat<6,8,8,1,4,4,4>" ["tvr list"]
 set -eu
 out=$1; pats=$2; tvrs=${3:-}
 here=$(cd "$(dirname "$0")/.." && pwd)
@@ -9,17 +9,23 @@ cat > "$out/j.hip" <<EOT
 #include <hip/hip_runtime.h>
 #include "nt_scan.h"
 using JitSet = nt::CtSet<nt::CtList<$pats>, nt::CtList<$tvrs>>;
-extern "C" __global__ void __launch_bounds__(256)
+#ifdef NT_SCAN_WAVES_EU
+#define NT_SCAN_ATTR __attribute__((amdgpu_waves_per_eu(NT_SCAN_WAVES_EU)))
+#else
+#define NT_SCAN_ATTR
+#endif
+extern "C" __global__ void __launch_bounds__(256) NT_SCAN_ATTR
 nt_scan_jit_lds(const NtProgram* __restrict__ prog, const uint32_t* __restrict__ thr, NtBatch B,
                 NtOut O, uint64_t* __restrict__ tmask, unsigned long long* __restrict__ queue,
-                uint32_t len_lo, uint32_t len_hi, uint32_t wave_words, uint32_t* __restrict__ gscr) {
+                uint32_t len_lo, uint32_t len_hi, uint32_t claim, uint32_t nstatic, uint32_t wave_words,
+                uint32_t* __restrict__ gscr) {
   extern __shared__ uint32_t smem[];
-  nt::scan_reads<JitSet, true>(prog, thr, B, O, tmask, queue, len_lo, len_hi,
+  nt::scan_reads<JitSet, true>(prog, thr, B, O, tmask, queue, len_lo, len_hi, claim, nstatic,
                                smem + (threadIdx.x >> 6) * wave_words);
 }
 EOT
 cd "$out"
-/opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -DNT_ISA_MARKS -I"$here/telomere-analyzer_amd/csrc" \
+/opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -DNT_ISA_MARKS ${ISA_DEFS:-} -I"$here/telomere-analyzer_amd/csrc" \
   -c --save-temps -Rpass-analysis=kernel-resource-usage j.hip -o j.o 2>&1 | grep -E "VGPRs:|SGPRs:|Occupancy" | sed 's/.*remark: //'
 python3 - <<'EOT'
 s=open('j-hip-amdgcn-amd-amdhsa-gfx950.s').read()
