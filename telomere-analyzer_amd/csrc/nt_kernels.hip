@@ -124,10 +124,158 @@ __device__ uint32_t cov32(const Lane& c, int q) {
   return cov & range_mask(q, 0, c.n - 1);
 }
 
-// |coverage ∩ [x, y]| (0-based positions)
-__device__ int cov_count(const Lane& c, int x, int y) {
+// ------------------------------------------- boundary neighbourhoods
+//
+// The calling touches the coverage only near a few positions (the partial
+// windows of range_count, the A10 boundary refinements).  A neighbourhood
+// computes the pass's coverage words over [q0, q0 + 32K) at once: one batch
+// of K+5 independent block loads, then the bit-sliced match of every pattern
+// at every start with the letter tables hoisted out of the word loop --
+// instead of a chain of dependent per-word recomputations (cov32), which
+// held the calling kernel on memory latency.
+// cov[i + 1] = coverage of [q0 + 32i, q0 + 32i + 31] for i = -1..K (kMarks: the
+// two neighbour words run marks need; else i = 0..K-1 are meaningful);
+// rs/re: P1's raw view starts / ends (c.raw) at the same positions.
+template <int K, bool kMarks = true>
+struct Nb {
+  int q0;
+  uint32_t cov[K + 2];
+  uint32_t rs[kMarks ? K + 2 : 1];
+  uint32_t re[kMarks ? K + 2 : 1];
+};
+
+template <int K, bool kMarks>
+__device__ __forceinline__ void nb_build(const Lane& c, int q0, Nb<K, kMarks>& nb) {
+  constexpr int E = kMarks ? 1 : 0;  // extra word each side
+  constexpr int NC = K + 2 * E;      // coverage words computed, i = -E..K-1+E
+  constexpr int NP = NC + 2;         // plane words, positions [q0 + 32i, +31], i = -E-1..K+E
+  constexpr int NH = NC + 1;         // hit words, starts [q0 + 32i, +31], i = -E-1..K-1+E
+  constexpr int T0 = -E - 1;         // index of plane / hit word 0
+  nb.q0 = q0;
+  uint32_t Lw[NP], Hw[NP], Vw[NP];
+  {
+    const int bb = (q0 >> 5) + T0;  // arithmetic shift: floor for q0 < 0
+    const uint32_t sh = (uint32_t)(q0 & 31);
+    uint2 blk[NP + 1];
+#pragma unroll
+    for (int t = 0; t <= NP; ++t) {
+      const int b = bb + t;
+      const bool ok = b >= 0 && b < c.rc.nblk;
+      blk[t] = ok ? c.rc.blk[b] : make_uint2(0u, 0u);
+    }
+#pragma unroll
+    for (int t = 0; t < NP; ++t) {
+      Lw[t] = funnel(blk[t + 1].x, blk[t].x, sh);
+      Hw[t] = funnel(blk[t + 1].y, blk[t].y, sh);
+      Vw[t] = range_mask((int64_t)q0 + 32 * (t + T0), 0, c.n - 1);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < K + 2; ++i) nb.cov[i] = 0u;
+  const NtProgram* prog = c.prog;
+  const int npt = prog->n_pat + (c.use_tvr ? prog->n_tvr : 0);
+  for (int pi = 0; pi < npt; ++pi) {
+    const bool is_tvr = pi >= prog->n_pat;
+    const NtPat& P = is_tvr ? prog->tvr[pi - prog->n_pat] : prog->pat[pi];
+    const int m = P.m;
+    uint32_t x0[NH], x1[NH];
+#pragma unroll
+    for (int h = 0; h < NH; ++h) x0[h] = x1[h] = 0xFFFFFFFFu;
+    for (int j = 0; j < m; ++j) {
+      const uint32_t t0 = P.tm_scan[j][0], t1 = P.tm_scan[j][1], t2 = P.tm_scan[j][2], t3 = P.tm_scan[j][3];
+#pragma unroll
+      for (int h = 0; h < NH; ++h) {
+        const uint32_t Ls = funnel(Lw[h + 1], Lw[h], (uint32_t)j);
+        const uint32_t Hs = funnel(Hw[h + 1], Hw[h], (uint32_t)j);
+        const uint32_t q = bfi(Hs, bfi(Ls, t3, t2), bfi(Ls, t1, t0)) & funnel(Vw[h + 1], Vw[h], (uint32_t)j);
+        x1[h] = (x1[h] & q) | x0[h];
+        x0[h] &= q;
+      }
+    }
+    if (m <= 1) {
+#pragma unroll
+      for (int h = 0; h < NH; ++h) x1[h] &= Vw[h];
+    }
+    if (c.rc.n_exc) {
+#pragma unroll
+      for (int h = 0; h < NH; ++h)
+        patch_exceptions(c.rc, (int64_t)q0 + 32 * (h + T0), 0, c.n - 1, P, false, x0[h], x1[h]);
+    }
+    const bool use_a1 = !is_tvr && c.k;
+    // coverage word ci (i = ci - E) from hit words i and i - 1
+#pragma unroll
+    for (int ci = 0; ci < NC; ++ci)
+      nb.cov[ci + 1 - E] |= spread(use_a1 ? x1[ci + 1] : x0[ci + 1], use_a1 ? x1[ci] : x0[ci], m);
+    if constexpr (kMarks) {
+      if (c.raw && pi == 0) {
+#pragma unroll
+        for (int ci = 0; ci < NC; ++ci) {
+          nb.rs[ci] = x0[ci + 1];
+          nb.re[ci] = m > 1 ? funnel(x0[ci + 1], x0[ci], (uint32_t)(32 - (m - 1))) : x0[ci + 1];
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int ci = 0; ci < NC; ++ci) nb.cov[ci + 1 - E] &= Vw[ci + 1];
+}
+
+// |coverage ∩ [a, b]|, [a, b] within [q0, q0 + 32K)
+template <int K, bool kMarks>
+__device__ __forceinline__ int nb_count(const Nb<K, kMarks>& nb, int a, int b) {
+  int t = 0;
+#pragma unroll
+  for (int i = 0; i < K; ++i) t += __builtin_popcount(nb.cov[i + 1] & range_mask((int64_t)nb.q0 + 32 * i, a, b));
+  return t;
+}
+
+// min(start(ranges)) with start in [a1, b1] (1-based), fallback if none;
+// run starts of the reduced coverage, or P1's raw view starts
+template <int K>
+__device__ __forceinline__ int nb_min_start(const Lane& c, const Nb<K>& nb, int a1, int b1, int fallback) {
+  const int a = max(a1 - 1, 0), b = min(b1 - 1, c.n - 1);
+  int res = fallback;
+  bool found = false;
+#pragma unroll
+  for (int i = 0; i < K; ++i) {
+    const uint32_t cur = nb.cov[i + 1];
+    const uint32_t mk = c.raw ? nb.rs[i + 1] : (cur & ~((cur << 1) | (nb.cov[i] >> 31)));
+    const uint32_t m = mk & range_mask((int64_t)nb.q0 + 32 * i, a, b);
+    if (!found && m) {
+      res = nb.q0 + 32 * i + __builtin_ctz(m) + 1;
+      found = true;
+    }
+  }
+  return res;
+}
+
+// max(end(ranges)) with end in [a1, b1] (1-based), fallback if none
+template <int K>
+__device__ __forceinline__ int nb_max_end(const Lane& c, const Nb<K>& nb, int a1, int b1, int fallback) {
+  const int a = max(a1 - 1, 0), b = min(b1 - 1, c.n - 1);
+  int res = fallback;
+  bool found = false;
+#pragma unroll
+  for (int i = K - 1; i >= 0; --i) {
+    const uint32_t cur = nb.cov[i + 1];
+    const uint32_t mk = c.raw ? nb.re[i + 1] : (cur & ~((cur >> 1) | (nb.cov[i + 2] << 31)));
+    const uint32_t m = mk & range_mask((int64_t)nb.q0 + 32 * i, a, b);
+    if (!found && m) {
+      res = nb.q0 + 32 * i + (31 - __builtin_clz(m)) + 1;
+      found = true;
+    }
+  }
+  return res;
+}
+
+// |coverage ∩ [x, y]| (0-based positions), 128 bases per neighbourhood
+__device__ __noinline__ int cov_count(const Lane& c, int x, int y) {
   int tot = 0;
-  for (int q = x; q <= y; q += 32) tot += __builtin_popcount(cov32(c, q) & range_mask(q, x, y));
+  for (int q = x; q <= y; q += 128) {
+    Nb<4, false> nb;
+    nb_build(c, q, nb);
+    tot += nb_count(nb, q, min(y, q + 127));
+  }
   return tot;
 }
 
@@ -163,47 +311,6 @@ __device__ int range_count(const Lane& c, int a1, int b1) {
 
 __device__ __forceinline__ double sub_density(const Lane& c, int s, int e) {
   return (double)range_count(c, s, e) / (double)(e - s + 1);
-}
-
-// Range-start (kind 0) / range-end (kind 1) marks of the pass's range set at
-// positions [q, q+31]: run starts / ends of the reduced coverage, or the raw
-// view starts / ends of P1's single fixed pattern.
-__device__ uint32_t marks32(const Lane& c, int q, int kind) {
-  if (c.raw) {
-    const NtPat& P = c.prog->pat[0];
-    uint32_t a0, a1;
-    hits_at(c.rc, P, false, kind == 0 ? q : (int64_t)q - (P.m - 1), 0, c.n - 1, a0, a1);
-    return a0;
-  }
-  const uint32_t cur = cov32(c, q);
-  if (!cur) return 0u;
-  if (kind == 0) return cur & ~((cur << 1) | (cov32(c, q - 32) >> 31));
-  return cur & ~((cur >> 1) | (cov32(c, q + 32) << 31));
-}
-
-// min(start(ranges)) with start in [a1, b1]; fallback if none.
-__device__ int min_start_in(const Lane& c, int a1, int b1, int fallback) {
-  int a = a1 - 1, b = b1 - 1;
-  if (a < 0) a = 0;
-  if (b > c.n - 1) b = c.n - 1;
-  for (int q = a; q <= b; q += 32) {
-    const uint32_t m = marks32(c, q, 0) & range_mask(q, a, b);
-    if (m) return q + __builtin_ctz(m) + 1;
-  }
-  return fallback;
-}
-
-// max(end(ranges)) with end in [a1, b1]; fallback if none.
-__device__ int max_end_in(const Lane& c, int a1, int b1, int fallback) {
-  int a = a1 - 1, b = b1 - 1;
-  if (a < 0) a = 0;
-  if (b > c.n - 1) b = c.n - 1;
-  if (a > b) return fallback;
-  for (int q = b - 31; q + 31 >= a; q -= 32) {
-    const uint32_t m = marks32(c, q, 1) & range_mask(q, a, b);
-    if (m) return q + (31 - __builtin_clz(m)) + 1;
-  }
-  return fallback;
 }
 
 // ---------------------------------------------------------------- A8 / A11
@@ -284,26 +391,33 @@ __device__ Pos find_right_telo(const Lane& c, bool& err) {
 
 // ------------------------------------------------------------------ A10
 
-// get_accurate_start (NanoTel.R:1726-1764)
-__device__ int accurate_start(const Lane& c, int s) {
+// get_accurate_start (NanoTel.R:1726-1764): every range it reads lies in
+// [s-37, s+98] (0-based), one neighbourhood [s-42, s+118)
+__device__ __noinline__ int accurate_start(const Lane& c, int s) {
   if (s == -1) return -1;
-  const double first_50 = (double)range_count(c, s, s + 49) / 50.0;
+  Nb<5> nb;
+  nb_build(c, s - 42, nb);
+  const int a = max(s, 1) - 1, b = min(s + 49, c.n) - 1;
+  const double first_50 = (double)(a > b ? 0 : nb_count(nb, a, b)) / 50.0;
   int t = s;
   if (first_50 < 0.3) {
-    t = min_start_in(c, s + 48, s + 99, t);
-    t = min_start_in(c, s + 33, s + 48, t);
+    t = nb_min_start(c, nb, s + 48, s + 99, t);
+    t = nb_min_start(c, nb, s + 33, s + 48, t);
   } else {
-    t = min_start_in(c, s, s + 99, t);
-    if (first_50 >= 0.72) t = min_start_in(c, s - 36, s - 1, t);
+    t = nb_min_start(c, nb, s, s + 99, t);
+    if (first_50 >= 0.72) t = nb_min_start(c, nb, s - 36, s - 1, t);
   }
   return t;
 }
 
-// get_accurate_end (NanoTel.R:1692-1721)
-__device__ int accurate_end(const Lane& c, int e) {
+// get_accurate_end (NanoTel.R:1692-1721): ranges in [e-100, e+49], one
+// neighbourhood [e-102, e+58)
+__device__ __noinline__ int accurate_end(const Lane& c, int e) {
   if (e == -1) return -1;
-  const int t = max_end_in(c, e - 99, e, e);
-  return max_end_in(c, e + 1, e + 50, t);
+  Nb<5> nb;
+  nb_build(c, e - 102, nb);
+  const int t = nb_max_end(c, nb, e - 99, e, e);
+  return nb_max_end(c, nb, e + 1, e + 50, t);
 }
 
 // ------------------------------------------------------------------ A12
@@ -418,11 +532,11 @@ __device__ void call_pass(const Lane& c, int& out_s, int& out_e, double& out_d, 
 #endif
 }
 
-// One lane per read (grid-stride over reads).  The kernel is memory-latency
-// bound: NT_CALL_WAVES_PER_EU caps the VGPRs for occupancy (4 waves/SIMD
-// measured best: 1.96 -> 1.57 ms at c50k; 3: 1.71, 5: 1.76).
+// One lane per read (grid-stride over reads).  NT_CALL_WAVES_PER_EU trades
+// VGPRs for occupancy: with the boundary neighbourhoods (register arrays) 2
+// waves/SIMD and no spills measured best (1M x 10 kb: 0.86 ms at 4, 0.78 at 2).
 #ifndef NT_CALL_WAVES_PER_EU
-#define NT_CALL_WAVES_PER_EU 4
+#define NT_CALL_WAVES_PER_EU 2
 #endif
 #define NT_CALL_ATTR __attribute__((amdgpu_waves_per_eu(NT_CALL_WAVES_PER_EU)))
 __global__ void __launch_bounds__(256) NT_CALL_ATTR
