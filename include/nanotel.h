@@ -158,6 +158,20 @@ int nt_analyze_host(nt_ctx* ctx, const char* const* seqs, const uint64_t* lens, 
                     int32_t* start, int32_t* end, double* density, uint8_t* flags,
                     uint16_t* win_counts, uint32_t* hits);
 
+/* --- --use_filter pre-filter ----------------------------------------------
+ * Replaces filter_reads(samples, patterns, do_rc = FALSE, right_edge) +
+ * filter_density (NanoTel.R:2083-2103, 2121-2163) as called per chunk from
+ * run_future_worker_chuncks (NanoTel.R:2227-2232): keep[r] = 1 iff read r
+ * (scan orientation) is >= 1e3 long and the union of the exact fixed=FALSE
+ * matches of the patterns covers >= 0.8 * min_density of its 200-base edge
+ * sub-read (subseq(start=71, width=200), or subseq(end=-71, width=200) with
+ * check_right_edge).  The caller keeps the reads with keep = 1, in order.
+ * nt_filter_call: device batch, keep = device [n_reads], asynchronous.
+ * nt_filter_host: host reads (+rc as compiled), keep = host [n_reads], sync. */
+int nt_filter_call(nt_ctx* ctx, const nt_batch* batch, uint8_t* keep);
+int nt_filter_host(nt_ctx* ctx, const char* const* seqs, const uint64_t* lens, uint64_t n_reads,
+                   uint8_t* keep);
+
 /* --- A15: serials and row order of one chunk (host only) ----------------- */
 /* Same contract as the reference: serial_start_io = this chunk's serial_start
  * (1.0 first), becomes max(Serial)+1; max_serial_io running max (-Inf first). */

@@ -772,6 +772,43 @@ int nto_analyze_read(const char* seq, int64_t n, const nto_patterns* P, int L, d
   return NTO_OK;
 }
 
+/* ----------------------------------------------------------- --use_filter */
+
+/* filter_reads + filter_density (NanoTel.R:2083-2103, 2121-2163), as called
+ * per chunk from run_future_worker_chuncks (NanoTel.R:2227-2232) with
+ * do_rc = FALSE (the chunk is already in scan orientation), subread_width =
+ * 200, trimm_length = 70, min_density = global_min_density * 0.8.  Reads
+ * shorter than 1e3 are dropped.  The edge sub-read is subseq(start = 71,
+ * width = 200) (left) or subseq(end = -71, width = 200) = [n-269, n-70]
+ * (right_edge = --check_right_edge).  Density = sum(width(union of the exact
+ * fixed=FALSE matches of every (unique) pattern)) / nchar(sub-read).
+ * Returns 1 = kept, 0 = dropped, <0 = error. */
+int nto_filter_read(const char* seq, int64_t n, const nto_patterns* P, double min_density,
+                    int right_edge) {
+  if (!seq || !P) return NTO_E_ARG;
+  if (n < 1000) return 0; /* samples[width(samples) >= 1e3] */
+  const int64_t w = 200;
+  const int64_t a = right_edge ? n - 269 : 71; /* 1-based start of the sub-read */
+  uint8_t S[200];
+  for (int64_t i = 0; i < w; i++) {
+    S[i] = nto_dna_code(seq[a - 1 + i]);
+    if (!S[i]) return NTO_E_BAD_LETTER;
+  }
+  rlist all = {0};
+  for (int i = 0; i < P->n_pat; i++) {
+    rlist v = {0};
+    int e = match_codes(P->pat[i].code, P->pat[i].m, 0, S, w, 0, &v);
+    if (!e) e = rl_union(&all, &v);
+    rl_free(&v);
+    if (e) { rl_free(&all); return e; }
+  }
+  int64_t cov = 0;
+  for (int64_t i = 0; i < all.n; i++) cov += all.v[i].e - all.v[i].s + 1;
+  rl_free(&all);
+  const double total_density = (double)cov / (double)w;
+  return total_density >= min_density * 0.8;
+}
+
 /* ------------------------------------------------------------- serials A15 */
 
 int64_t nto_assign_serials(const uint8_t* is_telo, int64_t n, double* serial_start_io,

@@ -89,6 +89,12 @@ int nto_analyze_read(const char* seq, int64_t n, const nto_patterns* P, int L,
                      double min_density, int right_edge, int legacy_no_ext,
                      nto_row* row, uint32_t* win_counts, uint32_t* hit_counts);
 
+/* --use_filter: filter_reads/filter_density (NanoTel.R:2083-2163) for one
+ * read in scan orientation; min_density = --min_density (the filter uses
+ * 0.8 * min_density).  1 = kept, 0 = dropped, <0 = error. */
+int nto_filter_read(const char* seq, int64_t n, const nto_patterns* P, double min_density,
+                    int right_edge);
+
 /* A15: serial numbers and row order for one chunk (NanoTel.R:2234-2258,
  * 2050-2070).  is_telo[n] (chunk reads in stream order);
  * serial_start_io: in = this chunk's serial_start (1 for the first chunk,

@@ -141,9 +141,10 @@ __device__ __forceinline__ uint32_t code_at(const ReadCtx& rc, int64_t pos) {
 // Mismatch count (capped at 2) of pattern P at start s; positions outside
 // [vlo, vhi] count as mismatches.  eq (edge steps, always fixed=TRUE) or a
 // fixed pattern: code equality; otherwise IUPAC bit-set AND (fixed=FALSE).
+// iupac: fixed=FALSE whatever the pattern (the --use_filter matches).
 __device__ __forceinline__ int mism_generic(const ReadCtx& rc, const NtPat& P, bool eq, int64_t s,
-                                            int64_t vlo, int64_t vhi) {
-  eq = eq || P.fixed;
+                                            int64_t vlo, int64_t vhi, bool iupac = false) {
+  eq = eq || (P.fixed && !iupac);
   int nm = 0;
   for (int j = 0; j < P.m && nm < 2; ++j) {
     const int64_t pos = s + j;
@@ -160,7 +161,7 @@ __device__ __forceinline__ int mism_generic(const ReadCtx& rc, const NtPat& P, b
 // vhi-m+2] (m>=2) or [vlo, vhi] (m==1); for k=0 [vlo, vhi-m+1].
 __device__ __forceinline__ void patch_exceptions(const ReadCtx& rc, int64_t base, int64_t vlo,
                                               int64_t vhi, const NtPat& P, bool eq, uint32_t& a0,
-                                              uint32_t& a1) {
+                                              uint32_t& a1, bool iupac = false) {
   const int m = P.m;
   const int64_t xlo = base > vlo ? base : vlo;
   int64_t xhi = base + 31 + m - 1;
@@ -176,7 +177,7 @@ __device__ __forceinline__ void patch_exceptions(const ReadCtx& rc, int64_t base
     const int b = __builtin_ctz(dirty);
     dirty &= dirty - 1u;
     const int64_t s = base + b;
-    const int nm = mism_generic(rc, P, eq, s, vlo, vhi);
+    const int nm = mism_generic(rc, P, eq, s, vlo, vhi, iupac);
     const uint32_t bit = 1u << b;
     a0 = (nm == 0 && s >= vlo && s <= vhi - m + 1) ? (a0 | bit) : (a0 & ~bit);
     a1 = (nm <= 1 && s >= k1lo && s <= k1hi) ? (a1 | bit) : (a1 & ~bit);

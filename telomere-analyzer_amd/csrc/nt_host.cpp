@@ -32,6 +32,8 @@ hipError_t nt_dev_launch_call(const NtProgram* prog, const NtBatch* B, const NtO
                               const uint64_t* tmask, int call_grid, hipStream_t stream);
 hipError_t nt_dev_launch_synth(const NtSynth* S, uint32_t* planes, uint64_t n_reads,
                                hipStream_t stream);
+hipError_t nt_dev_launch_filter(const NtProgram* prog, const NtBatch* B, uint8_t* keep,
+                                uint32_t thr_count, int right_edge, int grid, hipStream_t stream);
 hipError_t nt_dev_launch_uniform_layout(uint64_t n_reads, uint64_t nblk, uint64_t read_len,
                                         uint64_t nw, uint64_t* blk_off, uint32_t* len,
                                         uint64_t* win_off, hipStream_t stream);
@@ -687,13 +689,11 @@ int64_t nt_kernel_times(nt_ctx* ctx, double* scan_ms, double* call_ms) {
   return n;
 }
 
-int nt_analyze_host(nt_ctx* ctx, const char* const* seqs, const uint64_t* lens, uint64_t n_reads,
-                    int32_t* start, int32_t* end, double* density, uint8_t* flags,
-                    uint16_t* win_counts, uint32_t* hits) {
-  if (!ctx) return NT_E_ARG;
-  if (!ctx->compiled) return fail(ctx, NT_E_STATE, "nt_compile() not called");
-  if (n_reads == 0) return NT_OK;
-  const int L = ctx->prog.L, np = ctx->prog.n_pass;
+// Pack a host chunk (2-bit planes + exception lists, --rc fused) and upload
+// it to the context's device buffers; B describes the device batch.
+static int upload_reads(nt_ctx* ctx, const char* const* seqs, const uint64_t* lens, uint64_t n_reads,
+                        nt_batch* B, uint64_t* max_len) {
+  const int L = ctx->prog.L;
   uint64_t tb = 0, tw = 0, te = 0, ml = 0, badr = 0;
   int rc = nt_pack_count(seqs, lens, n_reads, L, &tb, &tw, &te, &ml, &badr);
   if (rc == NT_E_EMPTY_READ)
@@ -729,6 +729,72 @@ int nt_analyze_host(nt_ctx* ctx, const char* const* seqs, const uint64_t* lens, 
     NT_UP(exc_code, h_ecode);
   }
 #undef NT_UP
+  // the staging vectors are pageable: finish the copies before they go
+  if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess) return hip_fail(ctx, e, "hipStreamSynchronize");
+  *B = nt_batch{(const uint32_t*)ctx->planes.p, (const uint64_t*)ctx->blk_off.p,
+                (const uint32_t*)ctx->len.p, (const uint64_t*)ctx->win_off.p,
+                te ? (const uint32_t*)ctx->exc_off.p : nullptr,
+                te ? (const uint32_t*)ctx->exc_pos.p : nullptr,
+                te ? (const uint8_t*)ctx->exc_code.p : nullptr, n_reads, tw};
+  *max_len = ml;
+  return NT_OK;
+}
+
+// --use_filter threshold: the smallest covered count c of the 200-base edge
+// sub-read with c / 200 >= min_density * 0.8 (fp64, as R evaluates
+// filter_density(..., min_density = global_min_density*0.8), NanoTel.R:2143)
+static uint32_t filter_threshold(double min_density) {
+  const double thr = min_density * 0.8;
+  for (uint32_t c = 0; c <= 200; ++c)
+    if ((double)c / 200.0 >= thr) return c;
+  return 201;
+}
+
+int nt_filter_call(nt_ctx* ctx, const nt_batch* batch, uint8_t* keep) {
+  if (!ctx || !batch || (batch->n_reads && !keep)) return NT_E_ARG;
+  if (!ctx->compiled) return fail(ctx, NT_E_STATE, "nt_compile() not called");
+  if (batch->n_reads == 0) return NT_OK;
+  (void)hipSetDevice(ctx->device);
+  NtBatch B{batch->planes, batch->blk_off, batch->len, batch->win_off,
+            batch->exc_off, batch->exc_pos, batch->exc_code, batch->n_reads};
+  const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((batch->n_reads + 255) / 256, (uint64_t)ctx->cu_count * 16));
+  const hipError_t e = nt_dev_launch_filter(ctx->prog_dev, &B, keep, filter_threshold(ctx->prog.min_density),
+                                            ctx->prog.right_edge, (int)grid, ctx->stream);
+  if (e != hipSuccess) return hip_fail(ctx, e, "launch nt_filter_kernel");
+  return NT_OK;
+}
+
+int nt_filter_host(nt_ctx* ctx, const char* const* seqs, const uint64_t* lens, uint64_t n_reads,
+                   uint8_t* keep) {
+  if (!ctx || (n_reads && (!seqs || !lens || !keep))) return NT_E_ARG;
+  if (!ctx->compiled) return fail(ctx, NT_E_STATE, "nt_compile() not called");
+  if (n_reads == 0) return NT_OK;
+  nt_batch B;
+  uint64_t ml = 0;
+  int rc = upload_reads(ctx, seqs, lens, n_reads, &B, &ml);
+  if (rc) return rc;
+  hipError_t e;
+  if ((e = ctx->flags.ensure(n_reads)) != hipSuccess) return hip_fail(ctx, e, "hipMalloc(flags)");
+  if ((rc = nt_filter_call(ctx, &B, (uint8_t*)ctx->flags.p))) return rc;
+  if ((e = hipMemcpyAsync(keep, ctx->flags.p, n_reads, hipMemcpyDeviceToHost, ctx->stream)) != hipSuccess)
+    return hip_fail(ctx, e, "hipMemcpyAsync(keep)");
+  if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess) return hip_fail(ctx, e, "hipStreamSynchronize");
+  return NT_OK;
+}
+
+int nt_analyze_host(nt_ctx* ctx, const char* const* seqs, const uint64_t* lens, uint64_t n_reads,
+                    int32_t* start, int32_t* end, double* density, uint8_t* flags,
+                    uint16_t* win_counts, uint32_t* hits) {
+  if (!ctx) return NT_E_ARG;
+  if (!ctx->compiled) return fail(ctx, NT_E_STATE, "nt_compile() not called");
+  if (n_reads == 0) return NT_OK;
+  const int np = ctx->prog.n_pass;
+  nt_batch B;
+  uint64_t ml = 0;
+  int rc = upload_reads(ctx, seqs, lens, n_reads, &B, &ml);
+  if (rc) return rc;
+  const uint64_t tw = B.n_windows;
+  hipError_t e;
   const uint64_t nwc = tw * np;
   if ((e = ctx->wc.ensure(std::max<uint64_t>(1, nwc) * 2)) != hipSuccess) return hip_fail(ctx, e, "hipMalloc(wc)");
   if ((e = ctx->start.ensure(n_reads * 3 * 4)) != hipSuccess) return hip_fail(ctx, e, "hipMalloc(start)");
@@ -737,11 +803,6 @@ int nt_analyze_host(nt_ctx* ctx, const char* const* seqs, const uint64_t* lens, 
   if ((e = ctx->flags.ensure(n_reads)) != hipSuccess) return hip_fail(ctx, e, "hipMalloc(flags)");
   const uint64_t nh = (uint64_t)ctx->prog.n_hits * n_reads;
   if ((e = ctx->hits.ensure(std::max<uint64_t>(1, nh) * 4)) != hipSuccess) return hip_fail(ctx, e, "hipMalloc(hits)");
-  nt_batch B{(const uint32_t*)ctx->planes.p, (const uint64_t*)ctx->blk_off.p,
-             (const uint32_t*)ctx->len.p, (const uint64_t*)ctx->win_off.p,
-             te ? (const uint32_t*)ctx->exc_off.p : nullptr,
-             te ? (const uint32_t*)ctx->exc_pos.p : nullptr,
-             te ? (const uint8_t*)ctx->exc_code.p : nullptr, n_reads, tw};
   nt_out O{(uint16_t*)ctx->wc.p, (int32_t*)ctx->start.p, (int32_t*)ctx->end.p,
            (double*)ctx->dens.p, (uint8_t*)ctx->flags.p, hits ? (uint32_t*)ctx->hits.p : nullptr};
   rc = nt_scan_call(ctx, &B, &O, ml);

@@ -643,6 +643,90 @@ nt_layout_kernel(uint64_t n_reads, uint64_t nblk, uint64_t read_len, uint64_t nw
   }
 }
 
+// ============================================================== filter
+//
+// --use_filter (filter_reads / filter_density, NanoTel.R:2083-2163): one lane
+// per read.  Reads shorter than 1e3 are dropped; otherwise the density of
+// the union of the exact fixed=FALSE matches of the patterns inside the
+// 200-base edge sub-read [70, 270) (left) or [n-270, n-70) (right, 0-based)
+// must reach 0.8 * min_density, i.e. covered >= thr_count (host-computed).
+// The sub-read is 8 plane words from one batch of 9 independent block loads.
+__global__ void __launch_bounds__(256)
+nt_filter_kernel(const NtProgram* __restrict__ prog, NtBatch B, uint8_t* __restrict__ keep,
+                 uint32_t thr_count, int right_edge) {
+  for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < B.n_reads;
+       r += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t n = B.len[r];
+    if (n < 1000u) {
+      keep[r] = 0;
+      continue;
+    }
+    ReadCtx rc;
+    rc.n = n;
+    rc.nblk = (int32_t)((n + 31u) >> 5);
+    rc.blk = reinterpret_cast<const uint2*>(B.planes) + B.blk_off[r];
+    rc.n_exc = 0;
+    rc.exc_pos = nullptr;
+    rc.exc_code = nullptr;
+    if (B.exc_off) {
+      const uint32_t e0 = B.exc_off[r], e1 = B.exc_off[r + 1];
+      rc.n_exc = (int32_t)(e1 - e0);
+      rc.exc_pos = B.exc_pos + e0;
+      rc.exc_code = B.exc_code + e0;
+    }
+    const int lo = right_edge ? (int)n - 270 : 70, hi = lo + 199;
+    uint32_t Lw[8], Hw[8], Vw[8];
+    {
+      const int bb = lo >> 5;
+      const uint32_t sh = (uint32_t)(lo & 31);
+      uint2 blk[9];
+#pragma unroll
+      for (int t = 0; t < 9; ++t) blk[t] = bb + t < rc.nblk ? rc.blk[bb + t] : make_uint2(0u, 0u);
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        Lw[t] = funnel(blk[t + 1].x, blk[t].x, sh);
+        Hw[t] = funnel(blk[t + 1].y, blk[t].y, sh);
+        Vw[t] = range_mask((int64_t)lo + 32 * t, lo, hi);
+      }
+    }
+    uint32_t cov[7];
+#pragma unroll
+    for (int h = 0; h < 7; ++h) cov[h] = 0u;
+    for (int pi = 0; pi < prog->n_pat; ++pi) {
+      const NtPat& P = prog->pat[pi];
+      const int m = P.m;
+      uint32_t x0[7];
+#pragma unroll
+      for (int h = 0; h < 7; ++h) x0[h] = 0xFFFFFFFFu;
+      for (int j = 0; j < m; ++j) {
+        // fixed=FALSE: pattern letter j matches base c iff (code & (1 << c)) != 0
+        const uint32_t code = P.code[j];
+        const uint32_t t0 = (code & 1u) ? ~0u : 0u, t1 = (code & 2u) ? ~0u : 0u;
+        const uint32_t t2 = (code & 4u) ? ~0u : 0u, t3 = (code & 8u) ? ~0u : 0u;
+#pragma unroll
+        for (int h = 0; h < 7; ++h) {
+          const uint32_t Ls = funnel(Lw[h + 1], Lw[h], (uint32_t)j);
+          const uint32_t Hs = funnel(Hw[h + 1], Hw[h], (uint32_t)j);
+          x0[h] &= bfi(Hs, bfi(Ls, t3, t2), bfi(Ls, t1, t0)) & funnel(Vw[h + 1], Vw[h], (uint32_t)j);
+        }
+      }
+      if (rc.n_exc) {
+#pragma unroll
+        for (int h = 0; h < 7; ++h) {
+          uint32_t a1 = 0u;
+          patch_exceptions(rc, (int64_t)lo + 32 * h, lo, hi, P, false, x0[h], a1, true);
+        }
+      }
+#pragma unroll
+      for (int h = 0; h < 7; ++h) cov[h] |= spread(x0[h], h ? x0[h - 1] : 0u, m);
+    }
+    uint32_t c = 0;
+#pragma unroll
+    for (int h = 0; h < 7; ++h) c += __builtin_popcount(cov[h] & Vw[h]);
+    keep[r] = c >= thr_count ? 1 : 0;
+  }
+}
+
 }  // namespace nt
 
 // ================================================================ launchers
@@ -731,6 +815,13 @@ int nt_dev_scan_blocks_per_cu(int single, int one, int m6, int lds, size_t lds_b
 hipError_t nt_dev_launch_call(const NtProgram* prog, const NtBatch* B, const NtOut* O,
                               const uint64_t* tmask, int call_grid, hipStream_t stream) {
   hipLaunchKernelGGL(nt::nt_call_kernel, dim3(call_grid), dim3(256), 0, stream, prog, *B, *O, tmask);
+  return hipGetLastError();
+}
+
+hipError_t nt_dev_launch_filter(const NtProgram* prog, const NtBatch* B, uint8_t* keep,
+                                uint32_t thr_count, int right_edge, int grid, hipStream_t stream) {
+  hipLaunchKernelGGL(nt::nt_filter_kernel, dim3(grid), dim3(256), 0, stream, prog, *B, keep, thr_count,
+                     right_edge);
   return hipGetLastError();
 }
 

@@ -94,6 +94,8 @@ SIGNATURES = {
     "nt_kernel_times": (ctypes.c_int64, [_P, ctypes.POINTER(ctypes.c_double),
                                          ctypes.POINTER(ctypes.c_double)]),
     "nt_analyze_host": (ctypes.c_int, [_P, _P, _P, ctypes.c_uint64, _P, _P, _P, _P, _P, _P]),
+    "nt_filter_call": (ctypes.c_int, [_P, _P, _P]),
+    "nt_filter_host": (ctypes.c_int, [_P, _P, _P, ctypes.c_uint64, _P]),
     "nt_assign_serials": (ctypes.c_int64, [_P, ctypes.c_uint64, ctypes.POINTER(ctypes.c_double),
                                            ctypes.POINTER(ctypes.c_double), _P, _P]),
     "nt_reader_open": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),

@@ -152,6 +152,27 @@ class NanoTel:
             out["hits"] = hits[:, :self.n_hits]
         return out
 
+    def filter(self, seqs):
+        """--use_filter decision per read (bool array; True = kept), reads in
+        input orientation (the context's rc is applied as in analyze())."""
+        bseqs = [s.encode() if isinstance(s, str) else bytes(s) for s in seqs]
+        n = len(bseqs)
+        ptrs = (ctypes.c_char_p * max(1, n))(*bseqs)
+        lens = np.array([len(b) for b in bseqs], np.uint64)
+        return self._filter(ctypes.addressof(ptrs), lens, n)
+
+    def filter_chunk(self, chunk):
+        """filter() of an io.Reader chunk, zero-copy."""
+        return self._filter(chunk.seq_ptrs, chunk.lengths, chunk.n)
+
+    def _filter(self, ptrs_addr, lens, n):
+        keep = np.zeros(max(1, n), np.uint8)
+        if n:
+            lens = np.ascontiguousarray(lens, np.uint64)
+            _check(lib().nt_filter_host(self._h, ctypes.c_void_p(ptrs_addr), lens.ctypes.data, n,
+                                        keep.ctypes.data), self._h)
+        return keep[:n].astype(bool)
+
     def window_counts(self, res, read, p):
         """Window counts of pass p for read `read` from an analyze(want_windows) result."""
         nw = int(res["n_windows"][read])

@@ -5,7 +5,8 @@ block (NanoTel.R:30-93) and its argument checks (NanoTel.R:104-137).
 
 Multi-GPU: launch one process per GPU with torch.distributed.run; chunks are
 dealt round-robin to the ranks (driver.py / shard.py), rank 0 writes the
-summary.  --use_filter, --analysis and the plots are not part of this build.
+summary.  --use_filter runs the edge pre-filter on the GPU.  --analysis and
+the plots are not part of this build.
 """
 import argparse
 import os
@@ -55,8 +56,8 @@ def main(argv=None):
         sys.exit("Error: Missing required parameter:  --input_path")
     if a.format not in ("fasta", "fastq"):
         sys.exit("Error: Format should be a string fastq or fasta")
-    if a.use_filter or a.analysis:
-        sys.exit("Error: --use_filter / --analysis are not supported by this build")
+    if a.analysis:
+        sys.exit("Error: --analysis is not supported by this build")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dev = a.device if a.device is not None else local
@@ -70,7 +71,7 @@ def main(argv=None):
             min_density=a.min_density, subseq_length=a.subseq_length,
             check_right_edge=a.check_right_edge, tvr_patterns=a.tvr_patterns,
             legacy_no_ext=a.legacy_no_ext, device=dev, write_reads=not a.no_reads,
-            sci_threshold=a.readr_sci_threshold)
+            sci_threshold=a.readr_sci_threshold, use_filter=a.use_filter)
     finally:
         if world > 1:
             import torch.distributed as dist

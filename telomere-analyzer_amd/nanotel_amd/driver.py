@@ -9,8 +9,9 @@ then <basename>_summary.csv, reads_ids.txt and run.log (NanoTel.R:2340-2433).
 
 With torch.distributed initialised (one process per GPU), chunks are dealt
 round-robin to ranks and the serials are fixed by one all_reduce (shard.py);
-rank 0 writes the summary.  Plots, --analysis and --use_filter are out of
-scope of this build.
+rank 0 writes the summary.  --use_filter runs the edge pre-filter on the GPU
+(nt_filter_host, NanoTel.R:2083-2163, 2227-2232) and scans the kept reads
+only.  Plots and --analysis are out of scope of this build.
 """
 import os
 import time
@@ -86,9 +87,32 @@ def _summary_stats(v):
             f"3rd Qu. {q[3]:g}  Max. {q[4]:g}")
 
 
+def _scan_chunk(nt, ch, use_filter, write_reads, log):
+    """Scan + call one chunk (after --use_filter when on).  Returns
+    (rel_serials, row_order, rel_max, result, names, lengths, {read: seq})
+    over the reads that were scanned."""
+    names, lens = ch.names(), ch.lengths.copy()
+    if use_filter:
+        keep = np.flatnonzero(nt.filter_chunk(ch))
+        if keep.size == 0:
+            log("No read have passed the filteration at run_with_rc_and_filter!")
+            return None, np.zeros(0, np.int64), shard.SKIPPED, None, [], lens[:0], {}
+        seqs = [ch.seq(int(j)) for j in keep]
+        res = nt.analyze(seqs)
+        names = [names[int(j)] for j in keep]
+        lens = lens[keep]
+        get = seqs.__getitem__
+    else:
+        res = nt.analyze_chunk(ch)
+        get = lambda j: ch.seq(j)  # noqa: E731
+    rel, order, rmax = shard.chunk_relative(res["telomeric"])
+    seqs = {int(j): get(int(j)) for j in order} if write_reads else {}
+    return rel, order, rmax, res, names, lens, seqs
+
+
 def run(input_path, save_path, patterns, fmt="fastq", nrec=10000, rc=False, min_density=0.6,
         subseq_length=100, check_right_edge=False, tvr_patterns=None, legacy_no_ext=False,
-        device=0, write_reads=True, sci_threshold=None, log=print):
+        device=0, write_reads=True, sci_threshold=None, use_filter=False, log=print):
     """Run the pipeline; returns (summary rows, all read lengths) on rank 0."""
     import torch.distributed as dist
     dist_on = dist.is_available() and dist.is_initialized()
@@ -122,21 +146,16 @@ def run(input_path, save_path, patterns, fmt="fastq", nrec=10000, rc=False, min_
             lengths_all.append(ch.lengths.copy())
             if r == rank:
                 log(f"processing chunk {k + r + 1} ...")
-                res = nt.analyze_chunk(ch)
-                rel, order, rmax = shard.chunk_relative(res["telomeric"])
-                seqs = {int(j): ch.seq(int(j)) for j in order} if write_reads else {}
-                own = (r, rel, order, rmax, res, ch.names(), ch.lengths.copy(), seqs)
+                own = (r,) + _scan_chunk(nt, ch, use_filter, write_reads, log)
         if n_round == 0:
             break
         maxima = shard.exchange_rel_max({own[0]: own[3]} if own else {}, n_round)
         starts = np.empty(n_round, np.float64)
         for r in range(n_round):  # the reference's recurrence, chunk by chunk
-            starts[r] = s_next
-            v = s_next + maxima[r]
-            if v > m_run:
-                m_run = v
-            s_next = m_run + 1.0
-        if own is not None:
+            starts[r], s_next, m_run = shard.advance(s_next, m_run, float(maxima[r]))
+        if own is not None and own[4] is None:
+            local_rows[k + own[0]] = []  # --use_filter kept no read of this chunk
+        elif own is not None:
             r, rel, order, _, res, names, lens, seqs = own
             ser = shard.assign_chunk_serials(rel, starts[r])
             local_rows[k + r] = chunk_rows(res, names, lens, ser, order, nt.n_pass)

@@ -44,18 +44,32 @@ def chunk_relative(is_telo):
     return ser, order, mx
 
 
+# rel_max of a chunk that --use_filter emptied: the reference `next`s past it
+# (NanoTel.R:2229-2231), so serial_start is not recomputed.  Relative maxima
+# are -Inf or >= 0, so -1 survives the all_reduce(MAX) with -Inf elsewhere.
+SKIPPED = -1.0
+
+
+def advance(s, m, rel_max):
+    """One chunk of the reference's serial recurrence: returns (this chunk's
+    serial_start, next serial_start, running max(Serial)).
+    M = max(M, S + rel_max); S' = M + 1 (NanoTel.R:2258), same fp64 operations;
+    a SKIPPED chunk leaves S and M unchanged."""
+    if rel_max == SKIPPED:
+        return s, s, m
+    v = s + rel_max
+    if v > m:
+        m = v
+    return s, m + 1.0, m
+
+
 def serial_starts(rel_max):
     """serial_start of every chunk from the chunks' relative maxima, in chunk
-    order: S_0 = 1; M_k = max(M_{k-1}, S_k + rel_max_k); S_{k+1} = M_k + 1.
-    Same fp64 operations as the reference's running max(Serial) + 1."""
+    order: S_0 = 1; M_k = max(M_{k-1}, S_k + rel_max_k); S_{k+1} = M_k + 1."""
     starts = np.empty(len(rel_max), np.float64)
     s, m = 1.0, NEG_INF
     for k, r in enumerate(rel_max):
-        starts[k] = s
-        v = s + r
-        if v > m:
-            m = v
-        s = m + 1.0
+        starts[k], s, m = advance(s, m, float(r))
     return starts
 
 

@@ -50,6 +50,8 @@ def lib():
                                        ctypes.c_double, ctypes.c_int, ctypes.c_int,
                                        ctypes.POINTER(NtoRow), ctypes.POINTER(ctypes.c_uint32),
                                        ctypes.POINTER(ctypes.c_uint32)]
+        L.nto_filter_read.argtypes = [ctypes.c_char_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_double,
+                                      ctypes.c_int]
         L.nto_assign_serials.restype = ctypes.c_int64
         L.nto_assign_serials.argtypes = [ctypes.POINTER(ctypes.c_uint8), ctypes.c_int64,
                                          ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
@@ -130,6 +132,14 @@ def analyze_read(seq, pats, L=100, min_density=0.6, right_edge=False, legacy_no_
     if want_hits:
         out["hits"] = list(hc[:2 * pats.n_pat + pats.n_tvr])
     return out
+
+
+def filter_read(seq, pats, min_density=0.6, right_edge=False):
+    """--use_filter decision for one read in scan orientation (True = kept)."""
+    rc = lib().nto_filter_read(seq.encode(), len(seq), pats.h, min_density, int(right_edge))
+    if rc < 0:
+        raise OracleError(rc)
+    return bool(rc)
 
 
 def assign_serials(is_telo, serial_start=1.0, max_serial=-math.inf):

@@ -25,12 +25,23 @@ class OracleNanoTel:
         self.rc = rc
         self.n_pass = 3 if tvr_patterns else 2
 
+    def _scan_orientation(self, s):
+        s = s.decode() if isinstance(s, bytes) else s
+        return O.reverse_complement(s) if self.rc else s
+
+    def filter_chunk(self, ch):
+        return np.array([O.filter_read(self._scan_orientation(ch.seq(i)), self.P, self.kw["min_density"],
+                                       self.kw["right_edge"]) for i in range(ch.n)], bool)
+
     def analyze_chunk(self, ch):
-        n = ch.n
+        return self.analyze([ch.seq(i) for i in range(ch.n)])
+
+    def analyze(self, seqs):
+        n = len(seqs)
         res = {"start": np.full((n, 3), -1, np.int32), "end": np.full((n, 3), -1, np.int32),
                "density": np.zeros((n, 3)), "telomeric": np.zeros(n, bool)}
         for i in range(n):
-            s = ch.seq(i).decode()
+            s = seqs[i].decode() if isinstance(seqs[i], bytes) else seqs[i]
             if self.rc:
                 s = O.reverse_complement(s)
             r = O.analyze_read(s, self.P, **self.kw)
@@ -78,7 +89,7 @@ def _free_port():
     return p
 
 
-def _rank_main(rank, world, port, inp, out, rc):
+def _rank_main(rank, world, port, inp, out, rc, use_filter=False):
     import torch.distributed as dist
     from nanotel_amd import driver
     driver.NanoTel = OracleNanoTel
@@ -86,7 +97,7 @@ def _rank_main(rank, world, port, inp, out, rc):
         os.environ["MASTER_ADDR"] = "127.0.0.1"
         os.environ["MASTER_PORT"] = str(port)
         dist.init_process_group("gloo", rank=rank, world_size=world)
-    driver.run(inp, out, "TTAGGG", fmt="fasta", nrec=3, rc=rc, log=lambda *a: None)
+    driver.run(inp, out, "TTAGGG", fmt="fasta", nrec=3, rc=rc, use_filter=use_filter, log=lambda *a: None)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
@@ -125,3 +136,79 @@ def test_sharded_driver_matches_single_process(rc):
         assert [int(line.split(",")[0]) for line in summary[1:]] == sorted(
             int(line.split(",")[0]) for line in summary[1:])
         assert res[1]["reads_ids.txt"].decode().splitlines() == [line.split(",")[1] for line in summary[1:]]
+
+
+def _filter_input(d):
+    """Chunks of 3 (nrec=3) for --use_filter: chunk 1 loses every read to the
+    filter (short, or no telomeric edge), later chunks keep some."""
+    rng = np.random.default_rng(9)
+
+    def read(n, edge_tract):
+        s = list(rng.choice(list("ACGT"), n))
+        if edge_tract:
+            t = int(rng.integers(400, 1500))
+            s[:t] = list(("TTAGGG" * (t // 6 + 1))[:t])
+        return "".join(s)
+
+    recs = [("short_telo", read(900, True)), ("plain_a", read(3000, False)), ("plain_b", read(1500, False))]
+    for i in range(16):
+        recs.append((f"r{i}", read(int(rng.integers(1000, 5000)), i % 4 != 3)))
+    recs += [("plain_c", read(2000, False)), ("plain_d", read(2500, False)), ("plain_e", read(800, True))]
+    recs += [("last", read(3000, True))]
+    os.makedirs(os.path.join(d, "in"))
+    with open(os.path.join(d, "in", "a.fasta"), "w") as f:
+        for n, s in recs:
+            f.write(f">{n}\n{s}\n")
+    return os.path.join(d, "in"), recs
+
+
+def _reference_filter_rows(recs, nrec=3):
+    """run_future_worker_chuncks with use_filter (NanoTel.R:2209-2258) over the
+    oracle: a chunk the filter empties is skipped (`next`) without touching
+    serial_start; otherwise the kept reads are grouped and numbered as usual
+    and serial_start = max(all Serial) + 1."""
+    P = O.Patterns("TTAGGG")
+    serial_start, mx, rows = 1.0, -np.inf, []
+    for c in range(0, len(recs), nrec):
+        chunk = recs[c:c + nrec]
+        kept = [(n, s) for n, s in chunk if O.filter_read(s, P)]
+        if not kept:
+            continue
+        telo = np.array([O.analyze_read(s, P)["telomeric"] for _, s in kept], np.uint8)
+        ser, order, serial_start, mx = O.assign_serials(telo, serial_start, mx)
+        rows += [(float(ser[j]), kept[j][0]) for j in order]
+    return rows
+
+
+def test_use_filter_driver_matches_reference_flow():
+    import torch.multiprocessing as mp
+    with tempfile.TemporaryDirectory() as d:
+        inp, recs = _filter_input(d)
+        expect = _reference_filter_rows(recs)
+        assert 5 < len(expect) < 19
+        res = {}
+        for world in (1, 2):
+            out = os.path.join(d, f"out{world}")
+            if world == 1:
+                _rank_main(0, 1, 0, inp, out, False, True)
+            else:
+                mp.spawn(_rank_main, args=(world, _free_port(), inp, out, False, True), nprocs=world, join=True)
+            res[world] = _outputs(out)
+        assert res[1] == res[2]
+        lines = res[1]["in_summary.csv"].decode().splitlines()[1:]
+        got = [(float(x.split(",")[0]), x.split(",")[1]) for x in lines]
+        assert got == expect
+        assert got[0][0] == 1.0  # the emptied first chunk left serial_start at 1
+
+
+def test_filter_oracle_edges():
+    P = O.Patterns("TTAGGG")
+    tel = "TTAGGG" * 16  # 96 of 200 covered = 0.48 = 0.8 * 0.6
+    assert O.filter_read("A" * 70 + tel + "C" * 1000, P)
+    assert not O.filter_read("A" * 70 + tel[:-6] + "C" * 1000, P)
+    assert not O.filter_read("A" * 70 + tel + "C" * 763, P)  # 999 bases: dropped
+    assert not O.filter_read("A" * 71 + tel + "C" * 1000, P, min_density=0.61)
+    s = "C" * 1000 + tel + "A" * 70  # right edge sub-read [n-269, n-70]
+    assert O.filter_read(s, P, right_edge=True) and not O.filter_read(s, P)
+    # fixed=FALSE: a subject N matches any pattern letter
+    assert O.filter_read("A" * 70 + "N" * 96 + "C" * 1000, P)

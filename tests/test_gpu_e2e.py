@@ -67,3 +67,20 @@ def test_driver_gpu_matches_oracle_driver(tmp_path, rc):
     assert a == b
     assert len(a["in_summary.csv"].splitlines()) > 5
     assert np.all([k.endswith(".fasta.gz") or k in ("in_summary.csv", "reads_ids.txt") for k in a])
+
+
+def test_driver_use_filter_gpu_matches_oracle_driver(tmp_path):
+    from nanotel_amd import driver
+    from test_driver import _filter_input
+    inp, _ = _filter_input(str(tmp_path))
+    gpu_out, ora_out = str(tmp_path / "gpu"), str(tmp_path / "ora")
+    driver.run(inp, gpu_out, "TTAGGG", fmt="fasta", nrec=3, use_filter=True, log=lambda *a: None)
+    real = driver.NanoTel
+    try:
+        driver.NanoTel = OracleNanoTel
+        driver.run(inp, ora_out, "TTAGGG", fmt="fasta", nrec=3, use_filter=True, log=lambda *a: None)
+    finally:
+        driver.NanoTel = real
+    a, b = _outputs(gpu_out), _outputs(ora_out)
+    assert a == b
+    assert len(a["in_summary.csv"].splitlines()) > 5

@@ -307,3 +307,39 @@ def test_read_distribution_plans(plan):
     idx = list(range(0, len(seqs), 997))
     compare(nt, {k: v[idx] if isinstance(v, np.ndarray) and v.shape[:1] == (len(seqs),) else v
                  for k, v in res.items()}, oracle_rows([seqs[i] for i in idx], "TTAGGG"), check_windows=False)
+
+
+@pytest.mark.parametrize("cfg", [
+    dict(patterns="TTAGGG"),
+    dict(patterns="TTAGGG", check_right_edge=True),
+    dict(patterns="TTAGGG CCCTAA", min_density=0.5),
+    dict(patterns="YYAGGG", rc=True),
+    dict(patterns="ttaggn", min_density=0.7),
+    dict(patterns="TTAGGG", min_density=0.61),
+])
+def test_use_filter_matches_oracle(cfg):
+    # --use_filter (filter_reads/filter_density, NanoTel.R:2083-2163) on the GPU
+    rng = np.random.default_rng(zlib.crc32(str(sorted(cfg.items())).encode()))
+    right = cfg.get("check_right_edge", False)
+    motif = {"ttaggn": "TTAGGA"}.get(cfg["patterns"], "TTAGGG")
+    seqs = []  # scan orientation (the input is their reverse complement under rc)
+    for i in range(400):
+        n = int(rng.choice([rng.integers(1, 999), rng.integers(999, 1002), rng.integers(1002, 6000)]))
+        s = list(np.array(list("ACGT"))[rng.integers(0, 4, n)])
+        if n >= 300 and i % 2 == 0:  # an edge tract of varying length around the threshold
+            t = int(rng.integers(40, 200))
+            a = n - 270 + int(rng.integers(-20, 20)) if right else 70 + int(rng.integers(-20, 20))
+            a = max(0, min(a, n - t))
+            for j in range(t):
+                s[a + j] = motif[j % 6] if rng.random() > 0.03 else "ACGT"[rng.integers(0, 4)]
+        if i % 5 == 0:  # subject ambiguity letters / lowercase
+            for j in rng.integers(0, n, max(1, n // 100)):
+                s[j] = "NRYKMSWBDHVnacgt"[rng.integers(0, 16)]
+        seqs.append("".join(s))
+    nt = _nt(**cfg)
+    keep = nt.filter([O.reverse_complement(s) for s in seqs] if cfg.get("rc") else seqs)
+    P = O.Patterns(cfg["patterns"])
+    want = [O.filter_read(s, P, cfg.get("min_density", 0.6), right) for s in seqs]
+    bad = [i for i in range(len(seqs)) if bool(keep[i]) != want[i]]
+    assert not bad, (len(bad), bad[:5])
+    assert 20 < sum(want) < 380
