@@ -40,7 +40,7 @@ hipError_t nt_dev_launch_uniform_layout(uint64_t n_reads, uint64_t nblk, uint64_
 }
 
 int nt_jit_blocks_per_cu(void* fn, size_t lds_bytes);
-bool nt_jit_get(int device, const NtProgram& P, void** fn_lds, void** fn_gmem, std::string& err);
+bool nt_jit_get(int device, const NtProgram& P, void* fn[4], std::string& err);
 hipError_t nt_jit_launch(void* fn, int grid, size_t lds_bytes, hipStream_t stream,
                          const NtProgram* prog, const uint32_t* thr, const NtBatch* B,
                          const NtOut* O, uint64_t* tmask, unsigned long long* queue,
@@ -203,8 +203,7 @@ struct nt_ctx {
   std::vector<std::array<hipEvent_t, 3>> ev;
   size_t n_ev = 0;  // calls recorded since the last nt_kernel_times
   bool jit = false;  // hiprtc-specialised scan kernels (nt_jit.cpp)
-  void* jit_lds = nullptr;
-  void* jit_gmem = nullptr;
+  void* jit_fn[4] = {};  // [no hit counters ? 2 : 0] + [global scratch ? 1 : 0]
   std::string jit_err;
   NtProgram prog{};
   nt_params params{};
@@ -380,7 +379,7 @@ int nt_compile(nt_ctx* ctx, const nt_params* prm, nt_program_info* info) {
   ctx->prog = P;
   ctx->params = *prm;
   ctx->compiled = true;
-  ctx->jit = nt_jit_get(ctx->device, P, &ctx->jit_lds, &ctx->jit_gmem, ctx->jit_err);
+  ctx->jit = nt_jit_get(ctx->device, P, ctx->jit_fn, ctx->jit_err);
   if (info) {
     info->n_pass = P.n_pass;
     info->n_pat = P.n_pat;
@@ -592,10 +591,15 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
   const uint32_t ww_lds = nt_dev_wave_words(noslots, nh, np, cap_nw);
   const size_t lds_bytes = (size_t)ww_lds * 4u * 4u;
   // exactly the resident blocks (the waves take reads from a queue)
-  int bpc = ctx->jit ? nt_jit_blocks_per_cu(ctx->jit_lds, lds_bytes)
+  void* jit_lds = ctx->jit_fn[O.hits ? 0 : 2];
+  void* jit_gmem = ctx->jit_fn[O.hits ? 1 : 3];
+  int bpc = ctx->jit ? nt_jit_blocks_per_cu(jit_lds, lds_bytes)
                      : nt_dev_scan_blocks_per_cu(single, one, m6, 1, lds_bytes);
   if (bpc <= 0) bpc = 1;
   if (bpc_cap > 0) bpc = std::min(bpc, bpc_cap);
+  // fault isolation (debugging): NT_DBG_SKIP_SCAN / NT_DBG_SKIP_CALL launch only the other kernel
+  const bool dbg_skip_scan = std::getenv("NT_DBG_SKIP_SCAN") != nullptr;
+  const bool dbg_skip_call = std::getenv("NT_DBG_SKIP_CALL") != nullptr;
   const uint32_t ww_g = nt_dev_wave_words(noslots, nh, np, max_nw);
   const uint64_t grid_g = std::max<uint64_t>(1, std::min<uint64_t>((batch->n_reads + 3) / 4, (uint64_t)ctx->cu_count * 2));
   if (two && (e = ctx->scratch.ensure(grid_g * 4 * (uint64_t)ww_g * 4)) != hipSuccess)
@@ -622,16 +626,37 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
     const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((nr + 3) / 4, (uint64_t)ctx->cu_count * bpc));
     const QueuePlan qp = queue_plan(nr, batch->n_windows * (uint64_t)L / batch->n_reads, grid * 4);
     const uint32_t claim = qp.claim, nstatic = qp.nstatic;
-    if (ctx->jit)
-      e = nt_jit_launch(ctx->jit_lds, (int)grid, lds_bytes, ctx->stream, ctx->prog_dev,
-                        (const uint32_t*)ctx->thr.p, &Bk, &Ok, tmk, q, 0u, (uint32_t)len_cap, claim, nstatic, ww_lds, nullptr);
+    // NT_DBG_CHECK_PLANES=<planes in 16-byte segments> (debugging, with the
+    // scan JIT-built with -DNT_DBG_CHECK=1): address checks, report on stderr
+    uint64_t* dbg = nullptr;
+    if (const char* v = std::getenv("NT_DBG_CHECK_PLANES")) {
+      if (hipMalloc(&dbg, 9 * 8) == hipSuccess) {
+        const uint64_t h[9] = {std::strtoull(v, nullptr, 10), batch->n_windows * (uint64_t)np, tmw, 0, 0, 0, 0, 0, 0};
+        (void)hipMemcpy(dbg, h, sizeof h, hipMemcpyHostToDevice);
+      }
+    }
+    if (dbg_skip_scan)
+      e = hipSuccess;
+    else if (ctx->jit)
+      e = nt_jit_launch(jit_lds, (int)grid, lds_bytes, ctx->stream, ctx->prog_dev,
+                        (const uint32_t*)ctx->thr.p, &Bk, &Ok, tmk, q, 0u, (uint32_t)len_cap, claim, nstatic, ww_lds,
+                        (uint32_t*)dbg);
     else
       e = nt_dev_launch(ctx->prog_dev, (const uint32_t*)ctx->thr.p, &Bk, &Ok, tmk, q, 0u, (uint32_t)len_cap, claim, nstatic,
                         single, one, m6, 1, ww_lds, nullptr, (int)grid, 0, ctx->stream);
+    if (dbg && e == hipSuccess) {
+      uint64_t h[9];
+      (void)hipStreamSynchronize(ctx->stream);
+      (void)hipMemcpy(h, dbg, sizeof h, hipMemcpyDeviceToHost);
+      std::fprintf(stderr, "NT_DBG_CHECK: %llu violations; first kind %llu index %llu read %llu limit %llu\n",
+                   (unsigned long long)h[4], (unsigned long long)h[5], (unsigned long long)h[6],
+                   (unsigned long long)h[7], (unsigned long long)h[8]);
+      (void)hipFree(dbg);
+    }
     if (e != hipSuccess) return hip_fail(ctx, e, "launch nt_scan_kernel<lds>");
     if (two) {
       if (ctx->jit)
-        e = nt_jit_launch(ctx->jit_gmem, (int)grid_g, 0, ctx->stream, ctx->prog_dev, (const uint32_t*)ctx->thr.p,
+        e = nt_jit_launch(jit_gmem, (int)grid_g, 0, ctx->stream, ctx->prog_dev, (const uint32_t*)ctx->thr.p,
                           &Bk, &Ok, tmk, q + NT_QUEUE_WORDS, (uint32_t)len_cap, 0xFFFFFFFFu, 1u, 0u, ww_g, (uint32_t*)ctx->scratch.p);
       else
         e = nt_dev_launch(ctx->prog_dev, (const uint32_t*)ctx->thr.p, &Bk, &Ok, tmk, q + NT_QUEUE_WORDS, (uint32_t)len_cap,
@@ -639,10 +664,12 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
                           ctx->stream);
       if (e != hipSuccess) return hip_fail(ctx, e, "launch nt_scan_kernel<global>");
     }
-    const uint64_t call_grid = std::max<uint64_t>(1, std::min<uint64_t>((nr + 255) / 256, (uint64_t)ctx->cu_count * 64));
+    // one lane per (read, pass): 2 lanes per read, 4 with TVRs
+    const uint64_t call_lanes = nr * (np <= 2 ? 2u : 4u);
+    const uint64_t call_grid = std::max<uint64_t>(1, std::min<uint64_t>((call_lanes + 255) / 256, (uint64_t)ctx->cu_count * 64));
     if (nsub == 1) {
       if (ev) (void)hipEventRecord(ev[1], ctx->stream);
-      e = nt_dev_launch_call(ctx->prog_dev, &Bk, &Ok, tmk, (int)call_grid, ctx->stream);
+      e = dbg_skip_call ? hipSuccess : nt_dev_launch_call(ctx->prog_dev, &Bk, &Ok, tmk, (int)call_grid, ctx->stream);
     } else {
       // calling kernel of this sub-batch on the call stream, after its scan
       if ((e = hipEventRecord(ctx->ev_scan, ctx->stream)) != hipSuccess ||

@@ -28,7 +28,7 @@ namespace {
 
 struct JitEntry {
   hipModule_t mod = nullptr;
-  hipFunction_t lds = nullptr, gmem = nullptr;
+  hipFunction_t fn[4] = {};  // [no hits ? 2 : 0] + [global scratch ? 1 : 0]
   std::string err;
 };
 
@@ -60,22 +60,29 @@ std::string jit_source(const NtProgram& P) {
 #else
 #define NT_SCAN_ATTR
 #endif
-extern "C" __global__ void __launch_bounds__(256) NT_SCAN_ATTR
-nt_scan_jit_lds(const NtProgram* __restrict__ prog, const uint32_t* __restrict__ thr, NtBatch B,
-                NtOut O, uint64_t* __restrict__ tmask, unsigned long long* __restrict__ queue,
-                uint32_t len_lo, uint32_t len_hi, uint32_t claim, uint32_t nstatic, uint32_t wave_words, uint32_t* __restrict__ gscr) {
-  extern __shared__ uint32_t smem[];
-  nt::scan_reads<JitSet, true>(prog, thr, B, O, tmask, queue, len_lo, len_hi, claim, nstatic,
-                               smem + (threadIdx.x >> 6) * wave_words);
-}
-extern "C" __global__ void __launch_bounds__(256)
-nt_scan_jit_gmem(const NtProgram* __restrict__ prog, const uint32_t* __restrict__ thr, NtBatch B,
-                 NtOut O, uint64_t* __restrict__ tmask, unsigned long long* __restrict__ queue,
-                 uint32_t len_lo, uint32_t len_hi, uint32_t claim, uint32_t nstatic, uint32_t wave_words, uint32_t* __restrict__ gscr) {
-  const uint64_t gw = (uint64_t)blockIdx.x * nt::kNWaves + (threadIdx.x >> 6);
-  nt::scan_reads<JitSet, false>(prog, thr, B, O, tmask, queue, len_lo, len_hi, claim, nstatic,
-                                gscr + gw * wave_words);
-}
+#define NT_JIT_KERNELS(NAME, HITS)                                                                     \
+  extern "C" __global__ void __launch_bounds__(256) NT_SCAN_ATTR                                       \
+  NAME##_lds(const NtProgram* __restrict__ prog, const uint32_t* __restrict__ thr, NtBatch B, NtOut O, \
+             uint64_t* __restrict__ tmask, unsigned long long* __restrict__ queue, uint32_t len_lo,    \
+             uint32_t len_hi, uint32_t claim, uint32_t nstatic, uint32_t wave_words,                   \
+             uint32_t* __restrict__ gscr) {                                                           \
+    extern __shared__ uint32_t smem[];                                                                 \
+    nt::scan_reads<JitSet, true, HITS>(prog, thr, B, O, tmask, queue, len_lo, len_hi, claim, nstatic,  \
+                                       smem + (threadIdx.x >> 6) * wave_words,                         \
+                                       reinterpret_cast<nt::DbgRec*>(gscr));                           \
+  }                                                                                                    \
+  extern "C" __global__ void __launch_bounds__(256)                                                    \
+  NAME##_gmem(const NtProgram* __restrict__ prog, const uint32_t* __restrict__ thr, NtBatch B, NtOut O,\
+              uint64_t* __restrict__ tmask, unsigned long long* __restrict__ queue, uint32_t len_lo,   \
+              uint32_t len_hi, uint32_t claim, uint32_t nstatic, uint32_t wave_words,                  \
+              uint32_t* __restrict__ gscr) {                                                          \
+    const uint64_t gw = (uint64_t)blockIdx.x * nt::kNWaves + (threadIdx.x >> 6);                       \
+    nt::scan_reads<JitSet, false, HITS>(prog, thr, B, O, tmask, queue, len_lo, len_hi, claim, nstatic, \
+                                        gscr + gw * wave_words);                                       \
+  }
+// with the matchPattern hit counters, and without (the caller passed no hits buffer)
+NT_JIT_KERNELS(nt_scan_jit, true)
+NT_JIT_KERNELS(nt_scan_jit_nh, false)
 )";
   return s;
 }
@@ -125,8 +132,8 @@ bool compile(int device, const std::string& src, JitEntry& e) {
   hiprtcGetCode(prog, code.data());
   hiprtcDestroyProgram(&prog);
   hipError_t he = hipModuleLoadData(&e.mod, code.data());
-  if (he == hipSuccess) he = hipModuleGetFunction(&e.lds, e.mod, "nt_scan_jit_lds");
-  if (he == hipSuccess) he = hipModuleGetFunction(&e.gmem, e.mod, "nt_scan_jit_gmem");
+  const char* names4[4] = {"nt_scan_jit_lds", "nt_scan_jit_gmem", "nt_scan_jit_nh_lds", "nt_scan_jit_nh_gmem"};
+  for (int i = 0; i < 4 && he == hipSuccess; ++i) he = hipModuleGetFunction(&e.fn[i], e.mod, names4[i]);
   if (he != hipSuccess) {
     e.err = std::string("hipModuleLoadData: ") + hipGetErrorString(he);
     return false;
@@ -136,9 +143,10 @@ bool compile(int device, const std::string& src, JitEntry& e) {
 
 }  // namespace
 
-// Returns true with the two kernels of the program's pattern set, false (and
-// a message) when specialisation is off or failed.
-bool nt_jit_get(int device, const NtProgram& P, void** fn_lds, void** fn_gmem, std::string& err) {
+// Returns true with the four kernels of the program's pattern set (fn[i]:
+// i = [no hit counters ? 2 : 0] + [global scratch ? 1 : 0]), false (and a
+// message) when specialisation is off or failed.
+bool nt_jit_get(int device, const NtProgram& P, void* fn[4], std::string& err) {
   const char* env = std::getenv("NT_JIT");
   if (env && env[0] == '0') {
     err = "NT_JIT=0";
@@ -154,12 +162,11 @@ bool nt_jit_get(int device, const NtProgram& P, void** fn_lds, void** fn_gmem, s
     compile(device, src, e);
     it = g_cache.emplace(key, e).first;
   }
-  if (!it->second.lds) {
+  if (!it->second.fn[3]) {
     err = it->second.err;
     return false;
   }
-  *fn_lds = (void*)it->second.lds;
-  *fn_gmem = (void*)it->second.gmem;
+  for (int i = 0; i < 4; ++i) fn[i] = (void*)it->second.fn[i];
   return true;
 }
 

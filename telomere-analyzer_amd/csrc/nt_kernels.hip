@@ -46,10 +46,19 @@ nt_scan_kernel(const NtProgram* __restrict__ prog, const uint32_t* __restrict__ 
 }
 
 // ================================================================= call
+//
+// The calling kernel is bound by dependent memory round trips (one lane per
+// read-pass walks its read), so each step loads what it needs as one batch of
+// independent loads: the telomeric-bitmask words up front (reads of <= 512
+// windows), the counts of a run four windows at a time, both A10
+// neighbourhoods together, both edge-extension plane windows together, and
+// the two partial windows of a range count together with its checkpoints.
 
 struct Pos {
   int s, e;
 };
+
+constexpr int kTmRegs = 8;  // bitmask words held in registers
 
 // Per-lane state of one read-pass.
 struct Lane {
@@ -62,22 +71,39 @@ struct Lane {
   int k;         // 0 for P1, 1 for P2/P3
   bool use_tvr;  // P3
   bool raw;      // P1 raw views (single fixed pattern, NanoTel.R:349-355)
+  bool tm_reg;   // tmw holds tm[0 .. nmw)
+  uint64_t tmw[kTmRegs];
 };
 
 __device__ __forceinline__ int wstart(const Lane& c, int i) { return 1 + i * c.L; }
 __device__ __forceinline__ int wend(const Lane& c, int i) { return i == c.nw - 1 ? c.n : wstart(c, i) + c.L - 1; }
 __device__ __forceinline__ int wcount(const Lane& c, int i) { return c.cnt[i]; }
-__device__ __forceinline__ double wdens(const Lane& c, int i) {
-  return (double)wcount(c, i) / (double)(wend(c, i) - wstart(c, i) + 1);
+__device__ __forceinline__ double wdens_of(const Lane& c, int i, int cnt) {
+  return (double)cnt / (double)(wend(c, i) - wstart(c, i) + 1);
+}
+
+__device__ __forceinline__ void tm_preload(Lane& c) {
+  c.tm_reg = c.nmw > 0 && c.nmw <= kTmRegs;
+  if (!c.tm_reg) return;
+#pragma unroll
+  for (int t = 0; t < kTmRegs; ++t) c.tmw[t] = t < c.nmw ? c.tm[t] : 0ull;
 }
 
 __device__ __forceinline__ uint64_t tword(const Lane& c, int wi, bool inv) {
-  const uint64_t x = c.tm[wi];
+  uint64_t x;
+  if (c.tm_reg) {
+    x = c.tmw[0];
+#pragma unroll
+    for (int t = 1; t < kTmRegs; ++t)
+      if (wi == t) x = c.tmw[t];
+  } else {
+    x = c.tm[wi];
+  }
   return inv ? ~x : x;
 }
-__device__ __forceinline__ bool tbit(const Lane& c, int i) { return (c.tm[i >> 6] >> (i & 63)) & 1ull; }
+__device__ __forceinline__ bool tbit(const Lane& c, int i) { return (tword(c, i >> 6, false) >> (i & 63)) & 1ull; }
 
-__device__ int next_set(const Lane& c, int pos, bool inv) {
+__device__ __forceinline__ int next_set(const Lane& c, int pos, bool inv) {
   if (pos >= c.nw) return c.nw;
   int wi = pos >> 6;
   uint64_t x = tword(c, wi, inv) & (~0ull << (pos & 63));
@@ -91,7 +117,7 @@ __device__ int next_set(const Lane& c, int pos, bool inv) {
   }
 }
 
-__device__ int prev_set(const Lane& c, int pos, bool inv) {
+__device__ __forceinline__ int prev_set(const Lane& c, int pos, bool inv) {
   if (pos < 0) return -1;
   if (pos >= c.nw) pos = c.nw - 1;
   int wi = pos >> 6;
@@ -104,35 +130,14 @@ __device__ int prev_set(const Lane& c, int pos, bool inv) {
   }
 }
 
-// ------------------------------------------------- coverage from the planes
-
-// Coverage bits of positions [q, q+31] of this pass (0 outside the read):
-// OR over the pass's patterns of the trimmed views starting in [q-31, q+31].
-__device__ uint32_t cov32(const Lane& c, int q) {
-  const NtProgram* prog = c.prog;
-  uint32_t cov = 0u;
-  const int npt = prog->n_pat + (c.use_tvr ? prog->n_tvr : 0);
-  for (int i = 0; i < npt; ++i) {
-    const bool is_tvr = i >= prog->n_pat;
-    const NtPat& P = is_tvr ? prog->tvr[i - prog->n_pat] : prog->pat[i];
-    uint32_t p0, p1, c0w, c1w;
-    hits_at(c.rc, P, false, (int64_t)q - 32, 0, c.n - 1, p0, p1);
-    hits_at(c.rc, P, false, q, 0, c.n - 1, c0w, c1w);
-    const bool use_a1 = !is_tvr && c.k;
-    cov |= spread<0>(use_a1 ? c1w : c0w, use_a1 ? p1 : p0, P.m);
-  }
-  return cov & range_mask(q, 0, c.n - 1);
-}
-
 // ------------------------------------------- boundary neighbourhoods
 //
 // The calling touches the coverage only near a few positions (the partial
 // windows of range_count, the A10 boundary refinements).  A neighbourhood
-// computes the pass's coverage words over [q0, q0 + 32K) at once: one batch
-// of K+5 independent block loads, then the bit-sliced match of every pattern
-// at every start with the letter tables hoisted out of the word loop --
-// instead of a chain of dependent per-word recomputations (cov32), which
-// held the calling kernel on memory latency.
+// computes the pass's coverage words over [q0, q0 + 32K) at once from one
+// batch of K+5 block loads (nb_fetch), then the bit-sliced match of every
+// pattern at every start with the letter tables hoisted out of the word loop
+// (nb_compute).
 // cov[i + 1] = coverage of [q0 + 32i, q0 + 32i + 31] for i = -1..K (kMarks: the
 // two neighbour words run marks need; else i = 0..K-1 are meaningful);
 // rs/re: P1's raw view starts / ends (c.raw) at the same positions.
@@ -144,8 +149,26 @@ struct Nb {
   uint32_t re[kMarks ? K + 2 : 1];
 };
 
+template <int K, bool kMarks = true>
+struct NbBlocks {
+  uint2 b[K + (kMarks ? 2 : 0) + 3];
+};
+
 template <int K, bool kMarks>
-__device__ __forceinline__ void nb_build(const Lane& c, int q0, Nb<K, kMarks>& nb) {
+__device__ __forceinline__ void nb_fetch(const Lane& c, int q0, NbBlocks<K, kMarks>& f) {
+  constexpr int E = kMarks ? 1 : 0;
+  constexpr int NP = K + 2 * E + 2;
+  const int bb = (q0 >> 5) - E - 1;  // arithmetic shift: floor for q0 < 0
+#pragma unroll
+  for (int t = 0; t <= NP; ++t) {
+    const int b = bb + t;
+    f.b[t] = (b >= 0 && b < c.rc.nblk) ? c.rc.blk[b] : make_uint2(0u, 0u);
+  }
+}
+
+template <int K, bool kMarks>
+__device__ __forceinline__ void nb_compute(const Lane& c, int q0, const NbBlocks<K, kMarks>& f,
+                                           Nb<K, kMarks>& nb) {
   constexpr int E = kMarks ? 1 : 0;  // extra word each side
   constexpr int NC = K + 2 * E;      // coverage words computed, i = -E..K-1+E
   constexpr int NP = NC + 2;         // plane words, positions [q0 + 32i, +31], i = -E-1..K+E
@@ -153,22 +176,12 @@ __device__ __forceinline__ void nb_build(const Lane& c, int q0, Nb<K, kMarks>& n
   constexpr int T0 = -E - 1;         // index of plane / hit word 0
   nb.q0 = q0;
   uint32_t Lw[NP], Hw[NP], Vw[NP];
-  {
-    const int bb = (q0 >> 5) + T0;  // arithmetic shift: floor for q0 < 0
-    const uint32_t sh = (uint32_t)(q0 & 31);
-    uint2 blk[NP + 1];
+  const uint32_t sh = (uint32_t)(q0 & 31);
 #pragma unroll
-    for (int t = 0; t <= NP; ++t) {
-      const int b = bb + t;
-      const bool ok = b >= 0 && b < c.rc.nblk;
-      blk[t] = ok ? c.rc.blk[b] : make_uint2(0u, 0u);
-    }
-#pragma unroll
-    for (int t = 0; t < NP; ++t) {
-      Lw[t] = funnel(blk[t + 1].x, blk[t].x, sh);
-      Hw[t] = funnel(blk[t + 1].y, blk[t].y, sh);
-      Vw[t] = range_mask((int64_t)q0 + 32 * (t + T0), 0, c.n - 1);
-    }
+  for (int t = 0; t < NP; ++t) {
+    Lw[t] = funnel(f.b[t + 1].x, f.b[t].x, sh);
+    Hw[t] = funnel(f.b[t + 1].y, f.b[t].y, sh);
+    Vw[t] = range_mask((int64_t)q0 + 32 * (t + T0), 0, c.n - 1);
   }
 #pragma unroll
   for (int i = 0; i < K + 2; ++i) nb.cov[i] = 0u;
@@ -269,14 +282,37 @@ __device__ __forceinline__ int nb_max_end(const Lane& c, const Nb<K>& nb, int a1
 }
 
 // |coverage ∩ [x, y]| (0-based positions), 128 bases per neighbourhood
-__device__ __noinline__ int cov_count(const Lane& c, int x, int y) {
+__device__ __forceinline__ int cov_count(const Lane& c, int x, int y) {
   int tot = 0;
   for (int q = x; q <= y; q += 128) {
+    NbBlocks<4, false> f;
     Nb<4, false> nb;
-    nb_build(c, q, nb);
+    nb_fetch(c, q, f);
+    nb_compute(c, q, f, nb);
     tot += nb_count(nb, q, min(y, q + 127));
   }
   return tot;
+}
+
+// |coverage ∩ [x1, y1]| + |coverage ∩ [x2, y2]| (x > y: empty); both fetched
+// in one batch when each range spans at most 128 bases
+__device__ __forceinline__ int cov_count2(const Lane& c, int x1, int y1, int x2, int y2) {
+  if (y1 - x1 >= 128 || y2 - x2 >= 128) return cov_count(c, x1, y1) + cov_count(c, x2, y2);
+  NbBlocks<4, false> f1, f2;
+  nb_fetch(c, x1, f1);
+  nb_fetch(c, x2, f2);
+  int t = 0;
+  if (x1 <= y1) {
+    Nb<4, false> nb;
+    nb_compute(c, x1, f1, nb);
+    t += nb_count(nb, x1, y1);
+  }
+  if (x2 <= y2) {
+    Nb<4, false> nb;
+    nb_compute(c, x2, f2, nb);
+    t += nb_count(nb, x2, y2);
+  }
+  return t;
 }
 
 // sum(width(intersect(IRanges(a1, b1), ranges))): window counts for whole
@@ -293,7 +329,7 @@ __device__ __forceinline__ int cnt_before(const Lane& c, int k) {
   return t;
 }
 
-__device__ int range_count(const Lane& c, int a1, int b1) {
+__device__ __forceinline__ int range_count(const Lane& c, int a1, int b1) {
   const int a = (a1 < 1 ? 1 : a1) - 1, b = (b1 > c.n ? c.n : b1) - 1;
   if (a > b) return 0;
   if (c.nw == 0) return cov_count(c, a, b);
@@ -303,10 +339,9 @@ __device__ int range_count(const Lane& c, int a1, int b1) {
   const bool a_whole = a == ws_a, b_whole = b == we_b;
   if (ka == kb) return (a_whole && b_whole) ? wcount(c, ka) : cov_count(c, a, b);
   // whole windows from the running counts, partial end windows from coverage
-  int tot = cnt_before(c, b_whole ? kb + 1 : kb) - cnt_before(c, a_whole ? ka : ka + 1);
-  if (!a_whole) tot += cov_count(c, a, (ka + 1) * L - 1);
-  if (!b_whole) tot += cov_count(c, kb * L, b);
-  return tot;
+  const int whole = cnt_before(c, b_whole ? kb + 1 : kb) - cnt_before(c, a_whole ? ka : ka + 1);
+  return whole + cov_count2(c, a_whole ? 0 : a, a_whole ? -1 : (ka + 1) * L - 1, b_whole ? 0 : kb * L,
+                            b_whole ? -1 : b);
 }
 
 __device__ __forceinline__ double sub_density(const Lane& c, int s, int e) {
@@ -315,8 +350,9 @@ __device__ __forceinline__ double sub_density(const Lane& c, int s, int e) {
 
 // ---------------------------------------------------------------- A8 / A11
 
-// find_telo_position (NanoTel.R:973-1077) on the window bitmask.
-__device__ Pos find_telo_position(const Lane& c, int min_in_a_row, double thr) {
+// find_telo_position (NanoTel.R:973-1077) on the window bitmask; the scores
+// are summed in R's order, the counts of a run fetched four at a time.
+__device__ __forceinline__ Pos find_telo_position(const Lane& c, int min_in_a_row, double thr) {
   int pos = 0, found = -1, start = -1;
   for (;;) {
     const int r = next_set(c, pos, false);
@@ -324,9 +360,18 @@ __device__ Pos find_telo_position(const Lane& c, int min_in_a_row, double thr) {
     const int q = next_set(c, r, true) - 1;  // last window of the telomeric run
     if (q - r + 1 >= min_in_a_row) {
       double score = 0.0;
-      for (int j = r; j <= q; ++j) {
-        score = score + wdens(c, j);
-        if (j - r + 1 >= min_in_a_row && score >= thr) { found = j; break; }
+      for (int j0 = r; j0 <= q && found < 0; j0 += 4) {
+        int cn[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) cn[t] = wcount(c, min(j0 + t, q));
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int j = j0 + t;
+          if (j <= q && found < 0) {
+            score = score + wdens_of(c, j, cn[t]);
+            if (j - r + 1 >= min_in_a_row && score >= thr) found = j;
+          }
+        }
       }
       if (found >= 0) { start = wstart(c, r); break; }
     }
@@ -354,9 +399,18 @@ __device__ Pos find_telo_position(const Lane& c, int min_in_a_row, double thr) {
       const int r = rr > lo ? rr : lo;
       if (q - r + 1 >= min_in_a_row) {
         double score = 0.0;
-        for (int j = q; j >= r; --j) {
-          score = score + wdens(c, j);
-          if (q - j + 1 >= min_in_a_row && score >= thr) { hit = true; break; }
+        for (int j0 = q; j0 >= r && !hit; j0 -= 4) {
+          int cn[4];
+#pragma unroll
+          for (int t = 0; t < 4; ++t) cn[t] = wcount(c, max(j0 - t, r));
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const int j = j0 - t;
+            if (j >= r && !hit) {
+              score = score + wdens_of(c, j, cn[t]);
+              if (q - j + 1 >= min_in_a_row && score >= thr) hit = true;
+            }
+          }
         }
         if (hit) { end = wend(c, q); break; }
       }
@@ -369,7 +423,7 @@ __device__ Pos find_telo_position(const Lane& c, int min_in_a_row, double thr) {
 }
 
 // find_left_telo (NanoTel.R:906-959)
-__device__ Pos find_left_telo(const Lane& c) {
+__device__ __forceinline__ Pos find_left_telo(const Lane& c) {
   if (c.nw == 0) return Pos{1, 1};
   const int f = next_set(c, 0, false);
   if (f < c.nw && wstart(c, f) <= 200) return Pos{wstart(c, f), wend(c, next_set(c, f, true) - 1)};
@@ -378,7 +432,7 @@ __device__ Pos find_left_telo(const Lane& c) {
 }
 
 // find_right_telo (NanoTel.R:843-899).  err=true on a 0-row table.
-__device__ Pos find_right_telo(const Lane& c, bool& err) {
+__device__ __forceinline__ Pos find_right_telo(const Lane& c, bool& err) {
   if (c.nw == 0) { err = true; return Pos{1, 1}; }
   const int g = prev_set(c, c.nw - 1, false);
   if (g >= 0) {
@@ -391,41 +445,105 @@ __device__ Pos find_right_telo(const Lane& c, bool& err) {
 
 // ------------------------------------------------------------------ A10
 
-// get_accurate_start (NanoTel.R:1726-1764): every range it reads lies in
-// [s-37, s+98] (0-based), one neighbourhood [s-42, s+118)
-__device__ __noinline__ int accurate_start(const Lane& c, int s) {
-  if (s == -1) return -1;
-  Nb<5> nb;
-  nb_build(c, s - 42, nb);
-  const int a = max(s, 1) - 1, b = min(s + 49, c.n) - 1;
-  const double first_50 = (double)(a > b ? 0 : nb_count(nb, a, b)) / 50.0;
-  int t = s;
-  if (first_50 < 0.3) {
-    t = nb_min_start(c, nb, s + 48, s + 99, t);
-    t = nb_min_start(c, nb, s + 33, s + 48, t);
-  } else {
-    t = nb_min_start(c, nb, s, s + 99, t);
-    if (first_50 >= 0.72) t = nb_min_start(c, nb, s - 36, s - 1, t);
+// get_accurate_start (NanoTel.R:1726-1764) reads only ranges in [s-37, s+98]
+// and get_accurate_end (NanoTel.R:1692-1721) only ranges in [e-100, e+49]
+// (0-based; the offsets are hard-coded in the reference), so each is one
+// neighbourhood, [s-42, s+118) and [e-102, e+58); both fetched in one batch.
+__device__ __forceinline__ void accurate_both(const Lane& c, int s, int e, int& s_acc, int& e_acc) {
+  NbBlocks<5> fs, fe;
+  nb_fetch(c, s - 42, fs);
+  nb_fetch(c, e - 102, fe);
+  s_acc = -1;
+  e_acc = -1;
+  if (s != -1) {
+    Nb<5> nb;
+    nb_compute(c, s - 42, fs, nb);
+    const int a = max(s, 1) - 1, b = min(s + 49, c.n) - 1;
+    const double first_50 = (double)(a > b ? 0 : nb_count(nb, a, b)) / 50.0;
+    int t = s;
+    if (first_50 < 0.3) {
+      t = nb_min_start(c, nb, s + 48, s + 99, t);
+      t = nb_min_start(c, nb, s + 33, s + 48, t);
+    } else {
+      t = nb_min_start(c, nb, s, s + 99, t);
+      if (first_50 >= 0.72) t = nb_min_start(c, nb, s - 36, s - 1, t);
+    }
+    s_acc = t;
   }
-  return t;
-}
-
-// get_accurate_end (NanoTel.R:1692-1721): ranges in [e-100, e+49], one
-// neighbourhood [e-102, e+58)
-__device__ __noinline__ int accurate_end(const Lane& c, int e) {
-  if (e == -1) return -1;
-  Nb<5> nb;
-  nb_build(c, e - 102, nb);
-  const int t = nb_max_end(c, nb, e - 99, e, e);
-  return nb_max_end(c, nb, e + 1, e + 50, t);
+  if (e != -1) {
+    Nb<5> nb;
+    nb_compute(c, e - 102, fe, nb);
+    const int t = nb_max_end(c, nb, e - 99, e, e);
+    e_acc = nb_max_end(c, nb, e + 1, e + 50, t);
+  }
 }
 
 // ------------------------------------------------------------------ A12
 
+// Plane words of [q0, q0 + 32K) (q0 a multiple of 32; zero outside the read).
+// The four steps of one side of the edge extension match at bases within 33
+// (right) / 27 (left) of the lowest one, each over 64 positions, so one batch
+// of K = 5 block loads per side from the lowest base serves all of them.
+template <int K>
+struct Pw {
+  int q0;
+  uint32_t L[K], H[K];
+};
+
+template <int K>
+__device__ __forceinline__ void pw_load(const Lane& c, int q0, Pw<K>& w) {
+  w.q0 = q0;
+  const int b0 = q0 >> 5;
+#pragma unroll
+  for (int i = 0; i < K; ++i) {
+    const int b = b0 + i;
+    const uint2 x = (b >= 0 && b < c.rc.nblk) ? c.rc.blk[b] : make_uint2(0u, 0u);
+    w.L[i] = x.x;
+    w.H[i] = x.y;
+  }
+}
+
+// planes of [p, p + 31] (as plane_at), from the window when it holds them
+template <int K>
+__device__ __forceinline__ void pw_at(const Lane& c, const Pw<K>& w, int p, uint32_t& L, uint32_t& H) {
+  const int d = p - w.q0;
+  const int i = d >> 5;
+  if (d < 0 || i + 1 >= K) {
+    plane_at(c.rc, p, L, H);
+    return;
+  }
+  uint32_t l0 = w.L[0], h0 = w.H[0], l1 = w.L[1], h1 = w.H[1];
+#pragma unroll
+  for (int t = 1; t + 1 < K; ++t)
+    if (i == t) {
+      l0 = w.L[t];
+      h0 = w.H[t];
+      l1 = w.L[t + 1];
+      h1 = w.H[t + 1];
+    }
+  const uint32_t sh = (uint32_t)(d & 31);
+  L = funnel(l1, l0, sh);
+  H = funnel(h1, h0, sh);
+}
+
+// hits_at (nt_device.h) with the planes taken from the window
+template <int K>
+__device__ __forceinline__ void hits_at_w(const Lane& c, const Pw<K>& w, const NtPat& P, bool eq, int base,
+                                          int vlo, int vhi, uint32_t& a0, uint32_t& a1) {
+  uint32_t L0, H0, L1, H1;
+  pw_at(c, w, base, L0, H0);
+  pw_at(c, w, base + 32, L1, H1);
+  const uint32_t V0 = range_mask(base, vlo, vhi), V1 = range_mask((int64_t)base + 32, vlo, vhi);
+  hits32<true>(L0, L1, H0, H1, V0, V1, eq ? P.tm_eq : P.tm_scan, P.m, a0, a1);
+  if (P.m <= 1) a1 &= V0;
+  if (c.rc.n_exc) patch_exceptions(c.rc, base, vlo, vhi, P, eq, a0, a1);
+}
+
 // max end (right) / min start (left) of the fixed=TRUE matches of the pass's
 // pattern set in the sub-sequence [a1, b1], out-of-bound relative to the
 // sub-sequence (multi_pattern_step_right/left, NanoTel.R:496-575).
-__device__ bool step_extreme(const Lane& c, int a1, int b1, bool right, int& val) {
+template <int K>
+__device__ __forceinline__ bool step_extreme(const Lane& c, const Pw<K>& w, int a1, int b1, bool right, int& val) {
   const NtProgram* prog = c.prog;
   const int A = a1 - 1, Bz = b1 - 1, base = A - 1;
   const bool only_exact = c.use_tvr && c.k == 0;
@@ -437,7 +555,7 @@ __device__ bool step_extreme(const Lane& c, int a1, int b1, bool right, int& val
     const NtPat& P = is_tvr ? prog->tvr[i - prog->n_pat] : prog->pat[i];
     const int k = (is_tvr || only_exact) ? 0 : c.k;
     uint32_t a0, a1w;
-    hits_at(c.rc, P, true, base, A, Bz, a0, a1w);
+    hits_at_w(c, w, P, true, base, A, Bz, a0, a1w);
     const uint32_t h = k ? a1w : a0;
     if (!h) continue;
     any = true;
@@ -448,14 +566,16 @@ __device__ bool step_extreme(const Lane& c, int a1, int b1, bool right, int& val
   return any;
 }
 
-// search_right_patterns (NanoTel.R:635-697): width 18, step 10, 4 steps
-__device__ int search_right(const Lane& c, int end_index) {
+// search_right_patterns (NanoTel.R:635-697): width 18, step 10, 4 steps.
+// Match bases from max(min(end_index + 18, n) - 17, 1) - 2, up to +33.
+template <int K>
+__device__ __forceinline__ int search_right(const Lane& c, const Pw<K>& w, int end_index) {
   int subseq_end = min(end_index + 18, c.n);
   int new_end = end_index;
   for (int it = 0; it < 4; ++it) {
     const int curr_start = max(subseq_end - 17, 1);
     int v;
-    if (!step_extreme(c, curr_start, subseq_end, true, v)) break;
+    if (!step_extreme(c, w, curr_start, subseq_end, true, v)) break;
     new_end = v;
     const int ne = min(subseq_end + 11, c.n);
     if (ne == subseq_end) break;
@@ -464,14 +584,16 @@ __device__ int search_right(const Lane& c, int end_index) {
   return new_end;
 }
 
-// search_left_patterns (NanoTel.R:576-633)
-__device__ int search_left(const Lane& c, int start_index) {
+// search_left_patterns (NanoTel.R:576-633).  Match bases from
+// max(start_index - 18, 1) - 2 down to max(start_index - 45, 1) - 2.
+template <int K>
+__device__ __forceinline__ int search_left(const Lane& c, const Pw<K>& w, int start_index) {
   int subseq_start = max(start_index - 18, 1);
   int new_start = start_index;
   for (int it = 0; it < 4; ++it) {
     const int curr_end = min(subseq_start + 17, c.n);
     int v;
-    if (!step_extreme(c, subseq_start, curr_end, false, v)) break;
+    if (!step_extreme(c, w, subseq_start, curr_end, false, v)) break;
     new_start = v;
     const int ns = max(subseq_start - 9, 1);
     if (ns == subseq_start) break;
@@ -481,7 +603,8 @@ __device__ int search_left(const Lane& c, int start_index) {
 }
 
 // find_telo_position_wraper (NanoTel.R:1080-1155) + density (NanoTel.R:1840).
-__device__ void call_pass(const Lane& c, int& out_s, int& out_e, double& out_d, uint32_t& err) {
+__device__ __forceinline__ void call_pass(Lane& c, int& out_s, int& out_e, double& out_d, uint32_t& err) {
+  tm_preload(c);
   Pos tp = find_telo_position(c, 3, 2.0);
 #ifdef NT_DBG_NO_WRAP
   const double telo_density = 1.0;
@@ -498,8 +621,8 @@ __device__ void call_pass(const Lane& c, int& out_s, int& out_e, double& out_d, 
   const int s_acc = tp.s;
   int e_acc = tp.e;
 #else
-  const int s_acc = accurate_start(c, tp.s);
-  int e_acc = accurate_end(c, tp.e);
+  int s_acc, e_acc;
+  accurate_both(c, tp.s, tp.e, s_acc, e_acc);
 #endif
   if (s_acc > e_acc) e_acc = s_acc;
   tp = Pos{s_acc, e_acc};
@@ -517,9 +640,14 @@ __device__ void call_pass(const Lane& c, int& out_s, int& out_e, double& out_d, 
 #else
   if (!c.prog->legacy_no_ext) {
 #endif
+    // both sides' plane windows in one batch, then the step walks in registers
+    const int ei = tp.e + 1, si = tp.s - 1;
+    Pw<5> wr, wl;
+    pw_load(c, (max(min(ei + 18, c.n) - 17, 1) - 2) & ~31, wr);
+    pw_load(c, (max(si - 45, 1) - 2) & ~31, wl);
     int e2 = tp.e, s2 = tp.s;
-    if (tp.e < c.n) e2 = search_right(c, tp.e + 1);
-    if (tp.s > 1) s2 = search_left(c, tp.s - 1);
+    if (tp.e < c.n) e2 = search_right(c, wr, ei);
+    if (tp.s > 1) s2 = search_left(c, wl, si);
     tp = Pos{s2, e2};
   }
   if (tp.e < tp.s - 1) { err |= NT_FLAG_ERR_WIDTH; out_s = -1; out_e = -1; out_d = 0.0; return; }
@@ -532,9 +660,14 @@ __device__ void call_pass(const Lane& c, int& out_s, int& out_e, double& out_d, 
 #endif
 }
 
-// One lane per read (grid-stride over reads).  NT_CALL_WAVES_PER_EU trades
-// VGPRs for occupancy: with the boundary neighbourhoods (register arrays) 2
-// waves/SIMD and no spills measured best (1M x 10 kb: 0.86 ms at 4, 0.78 at 2).
+// One lane per (read, pass): the passes of a read are independent until the
+// row is assembled, so a read's G = 2 (P1, P2) or 4 (P1-P3 and an idle lane)
+// lanes call them side by side -- half the dependent memory round trips per
+// lane of a one-lane-per-read walk -- and combine flags / the max width over
+// the passes with lane shuffles (G divides 64 and the grid stride is a
+// multiple of 64, so a read's lanes share a wave).  NT_CALL_WAVES_PER_EU
+// trades VGPRs for occupancy: with the boundary neighbourhoods (register
+// arrays) 2 waves/SIMD and no spills measured best.
 #ifndef NT_CALL_WAVES_PER_EU
 #define NT_CALL_WAVES_PER_EU 2
 #endif
@@ -543,66 +676,91 @@ __global__ void __launch_bounds__(256) NT_CALL_ATTR
 nt_call_kernel(const NtProgram* __restrict__ prog, NtBatch B, NtOut O,
                const uint64_t* __restrict__ tmask) {
   const int np = prog->n_pass, L = prog->L;
-  for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < B.n_reads;
-       r += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t n32 = B.len[r];
-    if (B.blk_off[r] & 1u) {  // the scan skipped this read (layout contract)
-      for (int p = 0; p < 3; ++p) {
+  const int lg = np <= 2 ? 1 : 2;  // log2(G)
+  const uint64_t total = B.n_reads << lg;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t base = blockIdx.x * (uint64_t)blockDim.x; base < total; base += stride) {
+    const uint64_t idx = base + threadIdx.x;
+    const bool in = idx < total;  // whole waves stay in the loop for the shuffles
+    const uint64_t r = idx >> lg;
+    const int p = (int)(idx & ((1u << lg) - 1u));
+    int s = -1, e = -1;
+    double d = 0.0;
+    uint32_t flags = 0u;
+    int w = INT_MIN;
+    bool align = false;
+    if (in) {
+      const uint32_t n32 = B.len[r];
+      align = (B.blk_off[r] & 1u) != 0;  // the scan skipped this read (layout contract)
+      if (!align && p < np) {
+        Lane c;
+        c.rc.n = n32;
+        c.rc.nblk = (int32_t)((n32 + 31u) >> 5);
+        c.rc.blk = reinterpret_cast<const uint2*>(B.planes) + B.blk_off[r];
+        c.rc.n_exc = 0;
+        c.rc.exc_pos = nullptr;
+        c.rc.exc_code = nullptr;
+        if (B.exc_off) {
+          const uint32_t e0 = B.exc_off[r], e1 = B.exc_off[r + 1];
+          c.rc.n_exc = (int32_t)(e1 - e0);
+          c.rc.exc_pos = B.exc_pos + e0;
+          c.rc.exc_code = B.exc_code + e0;
+        }
+        c.prog = prog;
+        c.n = (int)n32;
+        c.L = L;
+        c.nw = (int)split_window_count(c.n, L);
+        c.nmw = (c.nw + 63) >> 6;
+        const uint64_t woff = B.win_off[r];
+        const uint64_t* tmr = tmask + aux_base(woff, r, np);
+        const uint32_t* ckr = reinterpret_cast<const uint32_t*>(tmr + np * aux_nmw(c.nw));
+        c.cnt = O.win_counts + woff * np + (uint64_t)p * c.nw;
+        c.tm = tmr + p * c.nmw;
+        c.ck = ckr + p * aux_nck(c.nw);
+        c.k = p == 0 ? 0 : 1;
+        c.use_tvr = p == 2;
+        c.raw = p == 0 && prog->raw_p1;
+        call_pass(c, s, e, d, flags);
+        if (s == -1) flags |= 1u << (NT_FLAG_NA_SHIFT + p);
+        w = e - s + 1;
+      }
+    }
+    // combine over the read's lanes
+    for (int o = 1; o < (1 << lg); o <<= 1) {
+      flags |= (uint32_t)__shfl_xor((int)flags, o, kWave);
+      w = max(w, __shfl_xor(w, o, kWave));
+    }
+    if (!in) continue;
+    if (align) {
+      if (p < 3) {
         O.start[r * 3 + p] = -1;
         O.end[r * 3 + p] = -1;
         O.density[r * 3 + p] = 0.0;
       }
-      O.flags[r] = (uint8_t)(NT_FLAG_DONE | NT_FLAG_ERR_ALIGN);
+      if (p == 0) {
+        if (lg == 1) {
+          O.start[r * 3 + 2] = -1;
+          O.end[r * 3 + 2] = -1;
+          O.density[r * 3 + 2] = 0.0;
+        }
+        O.flags[r] = (uint8_t)(NT_FLAG_DONE | NT_FLAG_ERR_ALIGN);
+      }
       continue;
     }
-    Lane c;
-    c.rc.n = n32;
-    c.rc.nblk = (int32_t)((n32 + 31u) >> 5);
-    c.rc.blk = reinterpret_cast<const uint2*>(B.planes) + B.blk_off[r];
-    c.rc.n_exc = 0;
-    c.rc.exc_pos = nullptr;
-    c.rc.exc_code = nullptr;
-    if (B.exc_off) {
-      const uint32_t e0 = B.exc_off[r], e1 = B.exc_off[r + 1];
-      c.rc.n_exc = (int32_t)(e1 - e0);
-      c.rc.exc_pos = B.exc_pos + e0;
-      c.rc.exc_code = B.exc_code + e0;
-    }
-    c.prog = prog;
-    c.n = (int)n32;
-    c.L = L;
-    c.nw = (int)split_window_count(c.n, L);
-    c.nmw = (c.nw + 63) >> 6;
-    const uint64_t woff = B.win_off[r];
-    const uint64_t* tmr = tmask + aux_base(woff, r, np);
-    const uint32_t* ckr = reinterpret_cast<const uint32_t*>(tmr + np * aux_nmw(c.nw));
-    int maxw = INT_MIN;
-    uint32_t flags = NT_FLAG_DONE;
-    for (int p = 0; p < np; ++p) {
-      c.cnt = O.win_counts + woff * np + (uint64_t)p * c.nw;
-      c.tm = tmr + p * c.nmw;
-      c.ck = ckr + p * aux_nck(c.nw);
-      c.k = p == 0 ? 0 : 1;
-      c.use_tvr = p == 2;
-      c.raw = p == 0 && prog->raw_p1;
-      int s, e;
-      double d;
-      uint32_t err = 0;
-      call_pass(c, s, e, d, err);
-      flags |= err;
-      if (s == -1) flags |= 1u << (NT_FLAG_NA_SHIFT + p);
-      maxw = max(maxw, e - s + 1);
+    if (p < 3) {  // passes >= np: -1 / -1 / 0
       O.start[r * 3 + p] = s;
       O.end[r * 3 + p] = e;
       O.density[r * 3 + p] = d;
     }
-    for (int p = np; p < 3; ++p) {
-      O.start[r * 3 + p] = -1;
-      O.end[r * 3 + p] = -1;
-      O.density[r * 3 + p] = 0.0;
+    if (p == 0) {
+      if (lg == 1) {
+        O.start[r * 3 + 2] = -1;
+        O.end[r * 3 + 2] = -1;
+        O.density[r * 3 + 2] = 0.0;
+      }
+      if (w >= 30) flags |= NT_FLAG_TELOMERIC;
+      O.flags[r] = (uint8_t)(flags | NT_FLAG_DONE);
     }
-    if (maxw >= 30) flags |= NT_FLAG_TELOMERIC;
-    O.flags[r] = (uint8_t)flags;
   }
 }
 

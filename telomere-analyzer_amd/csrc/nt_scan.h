@@ -400,6 +400,52 @@ __device__ __forceinline__ uint4 load_seg(const uint4* __restrict__ seg, int nse
   return make_uint4(ok ? x.x : 0u, ok ? x.y : 0u, ok ? x.z : 0u, ok ? x.w : 0u);
 }
 
+// NT_BUFLOAD: segment ring through buffer descriptors (range-checked loads);
+// NT_RING3: three ring slots, unrolled (1M x 50 kb: scan 3.76 -> 3.52 ms
+// with both).  0 selects the plain-load / rotating-ring forms (tuning).
+#ifndef NT_BUFLOAD
+#define NT_BUFLOAD 1
+#endif
+#ifndef NT_RING3
+#define NT_RING3 1
+#endif
+#if NT_BUFLOAD
+// The same through a buffer descriptor over the read's segments: the
+// hardware range check returns 0 for g outside [0, nseg) (a negative g is a
+// huge unsigned offset), so no address clamp and no zeroing VALU.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t seg_rsrc(const void* base, int nseg) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0,
+                                           __builtin_amdgcn_readfirstlane(nseg * 16), 0x00020000);
+}
+__device__ __forceinline__ uint4 load_segb(__amdgpu_buffer_rsrc_t r, int g) {
+  const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, g * 16, 0, 0);
+  return make_uint4(v[0], v[1], v[2], v[3]);
+}
+#endif
+
+// NT_DBG_CHECK (debugging aid, off): every HBM address the scan forms is
+// checked against the limits in a DbgRec the host passes as gscr (planes in
+// 16-byte segments, window counts, aux words); a violation is recorded (the
+// first one in full) and the access skipped.
+#ifndef NT_DBG_CHECK
+#define NT_DBG_CHECK 0
+#endif
+struct DbgRec {
+  unsigned long long lim[4];
+  unsigned long long nbad;
+  unsigned long long first[4];  // kind, index, read, limit
+};
+__device__ __forceinline__ bool dbg_ok(DbgRec* d, int kind, uint64_t idx, uint64_t r) {
+  if (!NT_DBG_CHECK || !d || idx < d->lim[kind]) return true;
+  if (atomicAdd(&d->nbad, 1ull) == 0ull) {
+    d->first[0] = (unsigned long long)kind;
+    d->first[1] = idx;
+    d->first[2] = r;
+    d->first[3] = d->lim[kind];
+  }
+  return false;
+}
+
 template <int kNHits>
 struct ScanState {
   uint32_t ov0, ov1, ov2;  // overflow carried into the next chunk's lane 0
@@ -407,8 +453,9 @@ struct ScanState {
   uint32_t acc[kNHits];    // register hit counters (per lane)
 };
 
-// One chunk (lane's segment g = g0 + lane).
-template <class S, bool kValid>
+// One chunk (lane's segment g = g0 + lane).  kHits: count the matchPattern
+// hits (only when the caller asked for them: 6 VALU per chunk otherwise).
+template <class S, bool kValid, bool kHits>
 __device__ __forceinline__ void scan_chunk(const NtProgram* __restrict__ prog, const ReadCtx& rc,
                                            int g0, int lane, int np, int nw, int L, DivL div,
                                            uint4 cur, uint2* cum01, uint32_t* cum2,
@@ -436,14 +483,16 @@ __device__ __forceinline__ void scan_chunk(const NtProgram* __restrict__ prog, c
       patch_exceptions(rc, base + 32, 0, n - 1, *d.P, false, a0B, a1B);
     }
     // matchPattern hit counts (lane 63's are dropped in the final sum)
-    const uint32_t h0 = __builtin_popcount(a0A) + __builtin_popcount(a0B);
-    const uint32_t h1 = __builtin_popcount(a1A) + __builtin_popcount(a1B);
-    if constexpr (S::kRegHits) {
-      st.acc[p] += h0;
-      st.acc[S::kNPat + p] += h1;
-    } else {
-      hitacc[p * kWave + lane] += h0;
-      hitacc[(n_pat + p) * kWave + lane] += h1;
+    if constexpr (kHits) {
+      const uint32_t h0 = __builtin_popcount(a0A) + __builtin_popcount(a0B);
+      const uint32_t h1 = __builtin_popcount(a1A) + __builtin_popcount(a1B);
+      if constexpr (S::kRegHits) {
+        st.acc[p] += h0;
+        st.acc[S::kNPat + p] += h1;
+      } else {
+        hitacc[p * kWave + lane] += h0;
+        hitacc[(n_pat + p) * kWave + lane] += h1;
+      }
     }
     seg_spread<decltype(d)::kM>(a0A, a0B, d.m(), cA0, cB0, ov0);
     seg_spread<decltype(d)::kM>(a1A, a1B, d.m(), cA1, cB1, ov1);
@@ -461,9 +510,11 @@ __device__ __forceinline__ void scan_chunk(const NtProgram* __restrict__ prog, c
         patch_exceptions(rc, base, 0, n - 1, *d.P, false, a0A, a1A);
         patch_exceptions(rc, base + 32, 0, n - 1, *d.P, false, a0B, a1B);
       }
-      const uint32_t h0 = __builtin_popcount(a0A) + __builtin_popcount(a0B);
-      if constexpr (S::kRegHits) st.acc[2 * S::kNPat + t] += h0;
-      else hitacc[(2 * n_pat + t) * kWave + lane] += h0;
+      if constexpr (kHits) {
+        const uint32_t h0 = __builtin_popcount(a0A) + __builtin_popcount(a0B);
+        if constexpr (S::kRegHits) st.acc[2 * S::kNPat + t] += h0;
+        else hitacc[(2 * n_pat + t) * kWave + lane] += h0;
+      }
       seg_spread<decltype(d)::kM>(a0A, a0B, d.m(), cA2, cB2, ov2);
     });
   }
@@ -537,13 +588,21 @@ struct ReadMeta {
   uint32_t e0, e1;      // exception list range (0, 0 without exceptions)
 };
 
+// Wave-uniform copy of a 64-bit value.  v_readfirstlane_b32 yields an int:
+// each half is kept unsigned before widening (a sign-extended low half once
+// turned every block offset >= 2^31 -- reads past ~1.37M x 50 kb -- into a
+// wild address).
+__device__ __forceinline__ uint64_t uniform_u64(uint64_t x) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(x >> 32));
+  return ((uint64_t)hi << 32) | (uint64_t)lo;
+}
+
 // The per-read metadata, all loads independent (one memory round trip).
 __device__ __forceinline__ ReadMeta load_meta(const NtBatch& B, uint64_t r) {
   ReadMeta m;
   m.len = B.len[r];
-  const uint64_t b = B.blk_off[r];
-  m.boff = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) << 32) |
-           __builtin_amdgcn_readfirstlane((uint32_t)b);  // uniform: SGPR base
+  m.boff = uniform_u64(B.blk_off[r]);  // uniform: SGPR base
   m.woff = B.win_off[r];
   m.e0 = m.e1 = 0u;
   if (B.exc_off) {
@@ -553,12 +612,13 @@ __device__ __forceinline__ ReadMeta load_meta(const NtBatch& B, uint64_t r) {
   return m;
 }
 
-template <class S, bool kLds>
+template <class S, bool kLds, bool kHits = true>
 __device__ __forceinline__ void scan_reads(const NtProgram* __restrict__ prog,
                                            const uint32_t* __restrict__ thr, const NtBatch& B,
                                            const NtOut& O, uint64_t* __restrict__ tmask,
                                            unsigned long long* __restrict__ queue,
-                                           uint32_t len_lo, uint32_t len_hi, uint32_t claim, uint32_t nstatic, uint32_t* wmem) {
+                                           uint32_t len_lo, uint32_t len_hi, uint32_t claim, uint32_t nstatic, uint32_t* wmem,
+                                           DbgRec* dbg = nullptr) {
   const int lane = threadIdx.x & (kWave - 1);
   const int np = S::kNPass ? S::kNPass : prog->n_pass;
   const int nh = S::kRegHits ? S::kNHits : prog->n_hits, L = prog->L;
@@ -577,7 +637,7 @@ __device__ __forceinline__ void scan_reads(const NtProgram* __restrict__ prog,
   // at every fraction tried (1M x 50 kb: 5.1 ms at 3/4 static, 3.8 ms at 0).
   const uint64_t nR = B.n_reads;
   const uint64_t W = (uint64_t)gridDim.x * kNWaves;
-  const uint64_t w = (uint64_t)blockIdx.x * kNWaves + __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const uint64_t w = (uint64_t)blockIdx.x * kNWaves + (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const uint64_t st_n = (uint64_t)nstatic * W < nR ? nstatic : nR / W;
   const uint64_t D0 = st_n * W, Dn = nR - D0;
   const uint64_t kc = claim ? claim : 1u;
@@ -588,8 +648,7 @@ __device__ __forceinline__ void scan_reads(const NtProgram* __restrict__ prog,
       const uint64_t q0 = D0 + Dn * qi / NT_QUEUES, q1 = D0 + Dn * (qi + 1) / NT_QUEUES;
       unsigned long long v = 0;
       if (lane == 0) v = atomicAdd(queue + qi * NT_QUEUE_STRIDE, (unsigned long long)kc);
-      const uint64_t o = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
-                         __builtin_amdgcn_readfirstlane((uint32_t)v);
+      const uint64_t o = uniform_u64(v);
       if (o < q1 - q0) {
         lo = q0 + o;
         hi = q1 - q0 - o > kc ? lo + kc : q1;
@@ -611,8 +670,11 @@ __device__ __forceinline__ void scan_reads(const NtProgram* __restrict__ prog,
   claim_next(bLo, bHi);
   uint64_t r = aLo;
   ReadMeta m = r < nR ? load_meta(B, r) : ReadMeta{};
-  uint4 nx1 = make_uint4(0u, 0u, 0u, 0u), nx2 = nx1;
-  bool ring_ok = false;  // nx1/nx2 hold chunks 0 and 1 of read r
+  uint4 nx0 = make_uint4(0u, 0u, 0u, 0u), nx1 = nx0, nx2 = nx0;
+  bool ring_ok = false;  // the ring holds chunks 0 and 1 of read r (after the realignment)
+#if NT_RING3
+  int ring_ph = 2;  // the slot phase the last read ended in
+#endif
   while (r < nR) {
     const bool cross = r + aStep >= aHi;
     const uint64_t rn = cross ? bLo : r + aStep;  // next read (>= nR: none)
@@ -629,7 +691,11 @@ __device__ __forceinline__ void scan_reads(const NtProgram* __restrict__ prog,
     rc.n = n32;
     rc.nblk = (int32_t)((n32 + 31u) >> 5);
     rc.blk = reinterpret_cast<const uint2*>(B.planes) + boff;
+#ifdef NT_ISA_NO_EXC  // ISA reading aid only: exception fix-ups compiled out
+    rc.n_exc = 0;
+#else
     rc.n_exc = (int32_t)(m.e1 - m.e0);
+#endif
     rc.exc_pos = B.exc_off ? B.exc_pos + m.e0 : nullptr;
     rc.exc_code = B.exc_off ? B.exc_code + m.e0 : nullptr;
     const int n = (int)n32;
@@ -637,7 +703,7 @@ __device__ __forceinline__ void scan_reads(const NtProgram* __restrict__ prog,
     const int nw = (int)split_window_count(n, L);
     uint2* cum01 = reinterpret_cast<uint2*>(wmem + (S::kRegHits ? 0 : nh * kWave));
     uint32_t* cum2 = reinterpret_cast<uint32_t*>(cum01 + (nw + 1));
-    if (!S::kRegHits)
+    if (kHits && !S::kRegHits)
       for (int c = 0; c < nh; ++c) hitacc[c * kWave + lane] = 0u;  // per-lane slots
 
     // ------------------------------------------------------------ scan
@@ -655,24 +721,65 @@ __device__ __forceinline__ void scan_reads(const NtProgram* __restrict__ prog,
       const int K = (nseg + kOwned) / kOwned;  // chunks: g0 = -1, 62, ... < nseg
       const uint4* segn = reinterpret_cast<const uint4*>(B.planes) + (mn.boff >> 1);
       const int nsegn = ((int)mn.len + 63) >> 6;
-      const bool pf = !skip_n && K >= 2 && (nsegn + kOwned) / kOwned >= 2;
-      if (!ring_ok) {
-        nx1 = load_seg(seg, nseg, lane - 1);
-        nx2 = load_seg(seg, nseg, kOwned - 1 + lane);
+      bool pf = !skip_n && K >= 2 && (nsegn + kOwned) / kOwned >= 2;
+      if (NT_DBG_CHECK) {
+        if (!dbg_ok(dbg, 0, (boff >> 1) + (uint64_t)(nseg > 0 ? nseg - 1 : 0), r)) break;
+        if (pf && !dbg_ok(dbg, 0, (mn.boff >> 1) + (uint64_t)(nsegn - 1), rn)) pf = false;
       }
-      int c = 0;
-      for (int g0 = -1; g0 < nseg; g0 += kOwned, ++c) {
+#if NT_BUFLOAD
+      const __amdgpu_buffer_rsrc_t rs = seg_rsrc(seg, nseg);
+      const __amdgpu_buffer_rsrc_t rsn = seg_rsrc(segn, pf ? nsegn : 0);
+      auto ld = [&](bool own, int g) { return load_segb(own ? rs : rsn, g); };
+#else
+      auto ld = [&](bool own, int g) { return load_seg(own ? seg : segn, own ? nseg : nsegn, g); };
+#endif
+      // chunk c of the stream: read the segments of cur, load position c + 2
+      // (this read's chunk, or the next read's chunk c + 2 - K) into dst
+      auto step = [&](int c, const uint4& cur, uint4& dst) {
+        const int g0 = c * kOwned - 1;
+        const int t = c + 2;
+        const bool own_t = t < K || !pf;
+        dst = ld(own_t, (own_t ? g0 + 2 * kOwned : (t - K) * kOwned - 1) + lane);
+        if (g0 >= 0 && 64 * (g0 + kWave) <= n)
+          scan_chunk<S, false, kHits>(prog, rc, g0, lane, np, nw, L, div, cur, cum01, cum2, hitacc, st);
+        else
+          scan_chunk<S, true, kHits>(prog, rc, g0, lane, np, nw, L, div, cur, cum01, cum2, hitacc, st);
+      };
+#if NT_RING3
+      // three ring slots, unrolled by three: no register rotation per chunk
+      // (moving an in-flight load's registers would wait for it); the slots
+      // are realigned once per read, before the next read's first chunk
+      if (ring_ph == 0) {
+        nx0 = nx1;
+        nx1 = nx2;
+      } else if (ring_ph == 1) {
+        const uint4 t = nx0;
+        nx0 = nx2;
+        nx1 = t;
+      }
+      if (!ring_ok) {
+        nx0 = ld(true, lane - 1);
+        nx1 = ld(true, kOwned - 1 + lane);
+      }
+      for (int c = 0;;) {
+        step(c, nx0, nx2);
+        if (++c >= K) { ring_ph = 0; break; }
+        step(c, nx1, nx0);
+        if (++c >= K) { ring_ph = 1; break; }
+        step(c, nx2, nx1);
+        if (++c >= K) { ring_ph = 2; break; }
+      }
+#else
+      if (!ring_ok) {
+        nx1 = ld(true, lane - 1);
+        nx2 = ld(true, kOwned - 1 + lane);
+      }
+      for (int c = 0; c < K; ++c) {
         const uint4 cur = nx1;
         nx1 = nx2;
-        const int t = c + 2;  // stream position loaded now
-        const bool own_t = t < K || !pf;
-        nx2 = load_seg(own_t ? seg : segn, own_t ? nseg : nsegn,
-                       (own_t ? g0 + 2 * kOwned : (t - K) * kOwned - 1) + lane);
-        if (g0 >= 0 && 64 * (g0 + kWave) <= n)
-          scan_chunk<S, false>(prog, rc, g0, lane, np, nw, L, div, cur, cum01, cum2, hitacc, st);
-        else
-          scan_chunk<S, true>(prog, rc, g0, lane, np, nw, L, div, cur, cum01, cum2, hitacc, st);
+        step(c, cur, nx2);
       }
+#endif
       ring_ok = pf;
     }
     if (lane == 0 && nw > 0) {
@@ -700,7 +807,8 @@ __device__ __forceinline__ void scan_reads(const NtProgram* __restrict__ prog,
     for (int p = 0; p < np; ++p) {
       for (int j = lane; j < nck; j += kWave) {
         const int i = 16 * j;  // i <= nw
-        cko[p * nck + j] = nw == 0 ? 0u : (p == 2 ? cum2[i] : (p == 1 ? cum01[i].y : cum01[i].x));
+        if (dbg_ok(dbg, 2, aux_base(m.woff, r, np) + (uint64_t)(np * nmw) + (uint64_t)(p * nck + j) / 2, r))
+          cko[p * nck + j] = nw == 0 ? 0u : (p == 2 ? cum2[i] : (p == 1 ? cum01[i].y : cum01[i].x));
       }
       for (int ch = 0; ch < nmw; ++ch) {
         const int i = ch * 64 + lane;
@@ -709,14 +817,14 @@ __device__ __forceinline__ void scan_reads(const NtProgram* __restrict__ prog,
           if (p == 2) cnt = cum2[i + 1] - cum2[i];
           else if (p == 1) cnt = cum01[i + 1].y - cum01[i].y;
           else cnt = cum01[i + 1].x - cum01[i].x;
-          wout[p * nw + i] = (uint16_t)cnt;
+          if (dbg_ok(dbg, 1, m.woff * np + (uint64_t)(p * nw + i), r)) wout[p * nw + i] = (uint16_t)cnt;
         }
         const bool t = i < nw && cnt >= (i == nw - 1 ? thr_last : thr_full);
         const uint64_t bal = __ballot(t);
-        if (lane == 0) tmo[p * nmw + ch] = bal;
+        if (lane == 0 && dbg_ok(dbg, 2, aux_base(m.woff, r, np) + (uint64_t)(p * nmw + ch), r)) tmo[p * nmw + ch] = bal;
       }
     }
-    if (O.hits) {
+    if (kHits && O.hits) {
       if constexpr (S::kRegHits) {
 #pragma unroll
         for (int c = 0; c < S::kNHits; ++c) {

@@ -260,6 +260,32 @@ def test_odd_block_offset_is_reported():
 
 
 @pytest.mark.parametrize("jit", [True, False], ids=["jit", "aot"])
+def test_offsets_beyond_32_bits(jit):
+    # Batches of 10M x 50 kb reads have block offsets >= 2^31 and window
+    # offsets >= 2^32 (a sign-extended 32-bit block offset once faulted there).
+    # Reproduced without allocating them: the planes / window-count base
+    # pointers are shifted down by exactly the offsets added to blk_off / win_off.
+    import torch
+    from nanotel_amd import synth_params
+    n, read_len = 64, 50000
+    nt = _nt(jit=jit, patterns="TTAGGG")
+    t = _device_batch(nt, synth_params(read_len=read_len, first_read=77), n, read_len)
+    _run_device(nt, t, n, read_len)
+    keys = ("start", "end", "dens", "flags", "wc")
+    ref = {k: t[k].clone() for k in keys}
+    for k in keys:
+        t[k].zero_()
+    boff, woff = 1 << 31, 1 << 32  # blocks of 8 bytes, windows
+    blk, win = t["blk_off"] + boff, t["win_off"] + woff
+    nt.scan_call_device(t["planes"].data_ptr() - boff * 8, blk.data_ptr(), t["lens"].data_ptr(), win.data_ptr(),
+                        n, woff + n * t["nw"], read_len, t["start"].data_ptr(), t["end"].data_ptr(),
+                        t["dens"].data_ptr(), t["flags"].data_ptr(), t["wc"].data_ptr() - woff * nt.n_pass * 2)
+    nt.synchronize()
+    for k in keys:
+        assert torch.equal(t[k], ref[k]), k
+
+
+@pytest.mark.parametrize("jit", [True, False], ids=["jit", "aot"])
 def test_subbatched_overlap_matches_serial(jit):
     # NT_SUBBATCH > 1: the calling kernel of sub-batch k runs on a second
     # stream beside the scan of sub-batch k+1; outputs must not change

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Offline ISA of the hiprtc-specialised scan for a pattern set (for reading
-# the inner loop): [ISA_DEFS=-D..] tools/jit_isa.sh OUTDIR "nt::CtPat<6,8,8,1,4,4,4>" ["tvr list"]
+# the inner loop): [ISA_HITS=true] [ISA_DEFS=-D..] tools/jit_isa.sh OUTDIR "nt::CtPat<6,8,8,1,4,4,4>" ["tvr list"]
 set -eu
 out=$1; pats=$2; tvrs=${3:-}
 here=$(cd "$(dirname "$0")/.." && pwd)
@@ -20,7 +20,7 @@ nt_scan_jit_lds(const NtProgram* __restrict__ prog, const uint32_t* __restrict__
                 uint32_t len_lo, uint32_t len_hi, uint32_t claim, uint32_t nstatic, uint32_t wave_words,
                 uint32_t* __restrict__ gscr) {
   extern __shared__ uint32_t smem[];
-  nt::scan_reads<JitSet, true>(prog, thr, B, O, tmask, queue, len_lo, len_hi, claim, nstatic,
+  nt::scan_reads<JitSet, true, ${ISA_HITS:-false}>(prog, thr, B, O, tmask, queue, len_lo, len_hi, claim, nstatic,
                                smem + (threadIdx.x >> 6) * wave_words);
 }
 EOT
