@@ -182,8 +182,8 @@ def main():
     total_bases = n * L * world * args.steps
     value = total_bases / wall / 1e9
     scan_s = scan_ms / n_calls / 1e3
-    nh = nt.n_hits
-    scan_bytes = n * scan_bytes_per_read(L, npass, nw, nh)
+    # no hit counters requested: the scan instance without them runs (no hit bytes)
+    scan_bytes = n * scan_bytes_per_read(L, npass, nw, 0)
     achieved = scan_bytes / scan_s / 1e9
     traffic = None
     if os.path.exists(args.traffic_json):
@@ -214,7 +214,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic,
-                         "kernel": ("nt_scan_jit_lds (scan specialised for the patterns, hiprtc)" if nt.jit
+                         "kernel": ("nt_scan_jit_nh_lds (scan specialised for the patterns, hiprtc)" if nt.jit
                                     else "nt::nt_scan_kernel (ahead-of-time scan)"),
                          "kernel_avg_ms": round(scan_s * 1e3, 4),
                          "algorithmic_bytes_per_launch": scan_bytes,

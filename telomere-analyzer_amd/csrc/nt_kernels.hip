@@ -666,10 +666,11 @@ __device__ __forceinline__ void call_pass(Lane& c, int& out_s, int& out_e, doubl
 // lane of a one-lane-per-read walk -- and combine flags / the max width over
 // the passes with lane shuffles (G divides 64 and the grid stride is a
 // multiple of 64, so a read's lanes share a wave).  NT_CALL_WAVES_PER_EU
-// trades VGPRs for occupancy: with the boundary neighbourhoods (register
-// arrays) 2 waves/SIMD and no spills measured best.
+// trades VGPRs for occupancy: the kernel waits on memory, so 3 waves/SIMD
+// (168 VGPRs, a few spills) beat 2 (196, none) and 4 (128, 109 spilled):
+// 1M x 50 kb call 1.03 / 0.90 / 0.98 ms at 2 / 3 / 4.
 #ifndef NT_CALL_WAVES_PER_EU
-#define NT_CALL_WAVES_PER_EU 2
+#define NT_CALL_WAVES_PER_EU 3
 #endif
 #define NT_CALL_ATTR __attribute__((amdgpu_waves_per_eu(NT_CALL_WAVES_PER_EU)))
 __global__ void __launch_bounds__(256) NT_CALL_ATTR

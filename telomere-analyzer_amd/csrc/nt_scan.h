@@ -804,24 +804,42 @@ __device__ __forceinline__ void scan_reads(const NtProgram* __restrict__ prog,
     const int nmw = aux_nmw(nw), nck = aux_nck(nw);
     uint64_t* tmo = tmask + aux_base(m.woff, r, np);
     uint32_t* cko = reinterpret_cast<uint32_t*>(tmo + np * nmw);
-    for (int p = 0; p < np; ++p) {
-      for (int j = lane; j < nck; j += kWave) {
-        const int i = 16 * j;  // i <= nw
-        if (dbg_ok(dbg, 2, aux_base(m.woff, r, np) + (uint64_t)(np * nmw) + (uint64_t)(p * nck + j) / 2, r))
-          cko[p * nck + j] = nw == 0 ? 0u : (p == 2 ? cum2[i] : (p == 1 ? cum01[i].y : cum01[i].x));
+    const uint64_t ab = aux_base(m.woff, r, np);
+    // passes 0 and 1 together from the packed running counts (one LDS read
+    // per window boundary), pass 2 after them
+    for (int j = lane; j < nck; j += kWave) {
+      const int i = 16 * j;  // i <= nw
+      const uint2 c01 = nw == 0 ? make_uint2(0u, 0u) : cum01[i];
+      if (dbg_ok(dbg, 2, ab + (uint64_t)(np * nmw) + (uint64_t)(nck + j) / 2, r)) {
+        cko[j] = c01.x;
+        cko[nck + j] = c01.y;
       }
-      for (int ch = 0; ch < nmw; ++ch) {
-        const int i = ch * 64 + lane;
-        uint32_t cnt = 0u;
-        if (i < nw) {
-          if (p == 2) cnt = cum2[i + 1] - cum2[i];
-          else if (p == 1) cnt = cum01[i + 1].y - cum01[i].y;
-          else cnt = cum01[i + 1].x - cum01[i].x;
-          if (dbg_ok(dbg, 1, m.woff * np + (uint64_t)(p * nw + i), r)) wout[p * nw + i] = (uint16_t)cnt;
+      if (np == 3 && dbg_ok(dbg, 2, ab + (uint64_t)(np * nmw) + (uint64_t)(2 * nck + j) / 2, r))
+        cko[2 * nck + j] = nw == 0 ? 0u : cum2[i];
+    }
+    for (int ch = 0; ch < nmw; ++ch) {
+      const int i = ch * 64 + lane;
+      const uint32_t tw = i == nw - 1 ? thr_last : thr_full;
+      uint32_t c0 = 0u, c1 = 0u, c2 = 0u;
+      if (i < nw) {
+        const uint2 a0 = cum01[i], a1 = cum01[i + 1];
+        c0 = a1.x - a0.x;
+        c1 = a1.y - a0.y;
+        if (dbg_ok(dbg, 1, m.woff * np + (uint64_t)(nw + i), r)) {
+          wout[i] = (uint16_t)c0;
+          wout[nw + i] = (uint16_t)c1;
         }
-        const bool t = i < nw && cnt >= (i == nw - 1 ? thr_last : thr_full);
-        const uint64_t bal = __ballot(t);
-        if (lane == 0 && dbg_ok(dbg, 2, aux_base(m.woff, r, np) + (uint64_t)(p * nmw + ch), r)) tmo[p * nmw + ch] = bal;
+        if (np == 3) {
+          c2 = cum2[i + 1] - cum2[i];
+          if (dbg_ok(dbg, 1, m.woff * np + (uint64_t)(2 * nw + i), r)) wout[2 * nw + i] = (uint16_t)c2;
+        }
+      }
+      const uint64_t b0 = __ballot(i < nw && c0 >= tw), b1 = __ballot(i < nw && c1 >= tw);
+      const uint64_t b2 = np == 3 ? __ballot(i < nw && c2 >= tw) : 0ull;
+      if (lane == 0 && dbg_ok(dbg, 2, ab + (uint64_t)((np - 1) * nmw + ch), r)) {
+        tmo[ch] = b0;
+        tmo[nmw + ch] = b1;
+        if (np == 3) tmo[2 * nmw + ch] = b2;
       }
     }
     if (kHits && O.hits) {
