@@ -182,7 +182,9 @@ int64_t nt_assign_serials(const uint8_t* is_telo, uint64_t n, double* serial_sta
 /* readDNAStringSet(open_input_files(path), nrec, format) (NanoTel.R:2171-2216):
  * path = a file or a directory (files listed recursively, sorted, read as one
  * record stream); format 0 = fasta, 1 = fastq; gzip transparent.  A chunk's
- * names/sequences stay valid until the next nt_reader_next / close.
+ * names/sequences stay valid through the next nt_reader_next call (two
+ * buffers in turn: chunk k+1 may be read while chunk k is scanned) and until
+ * the one after it, or close.
  * Returns the number of records (0 at the end) or < 0 (nt_reader_error). */
 typedef struct nt_reader nt_reader;
 int nt_reader_open(const char* path, int format, nt_reader** out);

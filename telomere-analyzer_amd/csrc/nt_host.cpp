@@ -2,6 +2,7 @@
 // host packing (+ reverse complement, A14), launches of the gfx950 kernels,
 // serial assignment (A15) and the synthetic-read generator.
 #include <hip/hip_runtime.h>
+#include <immintrin.h>
 
 #include <algorithm>
 #include <array>
@@ -70,22 +71,23 @@ struct DevBuf {
 
 // Biostrings DNA_ALPHABET codes (A=1 C=2 G=4 T=8, IUPAC = OR, '-'=16 '+'=32 '.'=64);
 // lower case letters are upper-cased by DNAString().
-uint8_t letter_code(unsigned char c) {
-  static uint8_t tab[256];
-  static bool init = false;
-  if (!init) {
+struct LetterTab {
+  uint8_t t[256] = {};
+  LetterTab() {
     const char* up = "ACGTMRWSYKVHDBN";
     const uint8_t codes[] = {1, 2, 4, 8, 3, 5, 9, 6, 10, 12, 7, 11, 13, 14, 15};
     for (int i = 0; i < 15; ++i) {
-      tab[(unsigned char)up[i]] = codes[i];
-      tab[(unsigned char)(up[i] - 'A' + 'a')] = codes[i];
+      t[(unsigned char)up[i]] = codes[i];
+      t[(unsigned char)(up[i] - 'A' + 'a')] = codes[i];
     }
-    tab[(unsigned char)'-'] = 16;
-    tab[(unsigned char)'+'] = 32;
-    tab[(unsigned char)'.'] = 64;
-    init = true;
+    t[(unsigned char)'-'] = 16;
+    t[(unsigned char)'+'] = 32;
+    t[(unsigned char)'.'] = 64;
   }
-  return tab[c];
+};
+uint8_t letter_code(unsigned char c) {
+  static const LetterTab tab;  // thread-safe one-time init (the packer runs on many threads)
+  return tab.t[c];
 }
 
 // 2-bit code for A/C/G/T (either case), else -1.
@@ -101,6 +103,56 @@ inline int base2(unsigned char c) {
 
 inline uint8_t complement_code(uint8_t x) {
   return (uint8_t)((x & 0xF0) | ((x & 1) << 3) | ((x & 8) >> 3) | ((x & 2) << 1) | ((x & 4) >> 1));
+}
+
+// 32 bases at a time: the 2-bit code of A/C/G/T (either case) is
+// lo = bit1 ^ bit2, hi = bit2 of the ASCII byte (A 0x41 -> 00, C 0x43 -> 01,
+// G 0x47 -> 10, T 0x54 -> 11).  pack32 returns false when any of the 32
+// bytes is not A/C/G/T; the caller then takes the per-base path (exceptions,
+// bad letters).  AVX2 when the host has it (runtime dispatch), else scalar.
+__attribute__((target("avx2"))) static bool pack32_avx2(const unsigned char* p, uint32_t& lo,
+                                                        uint32_t& hi) {
+  const __m256i v = _mm256_loadu_si256((const __m256i*)p);
+  const __m256i l = _mm256_or_si256(v, _mm256_set1_epi8(0x20));
+  const __m256i ok = _mm256_or_si256(
+      _mm256_or_si256(_mm256_cmpeq_epi8(l, _mm256_set1_epi8('a')), _mm256_cmpeq_epi8(l, _mm256_set1_epi8('c'))),
+      _mm256_or_si256(_mm256_cmpeq_epi8(l, _mm256_set1_epi8('g')), _mm256_cmpeq_epi8(l, _mm256_set1_epi8('t'))));
+  if ((uint32_t)_mm256_movemask_epi8(ok) != 0xFFFFFFFFu) return false;
+  const uint32_t b1 = (uint32_t)_mm256_movemask_epi8(_mm256_slli_epi16(v, 6));
+  const uint32_t b2 = (uint32_t)_mm256_movemask_epi8(_mm256_slli_epi16(v, 5));
+  lo = b1 ^ b2;
+  hi = b2;
+  return true;
+}
+
+static bool pack32_scalar(const unsigned char* p, uint32_t& lo, uint32_t& hi) {
+  uint32_t l = 0, h = 0;
+  for (int i = 0; i < 32; ++i) {
+    const int c = base2(p[i]);
+    if (c < 0) return false;
+    l |= (uint32_t)(c & 1) << i;
+    h |= (uint32_t)(c >> 1) << i;
+  }
+  lo = l;
+  hi = h;
+  return true;
+}
+
+static const bool g_avx2 = __builtin_cpu_supports("avx2");
+
+inline bool pack32(const unsigned char* p, uint32_t& lo, uint32_t& hi) {
+  return g_avx2 ? pack32_avx2(p, lo, hi) : pack32_scalar(p, lo, hi);
+}
+
+// number of non-A/C/G/T bytes in s[0, n)
+static uint64_t count_non_acgt(const unsigned char* s, uint64_t n) {
+  uint64_t e = 0, i = 0;
+  uint32_t lo, hi;
+  for (; i + 32 <= n; i += 32)
+    if (!pack32(s + i, lo, hi))
+      for (int k = 0; k < 32; ++k) e += base2(s[i + k]) < 0;
+  for (; i < n; ++i) e += base2(s[i]) < 0;
+  return e;
 }
 
 int64_t window_count(int64_t n, int L) {
@@ -401,9 +453,17 @@ int nt_pack_count(const char* const* seqs, const uint64_t* lens, uint64_t n_read
     const unsigned char* s = (const unsigned char*)seqs[r];
     uint64_t e = 0;
     int b = lens[r] == 0 ? 2 : 0;
-    for (uint64_t i = 0; i < lens[r] && !b; ++i) {
-      if (base2(s[i]) >= 0) continue;
-      if (letter_code(s[i])) ++e; else b = 1;
+    uint32_t lo, hi;
+    for (uint64_t i = 0; i < lens[r] && !b;) {
+      if (i + 32 <= lens[r] && pack32(s + i, lo, hi)) {
+        i += 32;
+        continue;
+      }
+      const uint64_t end = std::min<uint64_t>(lens[r], i + 32);
+      for (; i < end && !b; ++i) {
+        if (base2(s[i]) >= 0) continue;
+        if (letter_code(s[i])) ++e; else b = 1;
+      }
     }
     exc[r] = e;
     bad[r] = b;
@@ -445,9 +505,7 @@ int nt_pack_reads(const char* const* seqs, const uint64_t* lens, uint64_t n_read
     std::vector<uint64_t> cnt(n_reads, 0);
     parallel_for(n_reads, [&](uint64_t r) {
       const unsigned char* s = (const unsigned char*)seqs[r];
-      uint64_t e = 0;
-      for (uint64_t i = 0; i < lens[r]; ++i) e += base2(s[i]) < 0;
-      cnt[r] = e;
+      cnt[r] = count_non_acgt(s, lens[r]);
     });
     for (uint64_t r = 0; r < n_reads; ++r) eoff[r + 1] = eoff[r] + cnt[r];
     for (uint64_t r = 0; r <= n_reads; ++r) {
@@ -463,6 +521,19 @@ int nt_pack_reads(const char* const* seqs, const uint64_t* lens, uint64_t n_read
     uint64_t e = exc_off ? eoff[r] : 0;
     for (uint64_t blk = 0; blk * 32 < n; ++blk) {
       uint32_t lo = 0, hi = 0;
+      if (blk * 32 + 32 <= n) {  // whole block of plain bases: 32 at a time
+        // reverse complement: base i of the block is the complement of q[31 - i]
+        const unsigned char* q = rc ? s + (n - 32 - blk * 32) : s + blk * 32;
+        if (pack32(q, lo, hi)) {
+          if (rc) {
+            lo = ~__builtin_bitreverse32(lo);
+            hi = ~__builtin_bitreverse32(hi);
+          }
+          out[2 * blk] = lo;
+          out[2 * blk + 1] = hi;
+          continue;
+        }
+      }
       for (uint32_t i = 0; i < 32 && blk * 32 + i < n; ++i) {
         const uint64_t pos = blk * 32 + i;
         // reverseComplement: position pos of the RC read is the complement of n-1-pos

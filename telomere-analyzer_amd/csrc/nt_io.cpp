@@ -36,11 +36,19 @@ struct nt_reader {
   std::string err;
   std::string pending_header;  // FASTA: header already read for the next record
   bool has_pending = false;
-  // current chunk storage
-  std::string names_blob, seqs_blob;
-  std::vector<uint64_t> name_off, seq_off;
-  std::vector<const char*> name_ptr, seq_ptr;
-  std::vector<uint64_t> name_len, seq_len;
+  // chunk storage, two slots used in turn: a chunk stays valid through the
+  // next nt_reader_next call (so the caller can read chunk k+1 on another
+  // thread while it still scans chunk k)
+  struct Store {
+    std::string names_blob, seqs_blob;
+    std::vector<uint64_t> name_off, seq_off;
+    std::vector<const char*> name_ptr, seq_ptr;
+    std::vector<uint64_t> name_len, seq_len;
+  } store[2];
+  int cur = 0;
+  Store& c() { return store[cur]; }
+  bool seq_direct = false;  // FASTQ: next_record wrote the sequence into seqs_blob at seq_mark
+  size_t seq_mark = 0;
   uint64_t records_total = 0;
 };
 
@@ -78,41 +86,62 @@ bool open_next(nt_reader* r) {
   return true;
 }
 
-// One line of the current file (without '\n' / '\r'); false at end of file.
-bool get_line(nt_reader* r, std::string& line) {
-  line.clear();
+// One line of the current file (without '\n' / '\r') appended to `out`
+// (nullptr: skipped, e.g. FASTQ qualities); false at end of file.  Returns the
+// line length through `len`.
+bool take_line(nt_reader* r, std::string* out, size_t* len = nullptr) {
   if (!r->gz) return false;
+  const size_t base = out ? out->size() : 0;
+  size_t n_line = 0;
+  bool any = false;
   for (;;) {
     if (r->pos == r->end) {
-      if (r->eof_file) return !line.empty();
+      if (r->eof_file) break;
       const int n = gzread(r->gz, r->buf.data(), (unsigned)r->buf.size());
       if (n <= 0) {
         r->eof_file = true;
-        return !line.empty();
+        break;
       }
       r->pos = 0;
       r->end = (size_t)n;
     }
+    any = true;
     const char* b = r->buf.data() + r->pos;
     const char* nl = (const char*)memchr(b, '\n', r->end - r->pos);
+    const size_t k = nl ? (size_t)(nl - b) : r->end - r->pos;
+    if (out) out->append(b, k);
+    n_line += k;
+    r->pos += k;
     if (nl) {
-      line.append(b, nl - b);
-      r->pos += (nl - b) + 1;
-      if (!line.empty() && line.back() == '\r') line.pop_back();
+      ++r->pos;
+      if (out && out->size() > base && out->back() == '\r') out->pop_back(), --n_line;
+      else if (!out && k && b[k - 1] == '\r') --n_line;
+      if (len) *len = n_line;
       return true;
     }
-    line.append(b, r->end - r->pos);
-    r->pos = r->end;
   }
+  if (len) *len = n_line;
+  return any && n_line > 0;
+}
+
+bool get_line(nt_reader* r, std::string& line) {
+  line.clear();
+  return take_line(r, &line);
 }
 
 void add_record(nt_reader* r, const std::string& name, const std::string& seq) {
-  r->name_off.push_back(r->names_blob.size());
-  r->name_len.push_back(name.size());
-  r->names_blob += name;
-  r->seq_off.push_back(r->seqs_blob.size());
-  r->seq_len.push_back(seq.size());
-  r->seqs_blob += seq;
+  r->c().name_off.push_back(r->c().names_blob.size());
+  r->c().name_len.push_back(name.size());
+  r->c().names_blob += name;
+  if (r->seq_direct) {  // FASTQ: already in the blob from seq_mark on
+    r->c().seq_len.push_back(r->c().seqs_blob.size() - r->seq_mark);
+  } else {
+    r->c().seq_off.push_back(r->c().seqs_blob.size());
+    r->c().seq_len.push_back(seq.size());
+    r->c().seqs_blob += seq;
+    return;
+  }
+  r->c().seq_off.push_back(r->seq_mark);
 }
 
 // Next record of the stream; false at the end of all files (or error).
@@ -165,14 +194,19 @@ bool next_record(nt_reader* r, std::string& name, std::string& seq) {
       continue;
     }
     name = line.substr(1);
-    std::string plus, qual;
-    if (!get_line(r, seq) || !get_line(r, plus) || plus.empty() || plus[0] != '+') {
+    // the sequence line goes straight into the chunk's blob (seq_direct)
+    std::string plus;
+    const size_t s0 = r->c().seqs_blob.size();
+    size_t sl = 0, ql = 0, k = 0;
+    if (!take_line(r, &r->c().seqs_blob, &sl) || !get_line(r, plus) || plus.empty() || plus[0] != '+') {
+      r->c().seqs_blob.resize(s0);
       r->err = "malformed FASTQ record '" + name + "'";
       return false;
     }
-    // quality may in principle wrap; consume lines until its length matches
-    size_t ql = 0;
-    while (ql < seq.size() && get_line(r, qual)) ql += qual.size();
+    // quality may in principle wrap; skip lines until its length matches
+    while (ql < sl && take_line(r, nullptr, &k)) ql += k;
+    r->seq_mark = s0;
+    r->seq_direct = true;
     return true;
   }
 }
@@ -223,32 +257,34 @@ int64_t nt_reader_next(nt_reader* r, uint64_t nrec, const char* const** names,
                        const uint64_t** name_lens, const char* const** seqs,
                        const uint64_t** seq_lens) {
   if (!r || !names || !name_lens || !seqs || !seq_lens || nrec == 0) return NT_E_ARG;
-  r->names_blob.clear();
-  r->seqs_blob.clear();
-  r->name_off.clear();
-  r->seq_off.clear();
-  r->name_len.clear();
-  r->seq_len.clear();
+  r->cur ^= 1;
+  r->c().names_blob.clear();
+  r->c().seqs_blob.clear();
+  r->c().name_off.clear();
+  r->c().seq_off.clear();
+  r->c().name_len.clear();
+  r->c().seq_len.clear();
   if (!r->gz && r->file_idx == 0 && !open_next(r)) return r->err.empty() ? 0 : NT_E_ARG;
   std::string name, seq;
-  while (r->name_len.size() < nrec) {
+  while (r->c().name_len.size() < nrec) {
+    r->seq_direct = false;
     if (!next_record(r, name, seq)) {
       if (!r->err.empty()) return NT_E_ARG;
       break;
     }
     add_record(r, name, seq);
   }
-  const size_t n = r->name_len.size();
-  r->name_ptr.resize(n);
-  r->seq_ptr.resize(n);
+  const size_t n = r->c().name_len.size();
+  r->c().name_ptr.resize(n);
+  r->c().seq_ptr.resize(n);
   for (size_t i = 0; i < n; ++i) {
-    r->name_ptr[i] = r->names_blob.data() + r->name_off[i];
-    r->seq_ptr[i] = r->seqs_blob.data() + r->seq_off[i];
+    r->c().name_ptr[i] = r->c().names_blob.data() + r->c().name_off[i];
+    r->c().seq_ptr[i] = r->c().seqs_blob.data() + r->c().seq_off[i];
   }
-  *names = r->name_ptr.data();
-  *name_lens = r->name_len.data();
-  *seqs = r->seq_ptr.data();
-  *seq_lens = r->seq_len.data();
+  *names = r->c().name_ptr.data();
+  *name_lens = r->c().name_len.data();
+  *seqs = r->c().seq_ptr.data();
+  *seq_lens = r->c().seq_len.data();
   r->records_total += n;
   return (int64_t)n;
 }

@@ -15,6 +15,7 @@ only.  Plots and --analysis are out of scope of this build.
 """
 import os
 import time
+from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 
@@ -87,6 +88,10 @@ def _summary_stats(v):
             f"3rd Qu. {q[3]:g}  Max. {q[4]:g}")
 
 
+def _write_read(path, name, seq, rc):
+    write_fasta_gz(path, name, reverse_complement(seq) if rc else seq)
+
+
 def _scan_chunk(nt, ch, use_filter, write_reads, log):
     """Scan + call one chunk (after --use_filter when on).  Returns
     (rel_serials, row_order, rel_max, result, names, lengths, {read: seq})
@@ -110,6 +115,33 @@ def _scan_chunk(nt, ch, use_filter, write_reads, log):
     return rel, order, rmax, res, names, lens, seqs
 
 
+class _Prefetch:
+    """Chunk k+1 is parsed on a worker thread while chunk k is scanned: the C++
+    reader keeps two chunk buffers in turn and ctypes drops the GIL."""
+
+    def __init__(self, rdr, nrec):
+        self._rdr, self._nrec = rdr, nrec
+        self._ex = ThreadPoolExecutor(1)
+        self._f = self._ex.submit(rdr.next_chunk, nrec)
+
+    def next_chunk(self):
+        if self._f is None:
+            return None
+        ch = self._f.result()
+        self._f = self._ex.submit(self._rdr.next_chunk, self._nrec) if ch is not None else None
+        return ch
+
+    def close(self):
+        if self._f is not None:
+            self._f.cancel()
+            try:
+                self._f.result()
+            except Exception:  # noqa: BLE001 -- a read error after the last chunk used
+                pass
+            self._f = None
+        self._ex.shutdown()
+
+
 def run(input_path, save_path, patterns, fmt="fastq", nrec=10000, rc=False, min_density=0.6,
         subseq_length=100, check_right_edge=False, tvr_patterns=None, legacy_no_ext=False,
         device=0, write_reads=True, sci_threshold=None, use_filter=False, log=print):
@@ -127,6 +159,9 @@ def run(input_path, save_path, patterns, fmt="fastq", nrec=10000, rc=False, min_
     tvr = tvr_patterns is not None
     rdr = Reader(input_path, fmt)
     files = rdr.files()
+    src = _Prefetch(rdr, nrec)
+    writers = ThreadPoolExecutor(min(16, os.cpu_count() or 1)) if write_reads else None
+    pending = []
     lengths_all = []
     local_rows = {}
     k = 0  # global chunk index
@@ -139,7 +174,7 @@ def run(input_path, save_path, patterns, fmt="fastq", nrec=10000, rc=False, min_
         own = None
         n_round = 0
         for r in range(world):
-            ch = rdr.next_chunk(nrec)
+            ch = src.next_chunk()
             if ch is None:
                 break
             n_round += 1
@@ -160,14 +195,19 @@ def run(input_path, save_path, patterns, fmt="fastq", nrec=10000, rc=False, min_
             ser = shard.assign_chunk_serials(rel, starts[r])
             local_rows[k + r] = chunk_rows(res, names, lens, ser, order, nt.n_pass)
             if write_reads:
-                for j in order:
-                    j = int(j)
-                    seq = reverse_complement(seqs[j]) if rc else seqs[j]
-                    write_fasta_gz(os.path.join(reads_dir, f"{r_as_character(float(ser[j]))}.fasta.gz"),
-                                   names[j], seq)
+                for f in pending:  # the previous chunk's files (errors surface here)
+                    f.result()
+                pending = [writers.submit(_write_read, os.path.join(
+                    reads_dir, f"{r_as_character(float(ser[int(j)]))}.fasta.gz"), names[int(j)],
+                    seqs[int(j)], rc) for j in order]
         k += n_round
         if n_round < world:
             break
+    for f in pending:
+        f.result()
+    if writers is not None:
+        writers.shutdown()
+    src.close()
     rows = shard.gather_rows(local_rows)
     rdr.close()
     nt.close()

@@ -26,7 +26,8 @@ from ._lib import NanoTelError, lib
 
 
 class Chunk:
-    """One nt_reader_next() chunk; valid until the reader advances."""
+    """One nt_reader_next() chunk; valid through the next next_chunk() call
+    (the reader double-buffers), not after the one that follows."""
 
     def __init__(self, n, names_p, name_lens_p, seqs_p, seq_lens_p):
         self.n = int(n)
@@ -154,8 +155,11 @@ def r_as_character(x):
 
 
 def write_fasta_gz(path, name, seq, width=80):
-    """writeXStringSet(x, path, compress = TRUE): '>' name, 80-column lines."""
-    with gzip.open(path, "wb") as f:
-        f.write(b">" + name.encode() + b"\n")
-        for i in range(0, len(seq), width):
-            f.write(seq[i:i + width] + b"\n")
+    """writeXStringSet(x, path, compress = TRUE): '>' name, 80-column lines,
+    gzip at R's gzfile() default level 6.  One buffer, one zlib call (which
+    drops the GIL, so the driver writes a chunk's reads on a thread pool)."""
+    parts = [b">" + name.encode()]
+    parts += [seq[i:i + width] for i in range(0, len(seq), width)]
+    data = b"\n".join(parts) + b"\n"
+    with open(path, "wb") as f:
+        f.write(gzip.compress(data, compresslevel=6, mtime=0))

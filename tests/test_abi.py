@@ -125,3 +125,65 @@ def test_pack_reads_layout_and_rc():
                 c = int((w[0] >> (pos % 32)) & 1) | (int((w[1] >> (pos % 32)) & 1) << 1)
                 out.append(codes[exc[pos]] if pos in exc else "ACGT"[c])
             assert "".join(out) == ref, (r, rcflag)
+
+
+@pytest.mark.parametrize("rcflag", [0, 1])
+def test_pack_reads_whole_blocks_random(rcflag):
+    """The 32-bases-at-a-time packer (whole blocks of plain bases) against a
+    numpy decode: mixed case, ragged lengths, a few IUPAC letters so that
+    some blocks take the per-base path next to fast ones."""
+    import ctypes
+    from nanotel_amd import _lib
+    L = _lib.lib()
+    rng = np.random.default_rng(7 + rcflag)
+    alpha = np.frombuffer(b"ACGTacgt", np.uint8)
+    seqs = []
+    for r in range(40):
+        n = int(rng.integers(1, 3000))
+        s = alpha[rng.integers(0, 8, n)].copy()
+        if r % 3 == 0:
+            k = int(rng.integers(1, 4))
+            s[rng.integers(0, n, k)] = np.frombuffer(b"N", np.uint8)[0]
+        seqs.append(s.tobytes())
+    n = len(seqs)
+    ptrs = (ctypes.c_char_p * n)(*seqs)
+    lens = np.array([len(s) for s in seqs], np.uint64)
+    tb, tw, te, ml, bad = (ctypes.c_uint64() for _ in range(5))
+    assert L.nt_pack_count(ctypes.cast(ptrs, ctypes.c_void_p), lens.ctypes.data, n, 100,
+                           ctypes.byref(tb), ctypes.byref(tw), ctypes.byref(te), ctypes.byref(ml),
+                           ctypes.byref(bad)) == 0
+    assert te.value == sum(s.upper().count(b"N") for s in seqs)
+    planes = np.full(2 * tb.value, 0xDEADBEEF, np.uint32)
+    blk = np.zeros(n, np.uint64)
+    ln = np.zeros(n, np.uint32)
+    wo = np.zeros(n, np.uint64)
+    eo = np.zeros(n + 1, np.uint32)
+    ep = np.zeros(max(1, te.value), np.uint32)
+    ec = np.zeros(max(1, te.value), np.uint8)
+    assert L.nt_pack_reads(ctypes.cast(ptrs, ctypes.c_void_p), lens.ctypes.data, n, rcflag, 100,
+                           planes.ctypes.data, blk.ctypes.data, ln.ctypes.data, wo.ctypes.data,
+                           eo.ctypes.data, ep.ctypes.data, ec.ctypes.data) == 0
+    lut = np.full(256, 255, np.uint8)
+    for i, ch in enumerate(b"ACGT"):
+        lut[ch] = i
+        lut[ch + 32] = i
+    for r, s in enumerate(seqs):
+        a = np.frombuffer(s, np.uint8)
+        code = lut[a]
+        if rcflag:
+            code = code[::-1]
+            code = np.where(code == 255, 255, 3 - code)
+        m = len(s)
+        nblk = (m + 31) // 32
+        w = planes[2 * int(blk[r]):2 * (int(blk[r]) + nblk)].reshape(nblk, 2)
+        bits = np.arange(32, dtype=np.uint32)
+        lo = ((w[:, 0:1] >> bits) & 1).reshape(-1)[:m]
+        hi = ((w[:, 1:2] >> bits) & 1).reshape(-1)[:m]
+        got = (lo | (hi << 1)).astype(np.uint8)
+        exc = code == 255
+        assert np.array_equal(got[~exc], code[~exc]), r
+        assert np.all(got[exc] == 0), r  # planes hold A at exception positions
+        pos = ep[eo[r]:eo[r + 1]]
+        assert np.array_equal(np.sort(pos), np.flatnonzero(exc)), r
+        if nblk < 2 * ((m + 63) // 64):  # pad block of the 64-base segment is zeroed
+            assert planes[2 * (int(blk[r]) + nblk)] == 0 and planes[2 * (int(blk[r]) + nblk) + 1] == 0

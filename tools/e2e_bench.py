@@ -1,0 +1,77 @@
+"""End-to-end throughput: FASTQ(.gz) file -> summary.csv through the driver
+("End-to-end (file -> summary.csv) Gbases/s is reported
+separately").  This is the host-buffer path -- C++ reader, host 2-bit packer,
+pageable upload over PCIe, scan + call, rows back, serials, CSV -- not the
+bench.py metric (device-resident inputs).
+
+Synthetic Nanopore-like reads (uniform ACGT, half of them with a 1-15 kb
+(TTAGGG)n tract at the left edge, 2 % substitutions) are written once with
+numpy, then the driver runs over them with NanoTel's default nrec (10,000) unless --nrec says otherwise.
+Timed twice: without and with the per-read reads/<serial>.fasta.gz writes.
+
+    python tools/e2e_bench.py [--reads 8000] [--read_len 50000] [--nrec 10000] [--gz] [--dir /tmp/e2e]
+"""
+import argparse
+import gzip
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "telomere-analyzer_amd"))
+
+
+def write_input(path, n, L, gz, seed=20260501):
+    rng = np.random.default_rng(seed)
+    acgt = np.frombuffer(b"ACGT", np.uint8)
+    unit = np.frombuffer(b"TTAGGG", np.uint8)
+    op = gzip.open if gz else open
+    with op(path, "wb") as f:
+        for r in range(n):
+            s = acgt[rng.integers(0, 4, L)]
+            if rng.random() < 0.5:
+                t = min(L, int(rng.integers(1000, 15001)))
+                tract = np.resize(unit, t)
+                sub = rng.random(t) < 0.02
+                tract[sub] = acgt[rng.integers(0, 4, int(sub.sum()))]
+                s[:t] = tract
+            q = b"I" * L
+            f.write(b"@read_%d\n" % r + s.tobytes() + b"\n+\n" + q + b"\n")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reads", type=int, default=8000)
+    ap.add_argument("--read_len", type=int, default=50000)
+    ap.add_argument("--nrec", type=int, default=10000)
+    ap.add_argument("--gz", action="store_true")
+    ap.add_argument("--dir", default="/tmp/nt_e2e")
+    a = ap.parse_args()
+    os.makedirs(a.dir, exist_ok=True)
+    inp = os.path.join(a.dir, "reads.fastq" + (".gz" if a.gz else ""))
+    t = time.perf_counter()
+    write_input(inp, a.reads, a.read_len, a.gz)
+    gen_s = time.perf_counter() - t
+    from nanotel_amd import driver
+    bases = a.reads * a.read_len
+    out = {"input": os.path.basename(inp), "reads": a.reads, "nrec": a.nrec, "read_len": a.read_len, "bases": bases,
+           "input_bytes": os.path.getsize(inp), "generate_s": round(gen_s, 2)}
+    # warm-up (hiprtc specialisation, device buffers) on a small prefix-free run
+    driver.run(inp, os.path.join(a.dir, "warm"), "TTAGGG", fmt="fastq", nrec=10000, write_reads=False,
+               log=lambda *x: None)
+    for write_reads in (False, True):
+        save = os.path.join(a.dir, "out_reads" if write_reads else "out")
+        t = time.perf_counter()
+        rows, _ = driver.run(inp, save, "TTAGGG", fmt="fastq", nrec=a.nrec, write_reads=write_reads,
+                             log=lambda *x: None)
+        s = time.perf_counter() - t
+        key = "with_reads_fasta_gz" if write_reads else "summary_only"
+        out[key] = {"seconds": round(s, 3), "Gbases_per_s": round(bases / s / 1e9, 3), "rows": len(rows)}
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
