@@ -5,8 +5,10 @@ block (NanoTel.R:30-93) and its argument checks (NanoTel.R:104-137).
 
 Multi-GPU: launch one process per GPU with torch.distributed.run; chunks are
 dealt round-robin to the ranks (driver.py / shard.py), rank 0 writes the
-summary.  --use_filter runs the edge pre-filter on the GPU.  --analysis and
-the plots are not part of this build.
+summary.  --use_filter runs the edge pre-filter on the GPU.  --analysis writes
+<barcode>_filtered_sorted_summary.csv and <barcode>_results.txt (analysis.py;
+not its ggplot2 PNG).  The single-read plots are written as in the reference
+(plots.py) unless --no_plots.
 """
 import argparse
 import os
@@ -34,10 +36,13 @@ def parser():
     ap.add_argument("--tvr_patterns", default=None,
                     help="Space separated list of additional pattern(s) for Telomere variant repeats.")
     ap.add_argument("--version", action="store_true", help="Print version information and exit")
-    ap.add_argument("--analysis", action="store_true", help="Post-processing (not part of this build).")
+    ap.add_argument("--analysis", action="store_true",
+                    help="Post-processing: filtered sorted summary and results text (no plot).")
     # build-specific
     ap.add_argument("--device", type=int, default=None, help="GPU index (default: LOCAL_RANK or 0)")
     ap.add_argument("--no_reads", action="store_true", help="do not write reads/<serial>.fasta.gz")
+    ap.add_argument("--no_plots", action="store_true", help="do not write single_read_plots*/")
+    ap.add_argument("--no_jpeg", action="store_true", help="write the .eps plots only")
     ap.add_argument("--legacy_no_ext", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--readr_sci_threshold", type=float, default=None, help=argparse.SUPPRESS)
     return ap
@@ -56,8 +61,6 @@ def main(argv=None):
         sys.exit("Error: Missing required parameter:  --input_path")
     if a.format not in ("fasta", "fastq"):
         sys.exit("Error: Format should be a string fastq or fasta")
-    if a.analysis:
-        sys.exit("Error: --analysis is not supported by this build")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dev = a.device if a.device is not None else local
@@ -71,7 +74,8 @@ def main(argv=None):
             min_density=a.min_density, subseq_length=a.subseq_length,
             check_right_edge=a.check_right_edge, tvr_patterns=a.tvr_patterns,
             legacy_no_ext=a.legacy_no_ext, device=dev, write_reads=not a.no_reads,
-            sci_threshold=a.readr_sci_threshold, use_filter=a.use_filter)
+            sci_threshold=a.readr_sci_threshold, use_filter=a.use_filter,
+            analysis=a.analysis, plot=not a.no_plots, plot_jpeg=not a.no_jpeg)
     finally:
         if world > 1:
             import torch.distributed as dist

@@ -11,7 +11,9 @@ With torch.distributed initialised (one process per GPU), chunks are dealt
 round-robin to ranks and the serials are fixed by one all_reduce (shard.py);
 rank 0 writes the summary.  --use_filter runs the edge pre-filter on the GPU
 (nt_filter_host, NanoTel.R:2083-2163, 2227-2232) and scans the kept reads
-only.  Plots and --analysis are out of scope of this build.
+only.  --analysis writes the filtered/sorted summary and the results text
+(analysis.py).  Every telomeric read gets the reference's three density plots
+(plots.py: single_read_plots*/read<serial>.jpeg|eps) unless plot=False.
 """
 import os
 import time
@@ -19,7 +21,8 @@ from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 
-from . import shard
+from . import plots, shard
+from .analysis import write_analysis
 from .api import NanoTel
 from .io import Reader, csv_field, format_double, format_int, r_as_character, write_fasta_gz
 
@@ -92,7 +95,26 @@ def _write_read(path, name, seq, rc):
     write_fasta_gz(path, name, reverse_complement(seq) if rc else seq)
 
 
-def _scan_chunk(nt, ch, use_filter, write_reads, log):
+def _plot_jobs(nt, res, order, lens, ser, save_path):
+    """Arguments of plots.write_read_plots for every row of a chunk (the three
+    single-read plots of analyze_read, NanoTel.R:1876-1912)."""
+    jobs = []
+    for j in order:
+        j = int(j)
+        n = int(lens[j])
+        if int(res["n_windows"][j]) == 0:
+            continue
+        tabs = [plots.window_table(n, nt.subseq_length, nt.window_counts(res, j, p)) for p in range(nt.n_pass)]
+        se = [(int(res["start"][j, p]), int(res["end"][j, p])) for p in range(nt.n_pass)]
+        kw = {}
+        if nt.n_pass == 3:
+            kw = dict(subs_tvr=tabs[2], tvr_start=se[2][0], tvr_end=se[2][1])
+        jobs.append(((save_path, r_as_character(float(ser[j])), n, tabs[0], tabs[1], se[0][0], se[0][1],
+                      se[1][0], se[1][1]), kw))
+    return jobs
+
+
+def _scan_chunk(nt, ch, use_filter, write_reads, log, want_windows=False):
     """Scan + call one chunk (after --use_filter when on).  Returns
     (rel_serials, row_order, rel_max, result, names, lengths, {read: seq})
     over the reads that were scanned."""
@@ -103,12 +125,12 @@ def _scan_chunk(nt, ch, use_filter, write_reads, log):
             log("No read have passed the filteration at run_with_rc_and_filter!")
             return None, np.zeros(0, np.int64), shard.SKIPPED, None, [], lens[:0], {}
         seqs = [ch.seq(int(j)) for j in keep]
-        res = nt.analyze(seqs)
+        res = nt.analyze(seqs, want_windows=want_windows)
         names = [names[int(j)] for j in keep]
         lens = lens[keep]
         get = seqs.__getitem__
     else:
-        res = nt.analyze_chunk(ch)
+        res = nt.analyze_chunk(ch, want_windows=want_windows)
         get = lambda j: ch.seq(j)  # noqa: E731
     rel, order, rmax = shard.chunk_relative(res["telomeric"])
     seqs = {int(j): get(int(j)) for j in order} if write_reads else {}
@@ -144,7 +166,8 @@ class _Prefetch:
 
 def run(input_path, save_path, patterns, fmt="fastq", nrec=10000, rc=False, min_density=0.6,
         subseq_length=100, check_right_edge=False, tvr_patterns=None, legacy_no_ext=False,
-        device=0, write_reads=True, sci_threshold=None, use_filter=False, log=print):
+        device=0, write_reads=True, sci_threshold=None, use_filter=False, analysis=False,
+        plot=True, plot_jpeg=True, log=print):
     """Run the pipeline; returns (summary rows, all read lengths) on rank 0."""
     import torch.distributed as dist
     dist_on = dist.is_available() and dist.is_initialized()
@@ -153,6 +176,9 @@ def run(input_path, save_path, patterns, fmt="fastq", nrec=10000, rc=False, min_
     os.makedirs(save_path, exist_ok=True)
     reads_dir = os.path.join(save_path, "reads")
     os.makedirs(reads_dir, exist_ok=True)
+    if plot:  # create_dirs (NanoTel.R:1978-1996)
+        os.makedirs(os.path.join(save_path, "single_read_plots"), exist_ok=True)
+        os.makedirs(os.path.join(save_path, "single_read_plots_adj"), exist_ok=True)
     nt = NanoTel(patterns=patterns, tvr_patterns=tvr_patterns, subseq_length=subseq_length,
                  min_density=min_density, check_right_edge=check_right_edge, rc=rc,
                  legacy_no_ext=legacy_no_ext, device=device)
@@ -160,7 +186,7 @@ def run(input_path, save_path, patterns, fmt="fastq", nrec=10000, rc=False, min_
     rdr = Reader(input_path, fmt)
     files = rdr.files()
     src = _Prefetch(rdr, nrec)
-    writers = ThreadPoolExecutor(min(16, os.cpu_count() or 1)) if write_reads else None
+    writers = ThreadPoolExecutor(min(16, os.cpu_count() or 1)) if (write_reads or plot) else None
     pending = []
     lengths_all = []
     local_rows = {}
@@ -181,7 +207,7 @@ def run(input_path, save_path, patterns, fmt="fastq", nrec=10000, rc=False, min_
             lengths_all.append(ch.lengths.copy())
             if r == rank:
                 log(f"processing chunk {k + r + 1} ...")
-                own = (r,) + _scan_chunk(nt, ch, use_filter, write_reads, log)
+                own = (r,) + _scan_chunk(nt, ch, use_filter, write_reads, log, want_windows=plot)
         if n_round == 0:
             break
         maxima = shard.exchange_rel_max({own[0]: own[3]} if own else {}, n_round)
@@ -194,12 +220,16 @@ def run(input_path, save_path, patterns, fmt="fastq", nrec=10000, rc=False, min_
             r, rel, order, _, res, names, lens, seqs = own
             ser = shard.assign_chunk_serials(rel, starts[r])
             local_rows[k + r] = chunk_rows(res, names, lens, ser, order, nt.n_pass)
+            for f in pending:  # the previous chunk's files (errors surface here)
+                f.result()
+            pending = []
             if write_reads:
-                for f in pending:  # the previous chunk's files (errors surface here)
-                    f.result()
-                pending = [writers.submit(_write_read, os.path.join(
+                pending += [writers.submit(_write_read, os.path.join(
                     reads_dir, f"{r_as_character(float(ser[int(j)]))}.fasta.gz"), names[int(j)],
                     seqs[int(j)], rc) for j in order]
+            if plot:
+                pending += [writers.submit(plots.write_read_plots, *a, jpeg=plot_jpeg, **kw)
+                            for a, kw in _plot_jobs(nt, res, order, lens, ser, save_path)]
         k += n_round
         if n_round < world:
             break
@@ -219,6 +249,8 @@ def run(input_path, save_path, patterns, fmt="fastq", nrec=10000, rc=False, min_
     with open(os.path.join(save_path, "reads_ids.txt"), "w") as f:
         for r in rows:
             f.write(r[1] + "\n")
+    if analysis:  # --analysis post-processing (NanoTel.R:2437-2508)
+        write_analysis(save_path, barcode, rows, columns(tvr), format_row, sci_threshold)
     with open(os.path.join(save_path, "run.log"), "w") as f:
         f.write(VERSION + "\n")
         f.write(f"Work started at: {time.strftime('%Y-%m-%d %H:%M:%S', time.localtime(t0))}\n")

@@ -7,6 +7,7 @@ Outputs (all *data*, no reference source):
   sample.fasta                    -- Example/sample.fasta (the C1 input, 4 reads)
   example_summary.csv             -- Example/Example_output/summary.csv (2023 code version)
   reads/{1..4}.fasta              -- Example/Example_output/reads/*.fasta (written telomeric reads)
+  eps/read{1..4}.eps              -- Example/Example_output/single_read_plots_adj/read*.eps (plots)
   example_window_counts.json      -- per-window covered-base counts for P1 (exact)
                                      and P2 (1 mismatch), decoded from the density
                                      polygons of Example_output/single_read_plots_adj/read*.eps
@@ -87,6 +88,11 @@ def main():
     for serial in range(1, 5):
         shutil.copyfile(os.path.join(REF, "Example_output", "reads", f"{serial}.fasta"),
                         os.path.join(HERE, "reads", f"{serial}.fasta"))
+    # the single-read EPS plots as the reference wrote them (expected outputs of plots.py)
+    os.makedirs(os.path.join(HERE, "eps"), exist_ok=True)
+    for serial in range(1, 5):
+        shutil.copyfile(os.path.join(REF, "Example_output", "single_read_plots_adj", f"read{serial}.eps"),
+                        os.path.join(HERE, "eps", f"read{serial}.eps"))
     names, seqs = read_fasta(os.path.join(REF, "sample.fasta"))
     L = 100
     result = {"L": L, "min_density": 0.6, "patterns": "TTAGGG", "reads": []}

@@ -24,6 +24,7 @@ class OracleNanoTel:
                        legacy_no_ext=legacy_no_ext, want_windows=False, want_hits=False)
         self.rc = rc
         self.n_pass = 3 if tvr_patterns else 2
+        self.subseq_length = subseq_length
 
     def _scan_orientation(self, s):
         s = s.decode() if isinstance(s, bytes) else s
@@ -33,24 +34,32 @@ class OracleNanoTel:
         return np.array([O.filter_read(self._scan_orientation(ch.seq(i)), self.P, self.kw["min_density"],
                                        self.kw["right_edge"]) for i in range(ch.n)], bool)
 
-    def analyze_chunk(self, ch):
-        return self.analyze([ch.seq(i) for i in range(ch.n)])
+    def analyze_chunk(self, ch, want_windows=False):
+        return self.analyze([ch.seq(i) for i in range(ch.n)], want_windows)
 
-    def analyze(self, seqs):
+    def analyze(self, seqs, want_windows=False):
         n = len(seqs)
         res = {"start": np.full((n, 3), -1, np.int32), "end": np.full((n, 3), -1, np.int32),
-               "density": np.zeros((n, 3)), "telomeric": np.zeros(n, bool)}
+               "density": np.zeros((n, 3)), "telomeric": np.zeros(n, bool),
+               "n_windows": np.zeros(n, np.int64), "wins": []}
+        kw = dict(self.kw, want_windows=want_windows)
         for i in range(n):
             s = seqs[i].decode() if isinstance(seqs[i], bytes) else seqs[i]
             if self.rc:
                 s = O.reverse_complement(s)
-            r = O.analyze_read(s, self.P, **self.kw)
+            r = O.analyze_read(s, self.P, **kw)
             k = r["n_pass"]
             res["start"][i, :k] = r["start"]
             res["end"][i, :k] = r["end"]
             res["density"][i, :k] = r["density"]
             res["telomeric"][i] = r["telomeric"]
+            if want_windows:
+                res["n_windows"][i] = len(r["win_counts"][0])
+                res["wins"].append(r["win_counts"])
         return res
+
+    def window_counts(self, res, read, p):
+        return res["wins"][read][p]
 
     def close(self):
         pass
@@ -97,7 +106,8 @@ def _rank_main(rank, world, port, inp, out, rc, use_filter=False):
         os.environ["MASTER_ADDR"] = "127.0.0.1"
         os.environ["MASTER_PORT"] = str(port)
         dist.init_process_group("gloo", rank=rank, world_size=world)
-    driver.run(inp, out, "TTAGGG", fmt="fasta", nrec=3, rc=rc, use_filter=use_filter, log=lambda *a: None)
+    driver.run(inp, out, "TTAGGG", fmt="fasta", nrec=3, rc=rc, use_filter=use_filter, analysis=True,
+               log=lambda *a: None)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
@@ -136,6 +146,14 @@ def test_sharded_driver_matches_single_process(rc):
         assert [int(line.split(",")[0]) for line in summary[1:]] == sorted(
             int(line.split(",")[0]) for line in summary[1:])
         assert res[1]["reads_ids.txt"].decode().splitlines() == [line.split(",")[1] for line in summary[1:]]
+        # --analysis outputs (rank 0) agree across world sizes too and follow analysis.analyze
+        from nanotel_amd import analysis
+        assert "in_filtered_sorted_summary.csv" in res[1] and "in_results.txt" in res[1]
+        fs = res[1]["in_filtered_sorted_summary.csv"].decode().splitlines()
+        assert fs[0].endswith(",TelLenMM_RunningMed,SeqLen_minus_RunMed")
+        assert res[1]["in_results.txt"].decode().splitlines()[2].endswith(f": {len(fs) - 1}")
+        lens = [int(line.split(",")[2]) for line in fs[1:]]
+        assert lens == sorted(lens, reverse=True) and analysis.MAX_START_MM == 134
 
 
 def _filter_input(d):

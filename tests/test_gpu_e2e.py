@@ -1,9 +1,10 @@
 """End to end on the GPU: the command line (python -m nanotel_amd) reading
 FASTA/FASTQ(.gz), scanning on the MI355X and writing summary.csv,
-reads_ids.txt and reads/<serial>.fasta.gz.
+reads_ids.txt, reads/<serial>.fasta.gz and the single-read plots.
 
 * Example/sample.fasta in legacy mode (the 2023 code that produced
-  Example_output) -> byte-identical summary.csv and reads/*.fasta;
+  Example_output) -> byte-identical summary.csv, reads/*.fasta and
+  single_read_plots_adj/read*.eps;
 * a multi-file, multi-chunk FASTQ(.gz) input -> the same files as the
   oracle-driven driver (tests/test_driver.py's stand-in).
 """
@@ -36,6 +37,12 @@ def test_cli_example_legacy_byte_identical(tmp_path):
             os.path.join(GOLD, "reads", f"{i}.fasta"), "rb").read()
     names, _ = O.read_fasta(os.path.join(GOLD, "sample.fasta"))
     assert (out / "reads_ids.txt").read_text().splitlines() == names
+    # the single-read EPS plots from the GPU's window counts: the reference's files byte for byte
+    for i in range(1, 5):
+        assert (out / "single_read_plots_adj" / f"read{i}.eps").read_bytes() == open(
+            os.path.join(GOLD, "eps", f"read{i}.eps"), "rb").read()
+        assert (out / "single_read_plots" / f"read{i}.jpeg").stat().st_size > 1000
+        assert (out / "single_read_plots_adj" / f"read{i}.jpeg").stat().st_size > 1000
 
 
 def test_cli_example_current_code(tmp_path):
@@ -66,7 +73,8 @@ def test_driver_gpu_matches_oracle_driver(tmp_path, rc):
     a, b = _outputs(gpu_out), _outputs(ora_out)
     assert a == b
     assert len(a["in_summary.csv"].splitlines()) > 5
-    assert np.all([k.endswith(".fasta.gz") or k in ("in_summary.csv", "reads_ids.txt") for k in a])
+    assert np.all([k.endswith((".fasta.gz", ".eps", ".jpeg")) or k in ("in_summary.csv", "reads_ids.txt") for k in a])
+    assert any(k.endswith(".eps") for k in a)  # the plots (window counts from the GPU) match too
 
 
 def test_driver_use_filter_gpu_matches_oracle_driver(tmp_path):

@@ -1,0 +1,91 @@
+"""Single-read plots (plots.py; NanoTel.R:1271-1624, 1876-1912) on CPU.
+
+* The reference's Example plots (single_read_plots_adj/read1-4.eps, committed
+  as tests/golden/eps) are reproduced byte for byte from the golden window
+  counts and summary rows (tests/golden/make_golden.py);
+* every branch of the two plot functions (no exact telomere, no mismatch
+  telomere, TVR pass found or not) writes a well-formed EPS and JPEGs;
+* x-axis label thinning keeps labels at least one "m" apart.
+"""
+import json
+import os
+import re
+
+import pytest
+
+from nanotel_amd import plots
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _golden():
+    g = json.load(open(os.path.join(GOLD, "example_window_counts.json")))
+    rows = [ln.split(",") for ln in open(os.path.join(GOLD, "example_summary.csv")).read().splitlines()[1:]]
+    return g, rows
+
+
+@pytest.mark.parametrize("serial", [1, 2, 3, 4])
+def test_example_eps_byte_identical(serial):
+    g, rows = _golden()
+    rec, row = g["reads"][serial - 1], rows[serial - 1]
+    subs = plots.window_table(rec["n"], g["L"], rec["p1_counts"])
+    subs_mm = plots.window_table(rec["n"], g["L"], rec["p2_counts"])
+    ops = plots.plot_ops(rec["n"], rec["n"], subs, subs_mm, int(row[4]), int(row[5]), int(row[8]), int(row[9]))
+    assert plots.render_eps(ops) == open(os.path.join(GOLD, "eps", f"read{serial}.eps")).read()
+
+
+def _polys(eps):
+    return re.findall(r"/bg \{ ([^}]*) \} def\n(?:[^\n]*\n)*?np\n ", eps)
+
+
+CASES = [
+    # seq_start, seq_end, gray_start, gray_end, tvr (start, end) or None
+    (1, 3000, 1, 3400, None),
+    (200, 3000, 150, 3400, None),
+    (-1, -1, 400, 2000, None),
+    (1, 3000, -1, -1, None),
+    (1, 3000, 1, 3400, (1, 3600)),
+    (300, 3000, 250, 3400, (100, 3600)),
+    (1, 3000, -1, -1, (-1, -1)),
+    (1, 3000, -1, -1, (1, 3500)),
+    (-1, -1, 400, 2000, (300, 2500)),
+    (-1, -1, 400, 2000, (-1, -1)),
+]
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_branches_write_files(tmp_path, case):
+    s1, e1, s2, e2, tvr = case
+    n, L = 7345, 100
+    nw = 73
+    c1 = [min(100, (k * 7) % 101) for k in range(nw)]
+    c2 = [min(100, c + 3) for c in c1]
+    c3 = [min(100, c + 5) for c in c1]
+    for d in ("single_read_plots", "single_read_plots_adj"):
+        os.makedirs(tmp_path / d)
+    kw = {}
+    if tvr is not None:
+        kw = dict(subs_tvr=plots.window_table(n, L, c3), tvr_start=tvr[0], tvr_end=tvr[1])
+    plots.write_read_plots(str(tmp_path), "12", n, plots.window_table(n, L, c1), plots.window_table(n, L, c2),
+                           s1, e1, s2, e2, **kw)
+    eps = (tmp_path / "single_read_plots_adj" / "read12.eps").read_text()
+    assert eps.startswith("%!PS-Adobe-3.0 EPSF-3.0") and eps.endswith("%%EOF\n")
+    assert eps.count("cp p3") == (3 if tvr is not None else 2) and eps.count("cp p1") == 1
+    legend = 7 if tvr is not None else 5
+    assert eps.count("findfont 14 s") == 2  # legend, main title
+    assert len(re.findall(r"\) 0 0 t\n|\) 0 ta\n", eps.split("/Font1 findfont 14 s")[1].split("cl\n")[0])) == legend
+    assert "(Read length: 7345 " in eps
+    from PIL import Image
+    for d in ("single_read_plots", "single_read_plots_adj"):
+        im = Image.open(tmp_path / d / "read12.jpeg")
+        assert im.size == (750, 300)
+
+
+def test_axis_label_thinning():
+    fig_ops = plots.plot_ops(plots.MAX_LENGTH, 50000, ([1], [0.5]), ([1], [0.5]), 1, 100, 1, 120)
+    labs = [op for op in fig_ops if op[0] == "text" and op[3].endswith("kb")]
+    assert labs[0][3] == "0.0kb" and 3 < len(labs) < 100
+    gap = plots.str_width("m", 1, 12)
+    for a, b in zip(labs, labs[1:]):
+        wa, wb = plots.str_width(a[3], 1, 12), plots.str_width(b[3], 1, 12)
+        assert (b[1] - 0.5 * wb) - (a[1] + 0.5 * wa) >= gap - 1e-9

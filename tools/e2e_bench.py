@@ -7,9 +7,10 @@ bench.py metric (device-resident inputs).
 Synthetic Nanopore-like reads (uniform ACGT, half of them with a 1-15 kb
 (TTAGGG)n tract at the left edge, 2 % substitutions) are written once with
 numpy, then the driver runs over them with NanoTel's default nrec (10,000) unless --nrec says otherwise.
-Timed twice: without and with the per-read reads/<serial>.fasta.gz writes.
+Timed without and with the per-read reads/<serial>.fasta.gz writes, and with
+--plots also with the three single-read plots per telomeric read.
 
-    python tools/e2e_bench.py [--reads 8000] [--read_len 50000] [--nrec 10000] [--gz] [--dir /tmp/e2e]
+    python tools/e2e_bench.py [--reads 8000] [--read_len 50000] [--nrec 10000] [--gz] [--plots] [--dir /tmp/e2e]
 """
 import argparse
 import gzip
@@ -48,6 +49,7 @@ def main():
     ap.add_argument("--read_len", type=int, default=50000)
     ap.add_argument("--nrec", type=int, default=10000)
     ap.add_argument("--gz", action="store_true")
+    ap.add_argument("--plots", action="store_true", help="also time a run with the single-read plots")
     ap.add_argument("--dir", default="/tmp/nt_e2e")
     a = ap.parse_args()
     os.makedirs(a.dir, exist_ok=True)
@@ -61,14 +63,16 @@ def main():
            "input_bytes": os.path.getsize(inp), "generate_s": round(gen_s, 2)}
     # warm-up (hiprtc specialisation, device buffers) on a small prefix-free run
     driver.run(inp, os.path.join(a.dir, "warm"), "TTAGGG", fmt="fastq", nrec=10000, write_reads=False,
-               log=lambda *x: None)
-    for write_reads in (False, True):
-        save = os.path.join(a.dir, "out_reads" if write_reads else "out")
+               plot=False, log=lambda *x: None)
+    runs = [("summary_only", False, False), ("with_reads_fasta_gz", True, False)]
+    if a.plots:
+        runs.append(("with_reads_and_plots", True, True))
+    for key, write_reads, plot in runs:
+        save = os.path.join(a.dir, "out_" + key)
         t = time.perf_counter()
         rows, _ = driver.run(inp, save, "TTAGGG", fmt="fastq", nrec=a.nrec, write_reads=write_reads,
-                             log=lambda *x: None)
+                             plot=plot, log=lambda *x: None)
         s = time.perf_counter() - t
-        key = "with_reads_fasta_gz" if write_reads else "summary_only"
         out[key] = {"seconds": round(s, 3), "Gbases_per_s": round(bases / s / 1e9, 3), "rows": len(rows)}
     print(json.dumps(out))
 
