@@ -95,6 +95,15 @@ def _write_read(path, name, seq, rc):
     write_fasta_gz(path, name, reverse_complement(seq) if rc else seq)
 
 
+def _plot_pool():
+    """Spawned (not forked: this process holds a HIP context) plot workers,
+    one per host core of the GPU's share, at most 16; they import only
+    plots.py and never touch the GPU."""
+    import multiprocessing as mp
+    from concurrent.futures import ProcessPoolExecutor
+    return ProcessPoolExecutor(min(16, os.cpu_count() or 1), mp_context=mp.get_context("spawn"))
+
+
 def _plot_jobs(nt, res, order, lens, ser, save_path):
     """Arguments of plots.write_read_plots for every row of a chunk (the three
     single-read plots of analyze_read, NanoTel.R:1876-1912)."""
@@ -187,6 +196,7 @@ def run(input_path, save_path, patterns, fmt="fastq", nrec=10000, rc=False, min_
     files = rdr.files()
     src = _Prefetch(rdr, nrec)
     writers = ThreadPoolExecutor(min(16, os.cpu_count() or 1)) if (write_reads or plot) else None
+    plotters = None  # worker processes for the plots of large chunks (Python drawing holds the GIL)
     pending = []
     lengths_all = []
     local_rows = {}
@@ -228,8 +238,11 @@ def run(input_path, save_path, patterns, fmt="fastq", nrec=10000, rc=False, min_
                     reads_dir, f"{r_as_character(float(ser[int(j)]))}.fasta.gz"), names[int(j)],
                     seqs[int(j)], rc) for j in order]
             if plot:
-                pending += [writers.submit(plots.write_read_plots, *a, jpeg=plot_jpeg, **kw)
-                            for a, kw in _plot_jobs(nt, res, order, lens, ser, save_path)]
+                jobs = _plot_jobs(nt, res, order, lens, ser, save_path)
+                if len(jobs) >= 64 and plotters is None:
+                    plotters = _plot_pool()
+                pool = plotters if len(jobs) >= 64 else writers
+                pending += [pool.submit(plots.write_read_plots, *a, jpeg=plot_jpeg, **kw) for a, kw in jobs]
         k += n_round
         if n_round < world:
             break
@@ -237,6 +250,8 @@ def run(input_path, save_path, patterns, fmt="fastq", nrec=10000, rc=False, min_
         f.result()
     if writers is not None:
         writers.shutdown()
+    if plotters is not None:
+        plotters.shutdown()
     src.close()
     rows = shard.gather_rows(local_rows)
     rdr.close()

@@ -382,12 +382,15 @@ def render_eps(ops):
 # ---------------------------------------------------------------- JPEG output
 
 
+_JPEG_FONTS = {}  # (face, size) -> PIL font, loaded once per process
+
+
 def render_jpeg(ops, W, H, path):
     """Rasterise the same device operations with PIL (y flipped, 1 pt = 1 px)."""
     from PIL import Image, ImageDraw, ImageFont
     img = Image.new("RGB", (int(W), int(H)), (255, 255, 255))
     dr = ImageDraw.Draw(img)
-    fonts = {}
+    fonts = _JPEG_FONTS
 
     def font(face, size):
         key = (face, size)

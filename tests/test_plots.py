@@ -89,3 +89,32 @@ def test_axis_label_thinning():
     for a, b in zip(labs, labs[1:]):
         wa, wb = plots.str_width(a[3], 1, 12), plots.str_width(b[3], 1, 12)
         assert (b[1] - 0.5 * wb) - (a[1] + 0.5 * wa) >= gap - 1e-9
+
+
+def test_plot_worker_processes(tmp_path):
+    """The driver's spawned plot workers (large chunks) write the same files
+    as the in-process writer."""
+    from nanotel_amd import driver
+    for d in ("single_read_plots", "single_read_plots_adj"):
+        os.makedirs(tmp_path / "a" / d)
+        os.makedirs(tmp_path / "b" / d)
+    g, rows = _golden()
+    jobs = []
+    for rec, row in zip(g["reads"], rows):
+        t1 = plots.window_table(rec["n"], g["L"], rec["p1_counts"])
+        t2 = plots.window_table(rec["n"], g["L"], rec["p2_counts"])
+        jobs.append((str(rec["serial"]), rec["n"], t1, t2, int(row[4]), int(row[5]), int(row[8]), int(row[9])))
+    pool = driver._plot_pool()
+    try:
+        futs = [pool.submit(plots.write_read_plots, str(tmp_path / "a"), *j) for j in jobs]
+        for f in futs:
+            f.result()
+    finally:
+        pool.shutdown()
+    for j in jobs:
+        plots.write_read_plots(str(tmp_path / "b"), *j)
+    for j in jobs:
+        for rel in (f"single_read_plots_adj/read{j[0]}.eps", f"single_read_plots/read{j[0]}.jpeg"):
+            assert (tmp_path / "a" / rel).read_bytes() == (tmp_path / "b" / rel).read_bytes()
+        assert (tmp_path / "a" / f"single_read_plots_adj/read{j[0]}.eps").read_text() == open(
+            os.path.join(GOLD, "eps", f"read{j[0]}.eps")).read()
