@@ -51,6 +51,26 @@ namespace {
 
 constexpr uint32_t kLdsCapBytes = 64 * 1024;  // per 4-wave workgroup; longer reads: global scratch
 
+// Pinned host staging (hipHostMalloc), kept across calls: no page faults or
+// zero-fill per call and the uploads are DMA from page-locked memory.
+struct HostBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= cap) return hipSuccess;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    const size_t want = std::max<size_t>(bytes + bytes / 4, 4096);  // some headroom for the next chunk
+    hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+    if (e == hipSuccess) cap = want;
+    return e;
+  }
+  ~HostBuf() {
+    if (p) (void)hipHostFree(p);
+  }
+};
+
 struct DevBuf {
   void* p = nullptr;
   size_t cap = 0;
@@ -263,6 +283,7 @@ struct nt_ctx {
   int cu_count = 256;
   DevBuf planes, blk_off, len, win_off, exc_off, exc_pos, exc_code;
   DevBuf wc, start, end, dens, flags, hits, scratch, tmask, thr, queue;
+  HostBuf h_planes, h_meta;  // upload_reads staging
 };
 
 static int fail(nt_ctx* ctx, int code, const std::string& msg) {
@@ -486,6 +507,60 @@ int nt_pack_count(const char* const* seqs, const uint64_t* lens, uint64_t n_read
   return NT_OK;
 }
 
+// The planes of one read (reverse-complemented when rc): 32 bases per step
+// on runs of plain bases, per base around anything else.  Non-ACGT letters
+// are A in the planes and, when exc_pos is given, listed at exc_pos/exc_code
+// (IUPAC code, complemented under rc).  Returns the number of non-ACGT
+// letters, or -1 if one is outside DNA_ALPHABET.
+static int64_t pack_one(const unsigned char* s, uint64_t n, int rc, uint32_t* out, uint32_t* exc_pos,
+                        uint8_t* exc_code) {
+  int64_t e = 0;
+  bool bad = false;
+  for (uint64_t blk = 0; blk * 32 < n; ++blk) {
+    uint32_t lo = 0, hi = 0;
+    if (blk * 32 + 32 <= n) {  // whole block of plain bases: 32 at a time
+      // reverse complement: base i of the block is the complement of q[31 - i]
+      const unsigned char* q = rc ? s + (n - 32 - blk * 32) : s + blk * 32;
+      if (pack32(q, lo, hi)) {
+        if (rc) {
+          lo = ~__builtin_bitreverse32(lo);
+          hi = ~__builtin_bitreverse32(hi);
+        }
+        out[2 * blk] = lo;
+        out[2 * blk + 1] = hi;
+        continue;
+      }
+    }
+    for (uint32_t i = 0; i < 32 && blk * 32 + i < n; ++i) {
+      const uint64_t pos = blk * 32 + i;
+      // reverseComplement: position pos of the RC read is the complement of n-1-pos
+      const unsigned char ch = rc ? s[n - 1 - pos] : s[pos];
+      int c = base2(ch);
+      if (c < 0) {
+        uint8_t code = letter_code(ch);
+        if (!code) bad = true;
+        if (exc_pos && code) {
+          exc_pos[e] = (uint32_t)pos;
+          exc_code[e] = rc ? complement_code(code) : code;
+        }
+        ++e;
+        c = 0;  // planes hold A at exception positions
+      } else if (rc) {
+        c = 3 - c;
+      }
+      lo |= (uint32_t)(c & 1) << i;
+      hi |= (uint32_t)((c >> 1) & 1) << i;
+    }
+    out[2 * blk] = lo;
+    out[2 * blk + 1] = hi;
+  }
+  if ((n + 31) / 32 < read_blocks(n)) {  // zero the pad block of the 64-base segment
+    out[2 * ((n + 31) / 32)] = 0u;
+    out[2 * ((n + 31) / 32) + 1] = 0u;
+  }
+  return bad ? -1 : e;
+}
+
 int nt_pack_reads(const char* const* seqs, const uint64_t* lens, uint64_t n_reads, int32_t rc,
                   int32_t subseq_length, uint32_t* planes, uint64_t* blk_off, uint32_t* len,
                   uint64_t* win_off, uint32_t* exc_off, uint32_t* exc_pos, uint8_t* exc_code) {
@@ -515,53 +590,9 @@ int nt_pack_reads(const char* const* seqs, const uint64_t* lens, uint64_t n_read
   }
   std::atomic<int> bad{0};
   parallel_for(n_reads, [&](uint64_t r) {
-    const unsigned char* s = (const unsigned char*)seqs[r];
-    const uint64_t n = lens[r];
-    uint32_t* out = planes + 2 * blk_off[r];
-    uint64_t e = exc_off ? eoff[r] : 0;
-    for (uint64_t blk = 0; blk * 32 < n; ++blk) {
-      uint32_t lo = 0, hi = 0;
-      if (blk * 32 + 32 <= n) {  // whole block of plain bases: 32 at a time
-        // reverse complement: base i of the block is the complement of q[31 - i]
-        const unsigned char* q = rc ? s + (n - 32 - blk * 32) : s + blk * 32;
-        if (pack32(q, lo, hi)) {
-          if (rc) {
-            lo = ~__builtin_bitreverse32(lo);
-            hi = ~__builtin_bitreverse32(hi);
-          }
-          out[2 * blk] = lo;
-          out[2 * blk + 1] = hi;
-          continue;
-        }
-      }
-      for (uint32_t i = 0; i < 32 && blk * 32 + i < n; ++i) {
-        const uint64_t pos = blk * 32 + i;
-        // reverseComplement: position pos of the RC read is the complement of n-1-pos
-        const unsigned char ch = rc ? s[n - 1 - pos] : s[pos];
-        int c = base2(ch);
-        if (c < 0) {
-          uint8_t code = letter_code(ch);
-          if (!code || !exc_off) { bad.store(1); c = 0; }
-          else {
-            if (rc) code = complement_code(code);
-            exc_pos[e] = (uint32_t)pos;
-            exc_code[e] = code;
-            ++e;
-            c = 0;  // planes hold A at exception positions
-          }
-        } else if (rc) {
-          c = 3 - c;
-        }
-        lo |= (uint32_t)(c & 1) << i;
-        hi |= (uint32_t)((c >> 1) & 1) << i;
-      }
-      out[2 * blk] = lo;
-      out[2 * blk + 1] = hi;
-    }
-    if ((n + 31) / 32 < read_blocks(n)) {  // zero the pad block of the 64-base segment
-      out[2 * ((n + 31) / 32)] = 0u;
-      out[2 * ((n + 31) / 32) + 1] = 0u;
-    }
+    const int64_t k = pack_one((const unsigned char*)seqs[r], lens[r], rc, planes + 2 * blk_off[r],
+                               exc_off ? exc_pos + eoff[r] : nullptr, exc_off ? exc_code + eoff[r] : nullptr);
+    if (k < 0 || (k > 0 && !exc_off)) bad.store(1);
   });
   return bad.load() ? NT_E_LETTER : NT_OK;
 }
@@ -792,43 +823,85 @@ int64_t nt_kernel_times(nt_ctx* ctx, double* scan_ms, double* call_ms) {
 static int upload_reads(nt_ctx* ctx, const char* const* seqs, const uint64_t* lens, uint64_t n_reads,
                         nt_batch* B, uint64_t* max_len) {
   const int L = ctx->prog.L;
-  uint64_t tb = 0, tw = 0, te = 0, ml = 0, badr = 0;
-  int rc = nt_pack_count(seqs, lens, n_reads, L, &tb, &tw, &te, &ml, &badr);
-  if (rc == NT_E_EMPTY_READ)
-    return fail(ctx, rc, "read " + std::to_string(badr) + " is empty (seq(1, 0, by=L) errors)");
-  if (rc == NT_E_LETTER)
-    return fail(ctx, rc, "read " + std::to_string(badr) + " has a letter outside DNA_ALPHABET");
-  if (rc) return fail(ctx, rc, "nt_pack_count failed");
-  std::vector<uint32_t> h_planes(2 * tb + 2);
-  std::vector<uint64_t> h_blk(n_reads), h_win(n_reads);
-  std::vector<uint32_t> h_len(n_reads), h_eoff(te ? n_reads + 1 : 0), h_epos(te);
-  std::vector<uint8_t> h_ecode(te);
-  rc = nt_pack_reads(seqs, lens, n_reads, ctx->params.rc, L, h_planes.data(), h_blk.data(),
-                     h_len.data(), h_win.data(), te ? h_eoff.data() : nullptr,
-                     te ? h_epos.data() : nullptr, te ? h_ecode.data() : nullptr);
-  if (rc) return fail(ctx, rc, "nt_pack_reads failed");
+  if (n_reads && (!seqs || !lens)) return fail(ctx, NT_E_ARG, "null reads");
   (void)hipSetDevice(ctx->device);
   hipError_t e;
-#define NT_UP(buf, vec)                                                                      \
-  e = ctx->buf.ensure(vec.size() * sizeof(vec[0]));                                          \
+  // the staging is reused: a previous call that failed after its uploads may
+  // still be reading it (calls end synchronised otherwise, so this is free)
+  if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess) return hip_fail(ctx, e, "hipStreamSynchronize");
+  // the layout depends on the lengths only: blk_off | win_off | len straight
+  // into pinned staging, then ONE pass over the letters packs the planes
+  // (nt_pack_count + nt_pack_reads read them twice)
+  const size_t meta_bytes = n_reads * (8 + 8 + 4);
+  if ((e = ctx->h_meta.ensure(meta_bytes)) != hipSuccess) return hip_fail(ctx, e, "hipHostMalloc(meta)");
+  uint64_t* h_blk = (uint64_t*)ctx->h_meta.p;
+  uint64_t* h_win = h_blk + n_reads;
+  uint32_t* h_len = (uint32_t*)(h_win + n_reads);
+  uint64_t tb = 0, tw = 0, ml = 0;
+  for (uint64_t r = 0; r < n_reads; ++r) {
+    if (lens[r] > 0xFFFFFFFFull) return fail(ctx, NT_E_LIMIT, "read " + std::to_string(r) + " is longer than 2^32-1");
+    h_blk[r] = tb;
+    h_win[r] = tw;
+    h_len[r] = (uint32_t)lens[r];
+    tb += read_blocks(lens[r]);
+    tw += (uint64_t)window_count((int64_t)lens[r], L);
+    ml = std::max(ml, lens[r]);
+  }
+  const size_t pw = 2 * tb + 2;
+  if ((e = ctx->h_planes.ensure(pw * 4)) != hipSuccess) return hip_fail(ctx, e, "hipHostMalloc(planes)");
+  uint32_t* hp = (uint32_t*)ctx->h_planes.p;
+  hp[pw - 2] = hp[pw - 1] = 0u;
+  const int rc_flag = ctx->params.rc;
+  std::vector<int64_t> cnt(n_reads);
+  parallel_for(n_reads, [&](uint64_t r) {
+    cnt[r] = pack_one((const unsigned char*)seqs[r], lens[r], rc_flag, hp + 2 * h_blk[r], nullptr, nullptr);
+  });
+  uint64_t te = 0;
+  for (uint64_t r = 0; r < n_reads; ++r) {  // the first bad read in input order, as nt_pack_count
+    if (lens[r] == 0)
+      return fail(ctx, NT_E_EMPTY_READ, "read " + std::to_string(r) + " is empty (seq(1, 0, by=L) errors)");
+    if (cnt[r] < 0)
+      return fail(ctx, NT_E_LETTER, "read " + std::to_string(r) + " has a letter outside DNA_ALPHABET");
+    te += (uint64_t)cnt[r];
+  }
+  // reads with IUPAC letters: their exception lists (a second, rare pass)
+  std::vector<uint32_t> h_eoff(te ? n_reads + 1 : 0), h_epos(te);
+  std::vector<uint8_t> h_ecode(te);
+  if (te) {
+    if (te > 0xFFFFFFFFull) return fail(ctx, NT_E_LIMIT, "more than 2^32-1 non-ACGT letters in one call");
+    uint64_t acc = 0;
+    for (uint64_t r = 0; r < n_reads; ++r) {
+      h_eoff[r] = (uint32_t)acc;
+      acc += (uint64_t)cnt[r];
+    }
+    h_eoff[n_reads] = (uint32_t)acc;
+    parallel_for(n_reads, [&](uint64_t r) {
+      if (cnt[r] > 0)
+        pack_one((const unsigned char*)seqs[r], lens[r], rc_flag, hp + 2 * h_blk[r], h_epos.data() + h_eoff[r],
+                 h_ecode.data() + h_eoff[r]);
+    });
+  }
+#define NT_UP_PTR(buf, ptr, bytes)                                                           \
+  e = ctx->buf.ensure(bytes);                                                                \
   if (e != hipSuccess) return hip_fail(ctx, e, "hipMalloc(" #buf ")");                       \
-  if (!vec.empty()) {                                                                        \
-    e = hipMemcpyAsync(ctx->buf.p, vec.data(), vec.size() * sizeof(vec[0]),                  \
-                       hipMemcpyHostToDevice, ctx->stream);                                  \
+  if ((bytes) > 0) {                                                                         \
+    e = hipMemcpyAsync(ctx->buf.p, ptr, bytes, hipMemcpyHostToDevice, ctx->stream);          \
     if (e != hipSuccess) return hip_fail(ctx, e, "hipMemcpyAsync(" #buf ")");                \
   }
-  NT_UP(planes, h_planes);
-  NT_UP(blk_off, h_blk);
-  NT_UP(len, h_len);
-  NT_UP(win_off, h_win);
+#define NT_UP(buf, vec) NT_UP_PTR(buf, vec.data(), vec.size() * sizeof(vec[0]))
+  NT_UP_PTR(planes, hp, pw * 4);
+  NT_UP_PTR(blk_off, h_blk, n_reads * 8);
+  NT_UP_PTR(len, h_len, n_reads * 4);
+  NT_UP_PTR(win_off, h_win, n_reads * 8);
   if (te) {
     NT_UP(exc_off, h_eoff);
     NT_UP(exc_pos, h_epos);
     NT_UP(exc_code, h_ecode);
+    // the exception lists are pageable vectors: finish their copies before they go
+    if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess) return hip_fail(ctx, e, "hipStreamSynchronize");
   }
 #undef NT_UP
-  // the staging vectors are pageable: finish the copies before they go
-  if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess) return hip_fail(ctx, e, "hipStreamSynchronize");
+#undef NT_UP_PTR
   *B = nt_batch{(const uint32_t*)ctx->planes.p, (const uint64_t*)ctx->blk_off.p,
                 (const uint32_t*)ctx->len.p, (const uint64_t*)ctx->win_off.p,
                 te ? (const uint32_t*)ctx->exc_off.p : nullptr,
