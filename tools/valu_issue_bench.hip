@@ -58,6 +58,14 @@ __global__ void __launch_bounds__(256) kern(uint32_t* out, uint32_t seed) {
   if constexpr (KIND == 26) asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x80\n\tv_lshrrev_b32 %0, 3, %0" : "+v"(r[i]) : "v"(b), "v"(c));
     X16(OP)
 #undef OP
+    if constexpr (KIND == 27) {  // KIND 24's instructions, the slow ones clustered: 16 x 7 fast, then 16 alignbit
+#define OPF(i) asm volatile("v_and_b32 %0, %1, %0\n\tv_xor_b32 %0, %2, %0\n\tv_or_b32 %0, %1, %0\n\tv_and_b32 %0, %2, %0\n\tv_xor_b32 %0, %1, %0\n\tv_or_b32 %0, %2, %0\n\tv_add_u32 %0, %1, %0" : "+v"(r[i]) : "v"(b), "v"(c));
+#define OPS(i) asm volatile("v_alignbit_b32 %0, %1, %0, 3" : "+v"(r[i]) : "v"(b));
+      X16(OPF)
+      X16(OPS)
+#undef OPF
+#undef OPS
+    }
   }
   uint32_t acc = 0;
 #pragma unroll
@@ -72,7 +80,7 @@ static const char* kNames[] = {"v_and_b32 (VOP2)",     "v_bitop3_b32 (VOP3)",  "
                                "v_or_b32 (VOP2)", "v_cndmask_b32 (VOP2)", "v_lshlrev_b64", "v_or3_b32",
                                "v_and_or_b32", "v_lshrrev_b32 (VOP2)", "v_alignbyte_b32", "2 v_and + v_alignbit",
                                "v_xor_b32", "v_not_b32 (VOP1)", "3 fast (and xor or)", "3 fast + alignbit",
-                               "7 fast + alignbit", "waves: alignbit | and", "bitop3 + lshrrev"};
+                               "7 fast + alignbit", "waves: alignbit | and", "bitop3 + lshrrev", "7 fast x16, then alignbit x16"};
 
 template <int KIND>
 static void run(int cus, uint32_t* out, int wps) {
@@ -87,7 +95,7 @@ static void run(int cus, uint32_t* out, int wps) {
   (void)hipEventSynchronize(b);
   float ms = 0.f;
   (void)hipEventElapsedTime(&ms, a, b);
-  const double per = KIND == 9 || KIND == 26 ? 2.0 : (KIND == 19 || KIND == 22 ? 3.0 : (KIND == 23 ? 4.0 : (KIND == 24 ? 8.0 : 1.0)));
+  const double per = KIND == 9 || KIND == 26 ? 2.0 : (KIND == 19 || KIND == 22 ? 3.0 : (KIND == 23 ? 4.0 : (KIND == 24 || KIND == 27 ? 8.0 : 1.0)));
   const double instr_per_simd = (double)wps * 16.0 * ITER * per;
   const double cyc = ms * 1e-3 * 2.4e9;
   printf("%-24s waves/SIMD %d  %8.3f ms  %.3f wave-instr/cycle/SIMD\n", kNames[KIND], wps, ms, instr_per_simd / cyc);
@@ -104,7 +112,7 @@ int main(int argc, char** argv) {
 #define RUN(k) \
   if (only < 0 || only == k) run<k>(cus, out, wps);
   RUN(0) RUN(1) RUN(2) RUN(3) RUN(4) RUN(5) RUN(6) RUN(7) RUN(8) RUN(9) RUN(10) RUN(11) RUN(12) RUN(13)
-  RUN(14) RUN(15) RUN(16) RUN(17) RUN(18) RUN(19) RUN(20) RUN(21) RUN(22) RUN(23) RUN(24) RUN(25) RUN(26)
+  RUN(14) RUN(15) RUN(16) RUN(17) RUN(18) RUN(19) RUN(20) RUN(21) RUN(22) RUN(23) RUN(24) RUN(25) RUN(26) RUN(27)
   (void)hipFree(out);
   return 0;
 }
