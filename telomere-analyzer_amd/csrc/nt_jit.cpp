@@ -114,7 +114,11 @@ bool compile(int device, const std::string& src, JitEntry& e) {
       }
     }
   }
-  std::vector<const char*> opts = {arch.c_str(), "-O3", "-std=c++17", "-ffp-contract=off"};
+  // max-ilp machine scheduling: scan 3.41 -> 3.37 ms at 1M x 50 kb (c4 -0.8 %, c10k
+  // unchanged; tools/jit_sweep.sh); it orders the VALU stream with fewer slow/fast
+  // alternations
+  std::vector<const char*> opts = {arch.c_str(), "-O3", "-std=c++17", "-ffp-contract=off", "-mllvm",
+                                   "-amdgpu-sched-strategy=max-ilp"};
   for (const std::string& x : extra) opts.push_back(x.c_str());
   const hiprtcResult rc = hiprtcCompileProgram(prog, (int)opts.size(), opts.data());
   if (rc != HIPRTC_SUCCESS) {

@@ -582,6 +582,9 @@ __device__ __forceinline__ void scan_chunk(const NtProgram* __restrict__ prog, c
 #endif
 constexpr int kRing = NT_RING;  // prefetch depth in chunks (tuning knob)
 
+#ifndef NT_WOFF_UNIFORM
+#define NT_WOFF_UNIFORM 0  // tuning knob (c10k 2 % slower with it)
+#endif
 struct ReadMeta {
   uint32_t len;
   uint64_t boff, woff;  // block offset (uniform), window offset
@@ -603,7 +606,11 @@ __device__ __forceinline__ ReadMeta load_meta(const NtBatch& B, uint64_t r) {
   ReadMeta m;
   m.len = B.len[r];
   m.boff = uniform_u64(B.blk_off[r]);  // uniform: SGPR base
+#if NT_WOFF_UNIFORM
+  m.woff = uniform_u64(B.win_off[r]);  // uniform: SGPR bases of the window outputs
+#else
   m.woff = B.win_off[r];
+#endif
   m.e0 = m.e1 = 0u;
   if (B.exc_off) {
     m.e0 = B.exc_off[r];
@@ -817,11 +824,14 @@ __device__ __forceinline__ void scan_reads(const NtProgram* __restrict__ prog,
       if (np == 3 && dbg_ok(dbg, 2, ab + (uint64_t)(np * nmw) + (uint64_t)(2 * nck + j) / 2, r))
         cko[2 * nck + j] = nw == 0 ? 0u : cum2[i];
     }
+    // 64 windows per step: counts from the running sums (one ds_read2 per
+    // lane), the u16 count stores and one ballot per pass against the full-width
+    // threshold; the last window (wider) is re-tested once after its step.
     for (int ch = 0; ch < nmw; ++ch) {
       const int i = ch * 64 + lane;
-      const uint32_t tw = i == nw - 1 ? thr_last : thr_full;
+      const bool ok = i < nw;
       uint32_t c0 = 0u, c1 = 0u, c2 = 0u;
-      if (i < nw) {
+      if (ok) {
         const uint2 a0 = cum01[i], a1 = cum01[i + 1];
         c0 = a1.x - a0.x;
         c1 = a1.y - a0.y;
@@ -834,8 +844,22 @@ __device__ __forceinline__ void scan_reads(const NtProgram* __restrict__ prog,
           if (dbg_ok(dbg, 1, m.woff * np + (uint64_t)(2 * nw + i), r)) wout[2 * nw + i] = (uint16_t)c2;
         }
       }
-      const uint64_t b0 = __ballot(i < nw && c0 >= tw), b1 = __ballot(i < nw && c1 >= tw);
-      const uint64_t b2 = np == 3 ? __ballot(i < nw && c2 >= tw) : 0ull;
+      // (counts are 0 past the read's windows; the mask only matters for a zero threshold)
+      const uint64_t okm = __ballot(ok);
+      uint64_t b0 = __ballot(c0 >= thr_full) & okm, b1 = __ballot(c1 >= thr_full) & okm;
+      uint64_t b2 = np == 3 ? __ballot(c2 >= thr_full) & okm : 0ull;
+      if (ch == nmw - 1 && thr_last != thr_full) {  // the last window: its own width's threshold
+        const int ll = (nw - 1) & 63;
+        const uint64_t bit = 1ull << ll;
+        const uint32_t l0 = (uint32_t)__builtin_amdgcn_readlane((int)c0, ll);
+        const uint32_t l1 = (uint32_t)__builtin_amdgcn_readlane((int)c1, ll);
+        b0 = (b0 & ~bit) | (l0 >= thr_last ? bit : 0ull);
+        b1 = (b1 & ~bit) | (l1 >= thr_last ? bit : 0ull);
+        if (np == 3) {
+          const uint32_t l2 = (uint32_t)__builtin_amdgcn_readlane((int)c2, ll);
+          b2 = (b2 & ~bit) | (l2 >= thr_last ? bit : 0ull);
+        }
+      }
       if (lane == 0 && dbg_ok(dbg, 2, ab + (uint64_t)((np - 1) * nmw + ch), r)) {
         tmo[ch] = b0;
         tmo[nmw + ch] = b1;
