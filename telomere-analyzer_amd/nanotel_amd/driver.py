@@ -182,6 +182,10 @@ def run(input_path, save_path, patterns, fmt="fastq", nrec=10000, rc=False, min_
     dist_on = dist.is_available() and dist.is_initialized()
     rank = dist.get_rank() if dist_on else 0
     world = dist.get_world_size() if dist_on else 1
+    coll_dev = None  # RCCL (backend "nccl") reduces device tensors; gloo CPU ones
+    if dist_on and world > 1 and dist.get_backend() == "nccl":
+        import torch
+        coll_dev = torch.device("cuda", torch.cuda.current_device())
     os.makedirs(save_path, exist_ok=True)
     reads_dir = os.path.join(save_path, "reads")
     os.makedirs(reads_dir, exist_ok=True)
@@ -220,7 +224,7 @@ def run(input_path, save_path, patterns, fmt="fastq", nrec=10000, rc=False, min_
                 own = (r,) + _scan_chunk(nt, ch, use_filter, write_reads, log, want_windows=plot)
         if n_round == 0:
             break
-        maxima = shard.exchange_rel_max({own[0]: own[3]} if own else {}, n_round)
+        maxima = shard.exchange_rel_max({own[0]: own[3]} if own else {}, n_round, device=coll_dev)
         starts = np.empty(n_round, np.float64)
         for r in range(n_round):  # the reference's recurrence, chunk by chunk
             starts[r], s_next, m_run = shard.advance(s_next, m_run, float(maxima[r]))
