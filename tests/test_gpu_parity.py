@@ -153,6 +153,24 @@ def test_long_reads_global_scratch_path(jit):
         compare(nt, res, oracle_rows(seqs, pats, tvr=tvr))
 
 
+@pytest.mark.parametrize("right", [False, True], ids=["left_edge", "right_edge"])
+def test_reads_with_9_to_16_bitmask_words(right):
+    # the calling kernel copies a pass's telomeric-window bitmask to LDS when
+    # it has <= 16 words (<= 1,024 windows): reads of 513-1,024 windows, around
+    # the 512 / 1,024 boundaries, tracts at the left, right and inside
+    rng = np.random.default_rng(21 + int(right))
+    motif = "CCCTAA" if right else "TTAGGG"
+    seqs = []
+    for i, n in enumerate([51249, 51250, 51300, 64001, 77777, 90000, 102399, 102400, 102449, 102450,
+                           60000, 99000]):
+        seqs.append(_telo_read(rng, n, motif=motif, where=["left", "right", "mid"][i % 3], tract=(2000, 15000)))
+    for tvr in (None, "TTGGGG"):
+        nt = _nt(patterns=motif, tvr_patterns=tvr, check_right_edge=right)
+        res = nt.analyze(seqs, want_windows=True, want_hits=True)
+        compare(nt, res, oracle_rows(seqs, motif, tvr=tvr, right_edge=right))
+        assert res["telomeric"].sum() > 0
+
+
 def test_error_behaviour():
     from nanotel_amd import NanoTelError
     nt = _nt(patterns="CCCTAA", check_right_edge=True)
