@@ -66,7 +66,10 @@ struct Pos {
 #ifndef NT_CALL_TM_LDS
 #define NT_CALL_TM_LDS 1
 #endif
-constexpr int kTmRegs = NT_CALL_TM_LDS ? 16 : 8;  // bitmask words held per lane
+#ifndef NT_CALL_TM_WORDS
+#define NT_CALL_TM_WORDS 16
+#endif
+constexpr int kTmRegs = NT_CALL_TM_LDS ? NT_CALL_TM_WORDS : 8;  // bitmask words held per lane
 
 // Per-lane state of one read-pass.
 struct Lane {
@@ -79,6 +82,7 @@ struct Lane {
   int k;         // 0 for P1, 1 for P2/P3
   bool use_tvr;  // P3
   bool raw;      // P1 raw views (single fixed pattern, NanoTel.R:349-355)
+  uint32_t* pws;  // NT_CALL_PW_LDS: this lane's edge-extension plane words in LDS
   bool tm_reg;   // tmw holds tm[0 .. nmw)
 #if NT_CALL_TM_LDS
   uint64_t* tmw;  // this lane's words in LDS, stride 256 (word-major: conflict-free at equal word)
@@ -473,10 +477,13 @@ __device__ __forceinline__ Pos find_right_telo(const Lane& c, bool& err) {
 // and get_accurate_end (NanoTel.R:1692-1721) only ranges in [e-100, e+49]
 // (0-based; the offsets are hard-coded in the reference), so each is one
 // neighbourhood, [s-42, s+118) and [e-102, e+58); both fetched in one batch.
-__device__ __forceinline__ void accurate_both(const Lane& c, int s, int e, int& s_acc, int& e_acc) {
-  NbBlocks<5> fs, fe;
+__device__ __forceinline__ void accurate_fetch(const Lane& c, int s, int e, NbBlocks<5>& fs, NbBlocks<5>& fe) {
   nb_fetch(c, s - 42, fs);
   nb_fetch(c, e - 102, fe);
+}
+
+__device__ __forceinline__ void accurate_both(const Lane& c, int s, int e, const NbBlocks<5>& fs,
+                                              const NbBlocks<5>& fe, int& s_acc, int& e_acc) {
   s_acc = -1;
   e_acc = -1;
   if (s != -1) {
@@ -508,16 +515,39 @@ __device__ __forceinline__ void accurate_both(const Lane& c, int s, int e, int& 
 // The four steps of one side of the edge extension match at bases within 33
 // (right) / 27 (left) of the lowest one, each over 64 positions, so one batch
 // of K = 5 block loads per side from the lowest base serves all of them.
+#ifndef NT_CALL_PW_LDS
+#define NT_CALL_PW_LDS 0  // measured +-0 (edge-extension words in LDS)
+#endif
+#ifndef NT_CALL_ACC_EARLY
+#define NT_CALL_ACC_EARLY 0  // measured 1 % slower (0.559 vs 0.553 ms at c50k)
+#endif
 template <int K>
 struct Pw {
   int q0;
+#if NT_CALL_PW_LDS
+  uint32_t* s;  // this lane's 2K words in LDS (L then H), stride 256
+#else
   uint32_t L[K], H[K];
+#endif
 };
 
 template <int K>
 __device__ __forceinline__ void pw_load(const Lane& c, int q0, Pw<K>& w) {
   w.q0 = q0;
   const int b0 = q0 >> 5;
+#if NT_CALL_PW_LDS
+  uint2 x[K];
+#pragma unroll
+  for (int i = 0; i < K; ++i) {
+    const int b = b0 + i;
+    x[i] = (b >= 0 && b < c.rc.nblk) ? c.rc.blk[b] : make_uint2(0u, 0u);
+  }
+#pragma unroll
+  for (int i = 0; i < K; ++i) {
+    w.s[i * 256] = x[i].x;
+    w.s[(K + i) * 256] = x[i].y;
+  }
+#else
 #pragma unroll
   for (int i = 0; i < K; ++i) {
     const int b = b0 + i;
@@ -525,6 +555,7 @@ __device__ __forceinline__ void pw_load(const Lane& c, int q0, Pw<K>& w) {
     w.L[i] = x.x;
     w.H[i] = x.y;
   }
+#endif
 }
 
 // planes of [p, p + 31] (as plane_at), from the window when it holds them
@@ -536,6 +567,10 @@ __device__ __forceinline__ void pw_at(const Lane& c, const Pw<K>& w, int p, uint
     plane_at(c.rc, p, L, H);
     return;
   }
+#if NT_CALL_PW_LDS
+  const uint32_t l0 = w.s[i * 256], l1 = w.s[(i + 1) * 256];
+  const uint32_t h0 = w.s[(K + i) * 256], h1 = w.s[(K + i + 1) * 256];
+#else
   uint32_t l0 = w.L[0], h0 = w.H[0], l1 = w.L[1], h1 = w.H[1];
 #pragma unroll
   for (int t = 1; t + 1 < K; ++t)
@@ -545,6 +580,7 @@ __device__ __forceinline__ void pw_at(const Lane& c, const Pw<K>& w, int p, uint
       l1 = w.L[t + 1];
       h1 = w.H[t + 1];
     }
+#endif
   const uint32_t sh = (uint32_t)(d & 31);
   L = funnel(l1, l0, sh);
   H = funnel(h1, h0, sh);
@@ -630,23 +666,32 @@ __device__ __forceinline__ int search_left(const Lane& c, const Pw<K>& w, int st
 __device__ __forceinline__ void call_pass(Lane& c, int& out_s, int& out_e, double& out_d, uint32_t& err) {
   tm_preload(c);
   Pos tp = find_telo_position(c, 3, 2.0);
+#ifndef NT_DBG_NO_ACC
+  // get_accurate_* neighbourhoods fetched with the wrapper's density loads
+  // (one memory round trip less); refetched if the wrapper re-runs the call
+  NbBlocks<5> fs, fe;
+  if (NT_CALL_ACC_EARLY) accurate_fetch(c, tp.s, tp.e, fs, fe);
+#endif
 #ifdef NT_DBG_NO_WRAP
   const double telo_density = 1.0;
 #else
   const double telo_density = sub_density(c, tp.s, tp.e);
 #endif
   const int num_rows = (tp.e - tp.s + 1) / c.L;
+  bool refetch = !NT_CALL_ACC_EARLY;
   if (telo_density < 0.85 && num_rows > 5) {
     const int min_rows = num_rows <= 7 ? num_rows - 2 : 7;
     const double min_density = 0.6 * (double)min_rows;
     tp = find_telo_position(c, min_rows, min_density);
+    refetch = true;
   }
 #ifdef NT_DBG_NO_ACC  // timing experiments only (wrong results)
   const int s_acc = tp.s;
   int e_acc = tp.e;
 #else
+  if (refetch) accurate_fetch(c, tp.s, tp.e, fs, fe);
   int s_acc, e_acc;
-  accurate_both(c, tp.s, tp.e, s_acc, e_acc);
+  accurate_both(c, tp.s, tp.e, fs, fe, s_acc, e_acc);
 #endif
   if (s_acc > e_acc) e_acc = s_acc;
   tp = Pos{s_acc, e_acc};
@@ -667,6 +712,10 @@ __device__ __forceinline__ void call_pass(Lane& c, int& out_s, int& out_e, doubl
     // both sides' plane windows in one batch, then the step walks in registers
     const int ei = tp.e + 1, si = tp.s - 1;
     Pw<5> wr, wl;
+#if NT_CALL_PW_LDS
+    wr.s = c.pws;
+    wl.s = c.pws + 10 * 256;
+#endif
     pw_load(c, (max(min(ei + 18, c.n) - 17, 1) - 2) & ~31, wr);
     pw_load(c, (max(si - 45, 1) - 2) & ~31, wl);
     int e2 = tp.e, s2 = tp.s;
@@ -704,6 +753,9 @@ nt_call_kernel(const NtProgram* __restrict__ prog, NtBatch B, NtOut O,
 #if NT_CALL_TM_LDS
   __shared__ uint64_t tm_lds[kTmRegs * 256];
 #endif
+#if NT_CALL_PW_LDS
+  __shared__ uint32_t pw_lds[20 * 256];
+#endif
   const int lg = np <= 2 ? 1 : 2;  // log2(G)
   const uint64_t total = B.n_reads << lg;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -724,6 +776,9 @@ nt_call_kernel(const NtProgram* __restrict__ prog, NtBatch B, NtOut O,
         Lane c;
 #if NT_CALL_TM_LDS
         c.tmw = tm_lds + threadIdx.x;
+#endif
+#if NT_CALL_PW_LDS
+        c.pws = pw_lds + threadIdx.x;
 #endif
         c.rc.n = n32;
         c.rc.nblk = (int32_t)((n32 + 31u) >> 5);
