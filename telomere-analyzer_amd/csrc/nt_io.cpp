@@ -13,22 +13,124 @@
 //    lines skipped); FASTQ: 4-line records '@name', sequence, '+...', quality
 //    (quality dropped);
 //  * letters are kept as they are: validation against DNA_ALPHABET happens in
-//    nt_pack_count (NT_E_LETTER), as readDNAStringSet would fail.
+//    nt_pack_count (NT_E_LETTER), as readDNAStringSet would fail;
+//  * a multi-file input (a run directory of fastq.gz parts) is inflated by a
+//    few worker threads, files ahead of the parser, each into memory (zlib
+//    inflates one stream on one core; the parts are independent), and parsed
+//    in order from there.  A single file is streamed.
 #include <dirent.h>
 #include <sys/stat.h>
 #include <zlib.h>
 
 #include <algorithm>
+#include <condition_variable>
+#include <cstdlib>
 #include <cstring>
+#include <memory>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "nanotel.h"
+
+// zlib reports a truncated stream as end of file plus an error state
+static bool gz_failed(gzFile g) {
+  int e = Z_OK;
+  gzerror(g, &e);
+  return e != Z_OK && e != Z_STREAM_END;
+}
+
+// Whole-file inflation of the next files of a multi-file input, ahead of the
+// parser: worker threads take files in order, at most `window` beyond the one
+// being parsed; the parser waits for its file's buffer.
+struct Prefetcher {
+  struct Slot {
+    bool done = false;
+    std::string err;
+    std::vector<char> data;
+  };
+  const std::vector<std::string>* files = nullptr;
+  std::vector<Slot> slots;
+  size_t next = 0, consumed = 0, window = 1;
+  bool stop = false;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<std::thread> workers;
+
+  void start(const std::vector<std::string>& f, unsigned n_threads) {
+    files = &f;
+    slots.resize(f.size());
+    window = n_threads;
+    for (unsigned t = 0; t < n_threads; ++t) workers.emplace_back([this] { run(); });
+  }
+  void run() {
+    for (;;) {
+      size_t i;
+      {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return stop || (next < files->size() && next < consumed + window); });
+        if (stop) return;
+        i = next++;
+      }
+      Slot sl;
+      gzFile g = gzopen((*files)[i].c_str(), "rb");
+      if (!g) {
+        sl.err = "cannot open " + (*files)[i];
+      } else {
+        gzbuffer(g, 1 << 20);
+        size_t used = 0;
+        for (;;) {
+          if (sl.data.size() - used < (4u << 20)) sl.data.resize(std::max<size_t>(8u << 20, sl.data.size() * 2));
+          const int n = gzread(g, sl.data.data() + used, (unsigned)std::min<size_t>(sl.data.size() - used, 1u << 30));
+          if (n < 0 || (n == 0 && gz_failed(g))) {
+            sl.err = "read error in " + (*files)[i];
+            break;
+          }
+          if (n == 0) break;
+          used += (size_t)n;
+        }
+        sl.data.resize(used);
+        gzclose(g);
+      }
+      sl.done = true;
+      {
+        std::lock_guard<std::mutex> lk(mu);
+        slots[i] = std::move(sl);
+      }
+      cv.notify_all();
+    }
+  }
+  // the inflated file i (waits for it); releases the window for one more file
+  bool take(size_t i, std::vector<char>& out, std::string& err) {
+    std::unique_lock<std::mutex> lk(mu);
+    consumed = i + 1;
+    cv.notify_all();
+    cv.wait(lk, [&] { return slots[i].done; });
+    if (!slots[i].err.empty()) {
+      err = slots[i].err;
+      return false;
+    }
+    out.swap(slots[i].data);
+    std::vector<char>().swap(slots[i].data);
+    return true;
+  }
+  ~Prefetcher() {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      stop = true;
+    }
+    cv.notify_all();
+    for (auto& t : workers) t.join();
+  }
+};
 
 struct nt_reader {
   std::vector<std::string> files;
   size_t file_idx = 0;
   gzFile gz = nullptr;
+  bool active = false;  // a file is open (streamed through gz, or inflated in buf)
+  std::unique_ptr<Prefetcher> pf;
   int format = 0;  // 0 fasta, 1 fastq
   std::vector<char> buf;
   size_t pos = 0, end = 0;
@@ -74,15 +176,26 @@ bool open_next(nt_reader* r) {
     gzclose(r->gz);
     r->gz = nullptr;
   }
-  if (r->file_idx >= r->files.size()) return false;
+  r->active = false;
+  if (!r->err.empty() || r->file_idx >= r->files.size()) return false;
+  if (r->pf) {  // inflated ahead by the workers: parse straight from memory
+    if (!r->pf->take(r->file_idx++, r->buf, r->err)) return false;
+    r->pos = 0;
+    r->end = r->buf.size();
+    r->eof_file = true;
+    r->active = true;
+    return true;
+  }
   r->gz = gzopen(r->files[r->file_idx++].c_str(), "rb");
   if (!r->gz) {
     r->err = "cannot open " + r->files[r->file_idx - 1];
     return false;
   }
   gzbuffer(r->gz, 1 << 20);
+  if (r->buf.size() != (1u << 20)) std::vector<char>(1 << 20).swap(r->buf);
   r->pos = r->end = 0;
   r->eof_file = false;
+  r->active = true;
   return true;
 }
 
@@ -90,7 +203,7 @@ bool open_next(nt_reader* r) {
 // (nullptr: skipped, e.g. FASTQ qualities); false at end of file.  Returns the
 // line length through `len`.
 bool take_line(nt_reader* r, std::string* out, size_t* len = nullptr) {
-  if (!r->gz) return false;
+  if (!r->active) return false;
   const size_t base = out ? out->size() : 0;
   size_t n_line = 0;
   bool any = false;
@@ -98,6 +211,8 @@ bool take_line(nt_reader* r, std::string* out, size_t* len = nullptr) {
     if (r->pos == r->end) {
       if (r->eof_file) break;
       const int n = gzread(r->gz, r->buf.data(), (unsigned)r->buf.size());
+      if (n < 0 || (n == 0 && gz_failed(r->gz)))  // corrupt or truncated gzip stream
+        r->err = "read error in " + r->files[r->file_idx - 1];
       if (n <= 0) {
         r->eof_file = true;
         break;
@@ -235,6 +350,15 @@ int nt_reader_open(const char* path, int format, nt_reader** out) {
   }
   r->format = format;
   r->buf.resize(1 << 20);
+  if (r->files.size() > 1) {  // a run directory: inflate parts ahead on worker threads
+    unsigned nt = std::thread::hardware_concurrency();
+    nt = std::max(1u, std::min(nt == 0 ? 1u : nt, 16u));
+    if (const char* v = std::getenv("NT_READER_THREADS")) nt = (unsigned)std::max(0, atoi(v));
+    if (nt > 0) {
+      r->pf.reset(new Prefetcher());
+      r->pf->start(r->files, nt);
+    }
+  }
   *out = r;
   return NT_OK;
 }
@@ -264,7 +388,7 @@ int64_t nt_reader_next(nt_reader* r, uint64_t nrec, const char* const** names,
   r->c().seq_off.clear();
   r->c().name_len.clear();
   r->c().seq_len.clear();
-  if (!r->gz && r->file_idx == 0 && !open_next(r)) return r->err.empty() ? 0 : NT_E_ARG;
+  if (!r->active && r->file_idx == 0 && !open_next(r)) return r->err.empty() ? 0 : NT_E_ARG;
   std::string name, seq;
   while (r->c().name_len.size() < nrec) {
     r->seq_direct = false;

@@ -75,6 +75,40 @@ def test_reader_fastq_gz_directory_stream(tmp_path):
         assert sum(got, []) == recs
 
 
+@pytest.mark.parametrize("threads", ["0", "1", "3", None])
+def test_reader_run_directory_inflated_ahead(tmp_path, monkeypatch, threads):
+    """A run directory of many fastq.gz parts (the multi-file input is inflated
+    ahead on worker threads, NT_READER_THREADS; 0 = streamed): the same record
+    stream for every thread count, chunks spanning parts, an empty part, a
+    FASTA directory, and a broken part reported as an error."""
+    if threads is None:
+        monkeypatch.delenv("NT_READER_THREADS", raising=False)
+    else:
+        monkeypatch.setenv("NT_READER_THREADS", threads)
+    rng = np.random.default_rng(5)
+    recs = [(f"r{i} ch={i}", "".join(rng.choice(list("ACGT"), int(rng.integers(1, 2000))))) for i in range(60)]
+    d = tmp_path / "run"
+    d.mkdir()
+    cuts = [0, 7, 7, 20, 33, 34, 50, 60]  # part 1 is empty
+    for k in range(len(cuts) - 1):
+        _write_fastq(d / f"part_{k:02d}.fastq.gz", recs[cuts[k]:cuts[k + 1]], gz=True)
+    for nrec in (1, 6, 13, 1000):
+        got = _chunks(str(d), "fastq", nrec)
+        assert [len(c) for c in got] == [min(nrec, 60 - i) for i in range(0, 60, nrec)]
+        assert sum(got, []) == recs
+    fa = tmp_path / "fa"
+    fa.mkdir()
+    for k in range(3):
+        with gzip.open(fa / f"p{k}.fa.gz", "wt") as f:
+            for n, s in recs[20 * k:20 * k + 20]:
+                f.write(f">{n}\n" + "\n".join(s[i:i + 80] for i in range(0, len(s), 80)) + "\n")
+    assert sum(_chunks(str(fa), "fasta", 9), []) == recs
+    (d / "part_99.fastq.gz").write_bytes(b"\x1f\x8b\x08\x00garbage")
+    from nanotel_amd import NanoTelError
+    with pytest.raises(NanoTelError):
+        _chunks(str(d), "fastq", 1000)
+
+
 def test_reader_fasta_wrapped_blank_lines(tmp_path):
     p = tmp_path / "x.fa.gz"
     with gzip.open(p, "wt") as f:

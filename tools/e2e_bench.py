@@ -10,7 +10,7 @@ numpy, then the driver runs over them with NanoTel's default nrec (10,000) unles
 Timed without and with the per-read reads/<serial>.fasta.gz writes, and with
 --plots also with the three single-read plots per telomeric read.
 
-    python tools/e2e_bench.py [--reads 8000] [--read_len 50000] [--nrec 10000] [--gz] [--plots] [--dir /tmp/e2e]
+    python tools/e2e_bench.py [--reads 8000] [--read_len 50000] [--nrec 10000] [--gz] [--parts 1] [--plots] [--dir /tmp/e2e]
 """
 import argparse
 import gzip
@@ -25,22 +25,33 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "telomere-analyzer_amd"))
 
 
-def write_input(path, n, L, gz, seed=20260501):
+def write_input(path, n, L, gz, seed=20260501, parts=1):
+    """One file, or with parts > 1 a run directory of `parts` files (as a
+    sequencer writes them: fastq_pass/part_000.fastq.gz, ...)."""
     rng = np.random.default_rng(seed)
     acgt = np.frombuffer(b"ACGT", np.uint8)
     unit = np.frombuffer(b"TTAGGG", np.uint8)
-    op = gzip.open if gz else open
-    with op(path, "wb") as f:
-        for r in range(n):
-            s = acgt[rng.integers(0, 4, L)]
-            if rng.random() < 0.5:
-                t = min(L, int(rng.integers(1000, 15001)))
-                tract = np.resize(unit, t)
-                sub = rng.random(t) < 0.02
-                tract[sub] = acgt[rng.integers(0, 4, int(sub.sum()))]
-                s[:t] = tract
-            q = b"I" * L
-            f.write(b"@read_%d\n" % r + s.tobytes() + b"\n+\n" + q + b"\n")
+    if parts > 1:
+        os.makedirs(path, exist_ok=True)
+        names = [os.path.join(path, "part_%03d.fastq%s" % (k, ".gz" if gz else "")) for k in range(parts)]
+    else:
+        names = [path]
+    per = (n + len(names) - 1) // len(names)
+    r = 0
+    for name in names:
+        op = (lambda p, m: gzip.open(p, m, compresslevel=1)) if gz else open
+        with op(name, "wb") as f:
+            for _ in range(min(per, n - r)):
+                s = acgt[rng.integers(0, 4, L)]
+                if rng.random() < 0.5:
+                    t = min(L, int(rng.integers(1000, 15001)))
+                    tract = np.resize(unit, t)
+                    sub = rng.random(t) < 0.02
+                    tract[sub] = acgt[rng.integers(0, 4, int(sub.sum()))]
+                    s[:t] = tract
+                q = b"I" * L
+                f.write(b"@read_%d\n" % r + s.tobytes() + b"\n+\n" + q + b"\n")
+                r += 1
 
 
 def main():
@@ -50,17 +61,20 @@ def main():
     ap.add_argument("--nrec", type=int, default=10000)
     ap.add_argument("--gz", action="store_true")
     ap.add_argument("--plots", action="store_true", help="also time a run with the single-read plots")
+    ap.add_argument("--parts", type=int, default=1, help="write the input as a directory of this many files")
     ap.add_argument("--dir", default="/tmp/nt_e2e")
     a = ap.parse_args()
     os.makedirs(a.dir, exist_ok=True)
-    inp = os.path.join(a.dir, "reads.fastq" + (".gz" if a.gz else ""))
+    inp = os.path.join(a.dir, "run" if a.parts > 1 else "reads.fastq" + (".gz" if a.gz else ""))
     t = time.perf_counter()
-    write_input(inp, a.reads, a.read_len, a.gz)
+    write_input(inp, a.reads, a.read_len, a.gz, parts=a.parts)
     gen_s = time.perf_counter() - t
     from nanotel_amd import driver
     bases = a.reads * a.read_len
-    out = {"input": os.path.basename(inp), "reads": a.reads, "nrec": a.nrec, "read_len": a.read_len, "bases": bases,
-           "input_bytes": os.path.getsize(inp), "generate_s": round(gen_s, 2)}
+    size = (sum(os.path.getsize(os.path.join(inp, f)) for f in os.listdir(inp)) if os.path.isdir(inp)
+            else os.path.getsize(inp))
+    out = {"input": os.path.basename(inp), "parts": a.parts, "gz": a.gz, "reads": a.reads, "nrec": a.nrec,
+           "read_len": a.read_len, "bases": bases, "input_bytes": size, "generate_s": round(gen_s, 2)}
     # warm-up (hiprtc specialisation, device buffers) on a small prefix-free run
     driver.run(inp, os.path.join(a.dir, "warm"), "TTAGGG", fmt="fastq", nrec=10000, write_reads=False,
                plot=False, log=lambda *x: None)
