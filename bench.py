@@ -40,6 +40,10 @@ CONFIGS = {
     # BASELINE.json configs[3]
     "c4": dict(reads=10_000_000, read_len=50_000, patterns="TTAGGG TCAGGG", tvr="TGAGGG TTGGGG", rc=False,
                variant=0.05, desc="10M synthetic 50 kb reads / GPU, TTAGGG TCAGGG + TVR TGAGGG TTGGGG, P1+P2+P3"),
+    # BASELINE.json configs[4]: 100M x 50 kb over 8 GPUs = 12.5M reads (625 Gbases,
+    # 156 GB of planes) resident per GPU, one launch per step
+    "c5": dict(reads=12_500_000, read_len=50_000, patterns="TTAGGG", tvr=None, rc=False, variant=0.0,
+               desc="12.5M synthetic 50 kb reads / GPU (100M over 8 GPUs), TTAGGG, P1 + P2"),
 }
 
 METRICS = {
@@ -47,6 +51,7 @@ METRICS = {
     "c10k": "Gbases/s scanned (TTAGGG, 10 kb reads)",
     "c3": "Gbases/s scanned (YYAGGG --rc, 50 kb reads)",
     "c4": "Gbases/s scanned (multi-pattern + TVR + 1-mismatch, 50 kb reads)",
+    "c5": "Gbases/s scanned (TTAGGG, 50 kb reads)",
 }
 
 
