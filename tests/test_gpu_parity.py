@@ -95,6 +95,23 @@ def test_synthetic_generator_reads():
 
 
 @pytest.mark.parametrize("cfg", [
+    dict(read_len=10000, patterns="TTAGGG", tvr=None, rc=False, variant=0.0),  # BASELINE configs[1]
+    dict(read_len=50000, patterns="YYAGGG", tvr=None, rc=True, variant=0.05),  # configs[2] (--rc)
+    dict(read_len=50000, patterns="TTAGGG TCAGGG", tvr="TGAGGG TTGGGG", rc=False, variant=0.05),  # configs[3]
+], ids=["c10k", "c3", "c4"])
+def test_baseline_config_reads(cfg):
+    # the bench's synthetic reads of each BASELINE configuration (a sample of
+    # 64), through the host path and the hiprtc scan, against the oracle
+    from nanotel_amd import synth_params, synth_read_ascii
+    sp = synth_params(read_len=cfg["read_len"], rc_layout=cfg["rc"], variant_rate=cfg["variant"], first_read=4242)
+    seqs = [synth_read_ascii(sp, i) for i in range(64)]
+    nt = _nt(patterns=cfg["patterns"], tvr_patterns=cfg["tvr"], rc=cfg["rc"])
+    res = nt.analyze(seqs, want_windows=True, want_hits=True)
+    compare(nt, res, oracle_rows(seqs, cfg["patterns"], tvr=cfg["tvr"], rc=cfg["rc"]))
+    assert 0 < res["telomeric"].sum() < 64
+
+
+@pytest.mark.parametrize("cfg", [
     dict(patterns="TTAGGG"),
     dict(patterns="YYAGGG"),
     dict(patterns="TTAGGG TCAGGG"),
