@@ -68,7 +68,9 @@ def main(argv=None):
         import torch
         import torch.distributed as dist
         torch.cuda.set_device(dev)
-        dist.init_process_group("nccl")
+        # RCCL by default; NT_DIST_BACKEND=gloo runs the collectives on the host
+        # (e.g. several ranks sharing one GPU in a test)
+        dist.init_process_group(os.environ.get("NT_DIST_BACKEND", "nccl"))
     try:
         run(a.input_path, a.save_path, a.patterns, fmt=a.format, nrec=a.nrec, rc=a.rc,
             min_density=a.min_density, subseq_length=a.subseq_length,

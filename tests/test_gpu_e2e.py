@@ -92,3 +92,32 @@ def test_driver_use_filter_gpu_matches_oracle_driver(tmp_path):
     a, b = _outputs(gpu_out), _outputs(ora_out)
     assert a == b
     assert len(a["in_summary.csv"].splitlines()) > 5
+
+
+def test_cli_two_ranks_match_one(tmp_path):
+    """The command line under torch.distributed.run with 2 ranks (chunks dealt
+    round-robin, one serial all_reduce per round, rows gathered to rank 0)
+    writes the same files as one process.  Both ranks use GPU 0 here, so the
+    collectives run on gloo (NT_DIST_BACKEND); on a node each rank has its GPU
+    and RCCL."""
+    import socket
+    import subprocess
+    import sys
+    inp = _make_input(str(tmp_path), False)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONPATH=os.path.join(root, "telomere-analyzer_amd"), NT_DIST_BACKEND="gloo",
+               HSA_ENABLE_IPC_MODE_LEGACY="0")
+    args = ["-i", inp, "--format", "fasta", "--patterns", "TTAGGG", "-n", "4", "--device", "0"]
+    one = str(tmp_path / "one")
+    subprocess.run([sys.executable, "-m", "nanotel_amd", "--save_path", one] + args, env=env, check=True,
+                   timeout=120)
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    two = str(tmp_path / "two")
+    subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                    "--master-addr", "127.0.0.1", "--master-port", str(port), "-m", "nanotel_amd",
+                    "--save_path", two] + args, env=env, check=True, timeout=180)
+    a, b = _outputs(one), _outputs(two)
+    assert a == b and len(a["in_summary.csv"].splitlines()) > 5
