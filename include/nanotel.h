@@ -195,6 +195,10 @@ const char* nt_reader_error(const nt_reader* r);
 int64_t nt_reader_next(nt_reader* r, uint64_t nrec, const char* const** names,
                        const uint64_t** name_lens, const char* const** seqs,
                        const uint64_t** seq_lens);
+/* The next nrec records without copying them (a multi-GPU rank passing over
+ * the chunks other ranks scan): the same parse and errors as nt_reader_next,
+ * only the sequence lengths are kept (valid as nt_reader_next's arrays). */
+int64_t nt_reader_skip(nt_reader* r, uint64_t nrec, const uint64_t** seq_lens);
 
 /* --- synthetic long reads (bench / tests) --------------------------------- */
 int nt_synth_device(nt_ctx* ctx, const nt_synth_params* sp, uint64_t n_reads, uint32_t* planes_dev);

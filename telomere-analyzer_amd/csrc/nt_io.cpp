@@ -5,8 +5,9 @@
 //
 //  * input_path is a file, or a directory whose files are listed recursively
 //    and sorted by full path (dir(full.names = TRUE, recursive = TRUE),
-//    NanoTel.R:2176-2178); the files form ONE record stream, a chunk may span
-//    files;
+//    NanoTel.R:2176-2178); dot-files and dot-directories are left out, as
+//    dir()'s all.files = FALSE does; the files form ONE record stream, a chunk
+//    may span files;
 //  * gzip is transparent (zlib gzread also reads plain files);
 //  * FASTA: '>' starts a record whose name is the rest of the header line;
 //    sequence lines are concatenated (line breaks and '\r' dropped, blank
@@ -161,7 +162,9 @@ void list_files(const std::string& path, std::vector<std::string>& out) {
   if (!d) return;
   while (dirent* e = readdir(d)) {
     const std::string n = e->d_name;
-    if (n == "." || n == "..") continue;
+    // dir(all.files = FALSE): names starting with '.' (".", "..", ".DS_Store",
+    // AppleDouble "._x.fastq.gz", hidden directories) are not listed
+    if (n.empty() || n[0] == '.') continue;
     const std::string full = path + "/" + n;
     struct stat st;
     if (stat(full.c_str(), &st) != 0) continue;
@@ -326,6 +329,89 @@ bool next_record(nt_reader* r, std::string& name, std::string& seq) {
   }
 }
 
+// First byte of the current file's next line (refilling the buffer), -1 at
+// the end of the file.
+int peek_byte(nt_reader* r) {
+  if (!r->active) return -1;
+  if (r->pos == r->end) {
+    if (r->eof_file) return -1;
+    const int n = gzread(r->gz, r->buf.data(), (unsigned)r->buf.size());
+    if (n < 0 || (n == 0 && gz_failed(r->gz))) r->err = "read error in " + r->files[r->file_idx - 1];
+    if (n <= 0) {
+      r->eof_file = true;
+      return -1;
+    }
+    r->pos = 0;
+    r->end = (size_t)n;
+  }
+  return (unsigned char)r->buf[r->pos];
+}
+
+// next_record without the copies: the record's sequence length only (the
+// same parse and the same errors; names are short and parsed into a scratch
+// string).  false at the end of all files (or error).
+bool skip_record(nt_reader* r, uint64_t& len) {
+  std::string line;
+  len = 0;
+  for (;;) {
+    if (r->format == 0) {
+      if (!r->has_pending) {
+        bool got = false;
+        while (get_line(r, line)) {
+          if (!line.empty() && line[0] == '>') {
+            r->pending_header = line.substr(1);
+            r->has_pending = got = true;
+            break;
+          }
+        }
+        if (!got) {
+          if (!open_next(r)) return false;
+          continue;
+        }
+      }
+      r->has_pending = false;
+      for (;;) {
+        const int c = peek_byte(r);
+        if (c < 0) break;
+        if (c == '>') {  // the next record's header (its name is needed if next_record reads it)
+          get_line(r, line);
+          r->pending_header = line.substr(1);
+          r->has_pending = true;
+          break;
+        }
+        size_t k = 0;
+        if (!take_line(r, nullptr, &k)) break;
+        if (c != ';') len += k;  // ';' comment lines are dropped, as next_record does
+      }
+      return true;
+    }
+    bool got = false;
+    while (get_line(r, line)) {
+      if (line.empty()) continue;
+      if (line[0] != '@') {
+        r->err = "malformed FASTQ record (expected '@')";
+        return false;
+      }
+      got = true;
+      break;
+    }
+    if (!got) {
+      if (!open_next(r)) return false;
+      continue;
+    }
+    const std::string name = line.substr(1);
+    std::string plus;
+    size_t sl = 0, ql = 0, k = 0;
+    if (!take_line(r, nullptr, &sl) || !get_line(r, plus) || plus.empty() || plus[0] != '+') {
+      r->err = "malformed FASTQ record '" + name + "'";
+      return false;
+    }
+    while (ql < sl && take_line(r, nullptr, &k)) ql += k;
+    len = sl;
+    return true;
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -408,6 +494,32 @@ int64_t nt_reader_next(nt_reader* r, uint64_t nrec, const char* const** names,
   *names = r->c().name_ptr.data();
   *name_lens = r->c().name_len.data();
   *seqs = r->c().seq_ptr.data();
+  *seq_lens = r->c().seq_len.data();
+  r->records_total += n;
+  return (int64_t)n;
+}
+
+int64_t nt_reader_skip(nt_reader* r, uint64_t nrec, const uint64_t** seq_lens) {
+  if (!r || !seq_lens || nrec == 0) return NT_E_ARG;
+  r->cur ^= 1;
+  r->c().names_blob.clear();
+  r->c().seqs_blob.clear();
+  r->c().name_off.clear();
+  r->c().seq_off.clear();
+  r->c().name_len.clear();
+  r->c().seq_len.clear();
+  r->c().name_ptr.clear();
+  r->c().seq_ptr.clear();
+  if (!r->active && r->file_idx == 0 && !open_next(r)) return r->err.empty() ? 0 : NT_E_ARG;
+  uint64_t len = 0;
+  while (r->c().seq_len.size() < nrec) {
+    if (!skip_record(r, len)) {
+      if (!r->err.empty()) return NT_E_ARG;
+      break;
+    }
+    r->c().seq_len.push_back(len);
+  }
+  const size_t n = r->c().seq_len.size();
   *seq_lens = r->c().seq_len.data();
   r->records_total += n;
   return (int64_t)n;

@@ -106,6 +106,7 @@ SIGNATURES = {
     "nt_reader_next": (ctypes.c_int64, [_P, ctypes.c_uint64, ctypes.POINTER(ctypes.c_void_p),
                                         ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p),
                                         ctypes.POINTER(ctypes.c_void_p)]),
+    "nt_reader_skip": (ctypes.c_int64, [_P, ctypes.c_uint64, ctypes.POINTER(ctypes.c_void_p)]),
     "nt_synth_device": (ctypes.c_int, [_P, ctypes.POINTER(NtSynthParams), ctypes.c_uint64, _P]),
     "nt_uniform_layout_device": (ctypes.c_int, [_P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int32,
                                                 _P, _P, _P]),

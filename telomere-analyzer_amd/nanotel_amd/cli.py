@@ -68,9 +68,11 @@ def main(argv=None):
         import torch
         import torch.distributed as dist
         torch.cuda.set_device(dev)
-        # RCCL by default; NT_DIST_BACKEND=gloo runs the collectives on the host
-        # (e.g. several ranks sharing one GPU in a test)
-        dist.init_process_group(os.environ.get("NT_DIST_BACKEND", "nccl"))
+        # The driver's collectives are tiny and host-side (8 bytes per chunk,
+        # an error flag, the pickled summary rows): gloo by default.
+        # NT_DIST_BACKEND=nccl runs the per-round all_reduce over RCCL on a
+        # device tensor instead (opt-in).
+        dist.init_process_group(os.environ.get("NT_DIST_BACKEND", "gloo"))
     try:
         run(a.input_path, a.save_path, a.patterns, fmt=a.format, nrec=a.nrec, rc=a.rc,
             min_density=a.min_density, subseq_length=a.subseq_length,

@@ -15,6 +15,7 @@ only.  --analysis writes the filtered/sorted summary and the results text
 (analysis.py).  Every telomeric read gets the reference's three density plots
 (plots.py: single_read_plots*/read<serial>.jpeg|eps) unless plot=False.
 """
+import math
 import os
 import time
 from concurrent.futures import ThreadPoolExecutor
@@ -104,6 +105,11 @@ def _plot_pool():
     return ProcessPoolExecutor(min(16, os.cpu_count() or 1), mp_context=mp.get_context("spawn"))
 
 
+def _plot_rows(res, order):
+    """The rows of `order` that get plots (reads with at least one window)."""
+    return [int(j) for j in order if int(res["n_windows"][int(j)]) != 0]
+
+
 def _plot_jobs(nt, res, order, lens, ser, save_path):
     """Arguments of plots.write_read_plots for every row of a chunk (the three
     single-read plots of analyze_read, NanoTel.R:1876-1912)."""
@@ -147,19 +153,27 @@ def _scan_chunk(nt, ch, use_filter, write_reads, log, want_windows=False):
 
 
 class _Prefetch:
-    """Chunk k+1 is parsed on a worker thread while chunk k is scanned: the C++
-    reader keeps two chunk buffers in turn and ctypes drops the GIL."""
+    """Chunk k+1 is read on a worker thread while chunk k is scanned: the C++
+    reader keeps two chunk buffers in turn and ctypes drops the GIL.  Chunks
+    this rank does not scan (own(k) false) are passed over with the reader's
+    count-only skip path: record boundaries and lengths, no copies."""
 
-    def __init__(self, rdr, nrec):
-        self._rdr, self._nrec = rdr, nrec
+    def __init__(self, rdr, nrec, own=lambda k: True):
+        self._rdr, self._nrec, self._own = rdr, nrec, own
+        self._k = 0
         self._ex = ThreadPoolExecutor(1)
-        self._f = self._ex.submit(rdr.next_chunk, nrec)
+        self._f = self._ex.submit(self._read)
+
+    def _read(self):
+        k = self._k
+        self._k += 1
+        return self._rdr.next_chunk(self._nrec) if self._own(k) else self._rdr.skip_chunk(self._nrec)
 
     def next_chunk(self):
         if self._f is None:
             return None
         ch = self._f.result()
-        self._f = self._ex.submit(self._rdr.next_chunk, self._nrec) if ch is not None else None
+        self._f = self._ex.submit(self._read) if ch is not None else None
         return ch
 
     def close(self):
@@ -171,6 +185,24 @@ class _Prefetch:
                 pass
             self._f = None
         self._ex.shutdown()
+
+
+def _targets(ser, order):
+    """Rows of a chunk whose reads/plots are written now, and the last row with
+    a -Inf serial.  Once a chunk without rows leaves serial_start at -Inf
+    (max(numeric(0)) + 1, NanoTel.R:2258) every later row is -Inf and all of
+    them name reads/-Inf.fasta.gz and read-Inf.*: concurrent writers would
+    interleave there, so those rows are held back and only the last one in
+    stream order is written, at the end of the run (the reference keeps the
+    last-written read)."""
+    now, last_inf = [], None
+    for j in order:
+        j = int(j)
+        if math.isinf(float(ser[j])):
+            last_inf = j
+        else:
+            now.append(j)
+    return now, last_inf
 
 
 def run(input_path, save_path, patterns, fmt="fastq", nrec=10000, rc=False, min_density=0.6,
@@ -198,65 +230,100 @@ def run(input_path, save_path, patterns, fmt="fastq", nrec=10000, rc=False, min_
     tvr = tvr_patterns is not None
     rdr = Reader(input_path, fmt)
     files = rdr.files()
-    src = _Prefetch(rdr, nrec)
+    # chunk k of the stream is scanned by rank k % world (rounds of `world`
+    # chunks); the other ranks pass over it with the reader's skip path
+    src = _Prefetch(rdr, nrec, own=lambda k: k % world == rank)
     writers = ThreadPoolExecutor(min(16, os.cpu_count() or 1)) if (write_reads or plot) else None
     plotters = None  # worker processes for the plots of large chunks (Python drawing holds the GIL)
     pending = []
     lengths_all = []
     local_rows = {}
+    held = None  # (chunk, read args, plot job) of this rank's last -Inf row (see _targets)
     k = 0  # global chunk index
     s_next, m_run = 1.0, shard.NEG_INF  # serial_start of the next chunk, running max(Serial)
     t0 = time.time()
+    failure = None
     # rounds of `world` chunks: rank r scans chunk r of the round; one
-    # all_reduce per round fixes the serial_starts, so the stream is processed
-    # with O(1) state (every rank parses the stream to stay in step)
+    # all_reduce per round fixes the serial_starts (and carries an error flag,
+    # so that a rank that fails stops every rank at the same round instead of
+    # leaving them blocked in the next collective)
     while True:
         own = None
         n_round = 0
-        for r in range(world):
-            ch = src.next_chunk()
-            if ch is None:
-                break
-            n_round += 1
-            lengths_all.append(ch.lengths.copy())
-            if r == rank:
-                log(f"processing chunk {k + r + 1} ...")
-                own = (r,) + _scan_chunk(nt, ch, use_filter, write_reads, log, want_windows=plot)
-        if n_round == 0:
+        try:
+            for r in range(world):
+                ch = src.next_chunk()
+                if ch is None:
+                    break
+                n_round += 1
+                lengths_all.append(ch.lengths.copy())
+                if r == rank:
+                    log(f"processing chunk {k + r + 1} ...")
+                    own = (r,) + _scan_chunk(nt, ch, use_filter, write_reads, log, want_windows=plot)
+        except Exception as ex:  # noqa: BLE001 -- re-raised after the collective
+            failure = ex
+        maxima, failed = shard.exchange_rel_max({own[0]: own[3]} if own else {}, world, device=coll_dev,
+                                                failed=failure is not None)
+        if failed:
             break
-        maxima = shard.exchange_rel_max({own[0]: own[3]} if own else {}, n_round, device=coll_dev)
         starts = np.empty(n_round, np.float64)
         for r in range(n_round):  # the reference's recurrence, chunk by chunk
             starts[r], s_next, m_run = shard.advance(s_next, m_run, float(maxima[r]))
-        if own is not None and own[4] is None:
-            local_rows[k + own[0]] = []  # --use_filter kept no read of this chunk
-        elif own is not None:
-            r, rel, order, _, res, names, lens, seqs = own
-            ser = shard.assign_chunk_serials(rel, starts[r])
-            local_rows[k + r] = chunk_rows(res, names, lens, ser, order, nt.n_pass)
-            for f in pending:  # the previous chunk's files (errors surface here)
-                f.result()
-            pending = []
-            if write_reads:
-                pending += [writers.submit(_write_read, os.path.join(
-                    reads_dir, f"{r_as_character(float(ser[int(j)]))}.fasta.gz"), names[int(j)],
-                    seqs[int(j)], rc) for j in order]
-            if plot:
-                jobs = _plot_jobs(nt, res, order, lens, ser, save_path)
-                if len(jobs) >= 64 and plotters is None:
-                    plotters = _plot_pool()
-                pool = plotters if len(jobs) >= 64 else writers
-                pending += [pool.submit(plots.write_read_plots, *a, jpeg=plot_jpeg, **kw) for a, kw in jobs]
+        try:
+            if own is not None and own[4] is None:
+                local_rows[k + own[0]] = []  # --use_filter kept no read of this chunk
+            elif own is not None:
+                r, rel, order, _, res, names, lens, seqs = own
+                ser = shard.assign_chunk_serials(rel, starts[r])
+                local_rows[k + r] = chunk_rows(res, names, lens, ser, order, nt.n_pass)
+                for f in pending:  # the previous chunk's files (errors surface here)
+                    f.result()
+                pending = []
+                now, last_inf = _targets(ser, order)
+                jobs = _plot_jobs(nt, res, order, lens, ser, save_path) if plot else []
+                job_of = {int(j): jb for j, jb in zip(_plot_rows(res, order), jobs)}
+                if last_inf is not None:
+                    held = (k + r, (names[last_inf], seqs.get(last_inf), rc), job_of.get(last_inf))
+                if write_reads:
+                    pending += [writers.submit(_write_read, os.path.join(
+                        reads_dir, f"{r_as_character(float(ser[j]))}.fasta.gz"), names[j], seqs[j], rc)
+                        for j in now]
+                if plot:
+                    jobs = [job_of[j] for j in now if j in job_of]
+                    if len(jobs) >= 64 and plotters is None:
+                        plotters = _plot_pool()
+                    pool = plotters if len(jobs) >= 64 else writers
+                    pending += [pool.submit(plots.write_read_plots, *a, jpeg=plot_jpeg, **kw) for a, kw in jobs]
+        except Exception as ex:  # noqa: BLE001
+            failure = ex
         k += n_round
         if n_round < world:
             break
-    for f in pending:
-        f.result()
+    try:
+        for f in pending:
+            f.result()
+        # the last -Inf row of the whole stream: written by the rank that holds it
+        last = shard.max_over_ranks(held[0] if held else -1)
+        if held is not None and held[0] == last:
+            name, seq, rcf = held[1]
+            if write_reads:
+                _write_read(os.path.join(reads_dir, "-Inf.fasta.gz"), name, seq, rcf)
+            if plot and held[2] is not None:
+                a, kw = held[2]
+                plots.write_read_plots(*a, jpeg=plot_jpeg, **kw)
+    except Exception as ex:  # noqa: BLE001
+        failure = failure or ex
     if writers is not None:
         writers.shutdown()
     if plotters is not None:
         plotters.shutdown()
     src.close()
+    if shard.any_rank(failure is not None):
+        rdr.close()
+        nt.close()
+        if failure is not None:
+            raise failure
+        raise RuntimeError("NanoTel: another rank failed (see its error)")
     rows = shard.gather_rows(local_rows)
     rdr.close()
     nt.close()

@@ -51,6 +51,16 @@ class Chunk:
         return ctypes.string_at(self._sp[i], int(self.lengths[i]))
 
 
+class SkippedChunk:
+    """A chunk passed over with nt_reader_skip: the read lengths only (a rank
+    of a multi-GPU run steps over the chunks other ranks scan)."""
+
+    def __init__(self, n, seq_lens_p):
+        self.n = int(n)
+        self.lengths = np.ctypeslib.as_array(ctypes.cast(seq_lens_p, ctypes.POINTER(ctypes.c_uint64)),
+                                             shape=(self.n,)) if self.n else np.zeros(0, np.uint64)
+
+
 class Reader:
     def __init__(self, path, fmt="fastq"):
         if fmt not in ("fasta", "fastq"):
@@ -74,6 +84,17 @@ class Reader:
         if n == 0:
             return None
         return Chunk(n, a, b, c, d)
+
+    def skip_chunk(self, nrec):
+        """The next nrec records without copying names or sequences
+        (nt_reader_skip); None at the end."""
+        d = ctypes.c_void_p()
+        n = lib().nt_reader_skip(self._h, int(nrec), ctypes.byref(d))
+        if n < 0:
+            raise NanoTelError(int(n), lib().nt_reader_error(self._h).decode())
+        if n == 0:
+            return None
+        return SkippedChunk(n, d)
 
     def close(self):
         if getattr(self, "_h", None) is not None and self._h.value:

@@ -73,19 +73,39 @@ def serial_starts(rel_max):
     return starts
 
 
-def exchange_rel_max(local, n_chunks, group=None, device=None):
+def exchange_rel_max(local, n_chunks, group=None, device=None, failed=False):
     """All ranks' per-chunk relative maxima: local = {chunk: rel_max} for the
     chunks this rank owns.  One all_reduce(MAX) over an n_chunks float64
-    vector (gloo on CPU tensors, RCCL on device tensors)."""
+    vector plus one error flag (gloo on CPU tensors, RCCL on device tensors).
+    Returns (maxima, any rank failed): a rank that failed publishes the flag
+    so that every rank stops at this collective."""
     import torch
     import torch.distributed as dist
-    t = torch.full((n_chunks,), NEG_INF, dtype=torch.float64,
+    t = torch.full((n_chunks + 1,), NEG_INF, dtype=torch.float64,
                    device=device if device is not None else "cpu")
     for k, v in local.items():
         t[k] = v
+    t[n_chunks] = 1.0 if failed else 0.0
     if dist.is_initialized() and dist.get_world_size(group) > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
-    return t.cpu().numpy()
+    a = t.cpu().numpy()
+    return a[:n_chunks], bool(a[n_chunks] > 0.0)
+
+
+def max_over_ranks(x, group=None):
+    """max over the ranks of an integer (one all_reduce on the host)."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_initialized() and dist.get_world_size(group) > 1):
+        return int(x)
+    t = torch.tensor([int(x)], dtype=torch.int64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return int(t.item())
+
+
+def any_rank(flag, group=None):
+    """True on every rank if `flag` is true on any."""
+    return max_over_ranks(1 if flag else 0, group) > 0
 
 
 def assign_chunk_serials(rel, start):

@@ -230,3 +230,106 @@ def test_filter_oracle_edges():
     assert O.filter_read(s, P, right_edge=True) and not O.filter_read(s, P)
     # fixed=FALSE: a subject N matches any pattern letter
     assert O.filter_read("A" * 70 + "N" * 96 + "C" * 1000, P)
+
+
+def _inf_input(d):
+    """Chunk 1 (nrec=3) has no telomeric read: the reference's serial_start
+    becomes max(numeric(0)) + 1 = -Inf and every later row is -Inf, so all
+    telomeric reads name reads/-Inf.fasta.gz (NanoTel.R:1871, 2258)."""
+    rng = np.random.default_rng(21)
+
+    def read(n, tract):
+        s = list(rng.choice(list("ACGT"), n))
+        if tract:
+            t = int(rng.integers(300, min(n, 1500)))
+            s[:t] = list(("TTAGGG" * (t // 6 + 1))[:t])
+        return "".join(s)
+
+    recs = [(f"plain{i}", read(2000, False)) for i in range(3)]
+    recs += [(f"t{i}", read(int(rng.integers(1500, 4000)), i % 3 != 1)) for i in range(14)]
+    os.makedirs(os.path.join(d, "in"))
+    with open(os.path.join(d, "in", "a.fasta"), "w") as f:
+        for n, s in recs:
+            f.write(f">{n}\n{s}\n")
+    return os.path.join(d, "in"), recs
+
+
+def test_inf_serials_write_the_last_read_once():
+    import torch.multiprocessing as mp
+    with tempfile.TemporaryDirectory() as d:
+        inp, recs = _inf_input(d)
+        P = O.Patterns("TTAGGG")
+        telo = [n for n, s in recs if O.analyze_read(s, P)["telomeric"]]
+        assert telo and not any(n.startswith("plain") for n in telo)
+        res = {}
+        for world in (1, 2, 3):
+            out = os.path.join(d, f"out{world}")
+            if world == 1:
+                _rank_main(0, 1, 0, inp, out, False)
+            else:
+                mp.spawn(_rank_main, args=(world, _free_port(), inp, out, False), nprocs=world, join=True)
+            res[world] = _outputs(out)
+        assert res[1] == res[2] == res[3]
+        lines = res[1]["in_summary.csv"].decode().splitlines()[1:]
+        assert len(lines) == len(telo) and all(x.startswith("-Inf,") for x in lines)
+        reads = sorted(k for k in res[1] if k.startswith("reads" + os.sep))
+        assert reads == [os.path.join("reads", "-Inf.fasta.gz")]
+        # the row written last in the stream: the last telomeric read in row order
+        last = lines[-1].split(",")[1]
+        assert res[1][reads[0]].decode().splitlines()[0] == ">" + last
+        seq = dict(recs)[last]
+        assert "".join(res[1][reads[0]].decode().splitlines()[1:]) == seq
+
+
+class FailingNanoTel(OracleNanoTel):
+    """Raises on the second chunk it scans (rank 1 in a 2-rank run)."""
+
+    calls = 0
+
+    def analyze_chunk(self, ch, want_windows=False):
+        import torch.distributed as dist
+        FailingNanoTel.calls += 1
+        if dist.is_initialized() and dist.get_rank() == 1 and FailingNanoTel.calls == 2:
+            raise RuntimeError("injected scan failure")
+        return super().analyze_chunk(ch, want_windows)
+
+
+def _failing_rank(rank, world, port, inp, out, q):
+    import torch.distributed as dist
+    from nanotel_amd import driver
+    driver.NanoTel = FailingNanoTel
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        driver.run(inp, out, "TTAGGG", fmt="fasta", nrec=3, log=lambda *a: None, plot=False)
+        q.put((rank, "ok"))
+    except Exception as ex:  # noqa: BLE001
+        q.put((rank, str(ex)))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(180)
+def test_rank_failure_stops_every_rank():
+    """A rank that fails inside a chunk round publishes the error flag with the
+    serial all_reduce: every rank raises at that round (the reference stops at
+    the first error) instead of waiting in the next collective."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    with tempfile.TemporaryDirectory() as d:
+        inp = _make_input(d)
+        q = ctx.Queue()
+        port = _free_port()
+        ps = [ctx.Process(target=_failing_rank, args=(r, 2, port, inp, os.path.join(d, "o"), q)) for r in range(2)]
+        for p in ps:
+            p.start()
+        for p in ps:
+            p.join(150)
+        alive = [p.is_alive() for p in ps]
+        for p in ps:
+            if p.is_alive():
+                p.kill()
+        assert not any(alive)
+        got = dict(q.get(timeout=5) for _ in range(2))
+        assert got[1] == "injected scan failure"
+        assert "another rank failed" in got[0]

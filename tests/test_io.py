@@ -109,6 +109,58 @@ def test_reader_run_directory_inflated_ahead(tmp_path, monkeypatch, threads):
         _chunks(str(d), "fastq", 1000)
 
 
+def test_reader_skips_dot_files(tmp_path):
+    """dir(recursive = TRUE) leaves out names starting with '.' (all.files =
+    FALSE, NanoTel.R:2176): AppleDouble '._*' parts, .DS_Store and hidden
+    directories are not part of the record stream or the file list."""
+    rng = np.random.default_rng(11)
+    recs = [(f"r{i}", "".join(rng.choice(list("ACGT"), int(rng.integers(5, 400))))) for i in range(9)]
+    d = tmp_path / "run"
+    (d / ".hidden").mkdir(parents=True)
+    _write_fastq(d / "a.fastq.gz", recs[:4], gz=True)
+    _write_fastq(d / "b.fastq", recs[4:])
+    (d / "._a.fastq.gz").write_bytes(b"\x00\x05\x16\x07AppleDouble")
+    (d / ".DS_Store").write_bytes(b"\x00\x00\x00\x01Bud1")
+    _write_fastq(d / ".hidden" / "c.fastq", recs[:2])
+    with Reader(str(d), "fastq") as r:
+        assert [os.path.basename(p) for p in r.files()] == ["a.fastq.gz", "b.fastq"]
+    assert sum(_chunks(str(d), "fastq", 4), []) == recs
+
+
+@pytest.mark.parametrize("fmt", ["fasta", "fastq"])
+def test_reader_skip_path_matches_next(tmp_path, fmt):
+    """nt_reader_skip (ranks passing over other ranks' chunks) keeps the same
+    record boundaries and lengths as nt_reader_next, interleaved with it,
+    across wrapped FASTA lines, blank and ';' lines, CRLF, gzip and files."""
+    rng = np.random.default_rng(12)
+    recs = [(f"r{i} x", "".join(rng.choice(list("ACGTN"), int(rng.integers(0 if fmt == "fasta" else 1, 500)))))
+            for i in range(40)]
+    d = tmp_path / "in"
+    (d / "sub").mkdir(parents=True)
+    if fmt == "fastq":
+        _write_fastq(d / "a.fastq", recs[:15], crlf=True)
+        _write_fastq(d / "sub" / "b.fastq.gz", recs[15:], gz=True)
+    else:
+        with open(d / "a.fa", "w", newline="") as f:
+            for n, s in recs[:15]:
+                f.write(f">{n}\r\n" + "".join(s[i:i + 60] + "\r\n" for i in range(0, len(s), 60)) + "\n;c\n")
+        with gzip.open(d / "sub" / "b.fa.gz", "wt") as f:
+            for n, s in recs[15:]:
+                f.write(f">{n}\n{s}\n")
+    for nrec in (1, 3, 7, 100):
+        with Reader(str(d), fmt) as r:
+            k, seen = 0, []
+            while True:
+                ch = r.skip_chunk(nrec) if k % 2 else r.next_chunk(nrec)
+                if ch is None:
+                    break
+                if k % 2 == 0:
+                    assert [(ch.name(i), ch.seq(i).decode()) for i in range(ch.n)] == recs[len(seen):len(seen) + ch.n]
+                seen += [int(x) for x in ch.lengths]
+                k += 1
+        assert seen == [len(s) for _, s in recs]
+
+
 def test_reader_fasta_wrapped_blank_lines(tmp_path):
     p = tmp_path / "x.fa.gz"
     with gzip.open(p, "wt") as f:

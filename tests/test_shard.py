@@ -79,7 +79,8 @@ def _rank_main(rank, world, port, seed, out_path):
     flags = _chunks(seed)  # every rank knows the chunk layout, scans only its own chunks
     mine = shard.local_chunks(len(flags), rank, world)
     rel = {k: shard.chunk_relative(flags[k]) for k in mine}
-    all_max = shard.exchange_rel_max({k: rel[k][2] for k in mine}, len(flags))
+    all_max, failed = shard.exchange_rel_max({k: rel[k][2] for k in mine}, len(flags))
+    assert not failed
     starts = shard.serial_starts(all_max)
     rows = {}
     for k in mine:
