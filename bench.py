@@ -139,6 +139,7 @@ def main():
     ap.add_argument("--config", default="c50k", choices=sorted(CONFIGS))
     ap.add_argument("--reads", type=int, default=0, help="override reads per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--per-read", action="store_true", help="per-read scan only (no bundle layout)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     args = ap.parse_args()
 
@@ -181,12 +182,27 @@ def main():
     sp = synth_params(first_read=rank * n, read_len=L, variant_rate=cfg["variant"], rc_layout=cfg["rc"])
     nt.synth_device(sp, n, planes.data_ptr())
     nt.uniform_layout_device(n, L, blk_off.data_ptr(), lens.data_ptr(), win_off.data_ptr())
+    # the bundle layout (the reads transposed 32 to a bundle, the bundle scan's
+    # copy of them), built on the device before the timed region like the planes
+    bundles, keep = None, []
+    if nt.tscan and not args.per_read:
+        from nanotel_amd.api import DeviceBundles
+        import numpy as np
+        plan = nt.bundle_plan(np.full(n, L, np.uint32))
+        bread = torch.from_numpy(plan.bnd_read.view(np.int32)).to(dev)
+        bstripe = torch.from_numpy(plan.bnd_stripe.view(np.int64)).to(dev)
+        tpl = torch.empty(max(1, plan.tplane_bytes // 4), dtype=torch.int32, device=dev)
+        keep = [bread, bstripe, tpl]
+        bundles = DeviceBundles(tpl.data_ptr(), bread.data_ptr(), bstripe.data_ptr(), plan.n_bundles, 0, 0,
+                                plan.tplane_bytes)
+        nt.bundle_layout_device(planes.data_ptr(), blk_off.data_ptr(), lens.data_ptr(), win_off.data_ptr(),
+                                n, n * nw, bundles)
     torch.cuda.synchronize(dev)
 
     def step():
         nt.scan_call_device(planes.data_ptr(), blk_off.data_ptr(), lens.data_ptr(), win_off.data_ptr(),
                             n, n * nw, L, start.data_ptr(), end.data_ptr(), dens.data_ptr(),
-                            flags.data_ptr(), wc.data_ptr())
+                            flags.data_ptr(), wc.data_ptr(), bundles=bundles)
 
     for _ in range(args.warmup):
         step()
@@ -251,7 +267,9 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic,
-                         "kernel": ("nt_scan_jit_nh_lds (scan specialised for the patterns, hiprtc)" if nt.jit
+                         "kernel": ("nt_tscan_jit (bundle scan specialised for the patterns, hiprtc)"
+                                    if bundles is not None else
+                                    "nt_scan_jit_nh_lds (scan specialised for the patterns, hiprtc)" if nt.jit
                                     else "nt::nt_scan_kernel (ahead-of-time scan)"),
                          "kernel_avg_ms": round(scan_s * 1e3, 4),
                          "algorithmic_bytes_per_launch": scan_bytes,

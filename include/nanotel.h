@@ -75,6 +75,7 @@ typedef struct {
   int32_t raw_p1; /* P1 keeps raw views (single fixed pattern) */
   int32_t jit;    /* 1: the scan runs as a kernel specialised for these patterns (hiprtc);
                      0: ahead-of-time kernels (NT_JIT=0 in the environment, or hiprtc failed) */
+  int32_t tscan;  /* 1: bundled reads take the bundle scan (nt_tscan.h; NT_TSCAN=0 turns it off) */
 } nt_program_info;
 
 /* Device-resident read batch (device pointers).  Layout: see DESIGN.md
@@ -90,6 +91,16 @@ typedef struct {
   const uint8_t* exc_code;
   uint64_t n_reads;
   uint64_t n_windows;       /* sum of split_telo window counts (win_counts has n_windows*n_pass) */
+  /* Bundle scan (optional): the reads transposed 32 to a bundle
+   * (nt_bundle_plan + nt_bundle_layout).  tplanes == NULL: every read takes the
+   * per-read scan.  Else the bundled reads take the bundle scan and the reads
+   * in list[0 .. n_list) the per-read scan (list may be NULL when n_list == 0). */
+  const uint32_t* tplanes;
+  const uint32_t* bnd_read;   /* [n_bundles * 32] read of each slot, ~0u = empty */
+  const uint64_t* bnd_stripe; /* [n_bundles + 1] first stripe of each bundle */
+  uint64_t n_bundles;
+  const uint32_t* list;       /* reads outside the bundles */
+  uint64_t n_list;
 } nt_batch;
 
 /* Device-resident outputs (device pointers). */
@@ -139,6 +150,20 @@ int nt_pack_count(const char* const* seqs, const uint64_t* lens, uint64_t n_read
 int nt_pack_reads(const char* const* seqs, const uint64_t* lens, uint64_t n_reads, int32_t rc,
                   int32_t subseq_length, uint32_t* planes, uint64_t* blk_off, uint32_t* len,
                   uint64_t* win_off, uint32_t* exc_off, uint32_t* exc_pos, uint8_t* exc_code);
+
+/* --- bundle layout (the bundle scan's copy of the reads) ------------------- */
+/* Host: group the reads of a batch 32 to a bundle (longest first; the compiled
+ * program fixes the block size L).  has_exc (NULL = none) marks reads with
+ * non-ACGT letters, which stay outside the bundles, as do reads of any
+ * program the bundle scan does not cover (then *n_bundles = 0).  Outputs:
+ * bnd_read [ceil(n/32)*32], bnd_stripe [ceil(n/32)+1], list [n] (the reads
+ * left out, in order), and the bytes of the T-layout buffer. */
+int nt_bundle_plan(nt_ctx* ctx, const uint32_t* len, const uint8_t* has_exc, uint64_t n_reads,
+                   uint32_t* bnd_read, uint64_t* bnd_stripe, uint64_t* n_bundles, uint32_t* list,
+                   uint64_t* n_list, uint64_t* tplane_bytes);
+/* Device: write the T-layout (batch->tplanes, tplane_bytes from the plan) from
+ * the batch's per-read planes.  Asynchronous on the context stream. */
+int nt_bundle_layout(nt_ctx* ctx, const nt_batch* batch, uint32_t* tplanes, uint64_t tplane_bytes);
 
 /* --- the hot path --------------------------------------------------------- */
 /* Asynchronous on the context stream.  max_len = longest read of the batch. */

@@ -77,6 +77,15 @@ struct NtProgram {
   NtPat tvr[NT_MAX_PAT];
 };
 
+// T-layout ("bundles", the bundle scan's copy of the reads, nt_tscan.h):
+//   reads grouped NT_BUNDLE to a bundle, slots sorted by length (non-increasing;
+//   read index ~0u = empty slot).  Bundle b's positions are cut into blocks of
+//   L = subseq_length positions, 64 blocks to a STRIPE; stripe g holds T*64
+//   16-byte words (T = ceil(L/2)): word t*64 + l = {lo, hi of position q,
+//   lo, hi of position q+1} of block l, q = block start + 2t, bit s = slot s.
+//   Bundle b owns stripes [bnd_stripe[b], bnd_stripe[b+1]).
+#define NT_BUNDLE 32
+
 struct NtBatch {
   const uint32_t* planes;   // uint2 blocks
   const uint64_t* blk_off;  // [n_reads]
@@ -86,6 +95,14 @@ struct NtBatch {
   const uint32_t* exc_pos;  // sorted per read, 0-based positions
   const uint8_t* exc_code;  // Biostrings DNA codes
   uint64_t n_reads;
+  // per-read scan (scan_reads): the reads it scans, list[i] (nullptr: all n_reads)
+  const uint32_t* list;
+  uint64_t n_list;
+  // bundle scan (nt_tscan.h); tplanes == nullptr: no bundles
+  const uint32_t* tplanes;     // 16-byte words, see above
+  const uint32_t* bnd_read;    // [n_bundles * NT_BUNDLE]
+  const uint64_t* bnd_stripe;  // [n_bundles + 1]
+  uint64_t n_bundles;
 };
 
 struct NtOut {

@@ -30,7 +30,9 @@ hipError_t nt_dev_launch(const NtProgram* prog, const uint32_t* thr, const NtBat
 hipError_t nt_dev_set_lds_limit(uint32_t bytes);
 int nt_dev_scan_blocks_per_cu(int single, int one, int m6, int lds, size_t lds_bytes);
 hipError_t nt_dev_launch_call(const NtProgram* prog, const NtBatch* B, const NtOut* O,
-                              const uint64_t* tmask, int call_grid, hipStream_t stream);
+                              const uint64_t* tmask, const uint32_t* thr, uint32_t thr_size, int fix_last,
+                              int call_grid, hipStream_t stream);
+hipError_t nt_dev_launch_bundle(const NtBatch* B, uint32_t* tp, int L, hipStream_t stream, int cu_count);
 hipError_t nt_dev_launch_synth(const NtSynth* S, uint32_t* planes, uint64_t n_reads,
                                hipStream_t stream);
 hipError_t nt_dev_launch_filter(const NtProgram* prog, const NtBatch* B, uint8_t* keep,
@@ -41,7 +43,10 @@ hipError_t nt_dev_launch_uniform_layout(uint64_t n_reads, uint64_t nblk, uint64_
 }
 
 int nt_jit_blocks_per_cu(void* fn, size_t lds_bytes);
-bool nt_jit_get(int device, const NtProgram& P, void* fn[4], std::string& err);
+bool nt_jit_get(int device, const NtProgram& P, void* fn[4], void** tfn, std::string& err);
+bool nt_tscan_eligible(const NtProgram& P);
+hipError_t nt_tjit_launch(void* fn, int grid, hipStream_t stream, const NtBatch* B, const NtOut* O,
+                          uint64_t* tmask, unsigned long long* queue, uint32_t thr_full);
 hipError_t nt_jit_launch(void* fn, int grid, size_t lds_bytes, hipStream_t stream,
                          const NtProgram* prog, const uint32_t* thr, const NtBatch* B,
                          const NtOut* O, uint64_t* tmask, unsigned long long* queue,
@@ -276,6 +281,9 @@ struct nt_ctx {
   size_t n_ev = 0;  // calls recorded since the last nt_kernel_times
   bool jit = false;  // hiprtc-specialised scan kernels (nt_jit.cpp)
   void* jit_fn[4] = {};  // [no hit counters ? 2 : 0] + [global scratch ? 1 : 0]
+  void* tjit_fn = nullptr;  // the bundle scan of the program (nt_tscan.h), or null
+  std::vector<uint32_t> thr_h;  // telomeric threshold per window width (nt_compile)
+  int tscan_bpc = 0;        // its resident 256-thread blocks per CU
   std::string jit_err;
   NtProgram prog{};
   nt_params params{};
@@ -283,6 +291,7 @@ struct nt_ctx {
   int cu_count = 256;
   DevBuf planes, blk_off, len, win_off, exc_off, exc_pos, exc_code;
   DevBuf wc, start, end, dens, flags, hits, scratch, tmask, thr, queue;
+  DevBuf tplanes, bnd_read, bnd_stripe, list;  // upload_reads' bundle layout
   HostBuf h_planes, h_meta;  // upload_reads staging
 };
 
@@ -450,9 +459,16 @@ int nt_compile(nt_ctx* ctx, const nt_params* prm, nt_program_info* info) {
   e = hipMemcpy(ctx->thr.p, thr.data(), thr.size() * 4, hipMemcpyHostToDevice);
   if (e != hipSuccess) return hip_fail(ctx, e, "hipMemcpy(thr)");
   ctx->prog = P;
+  ctx->thr_h = thr;
   ctx->params = *prm;
   ctx->compiled = true;
-  ctx->jit = nt_jit_get(ctx->device, P, ctx->jit_fn, ctx->jit_err);
+  ctx->jit = nt_jit_get(ctx->device, P, ctx->jit_fn, &ctx->tjit_fn, ctx->jit_err);
+  ctx->tscan_bpc = 0;
+  if (ctx->tjit_fn && std::getenv("NT_TSCAN") && std::getenv("NT_TSCAN")[0] == '0') ctx->tjit_fn = nullptr;
+  if (ctx->tjit_fn) {
+    ctx->tscan_bpc = nt_jit_blocks_per_cu(ctx->tjit_fn, 0);
+    if (ctx->tscan_bpc <= 0) ctx->tjit_fn = nullptr;
+  }
   if (info) {
     info->n_pass = P.n_pass;
     info->n_pat = P.n_pat;
@@ -460,6 +476,7 @@ int nt_compile(nt_ctx* ctx, const nt_params* prm, nt_program_info* info) {
     info->n_hits = P.n_hits;
     info->raw_p1 = P.raw_p1;
     info->jit = ctx->jit ? 1 : 0;
+    info->tscan = ctx->tjit_fn ? 1 : 0;
   }
   return NT_OK;
 }
@@ -628,8 +645,15 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
   const int single = (P.n_pat == 1 && P.n_tvr == 0 && np == 2) ? 1 : 0;
   const int one = (single && P.pat[0].onehot) ? 1 : 0;
   const int m6 = (single && P.pat[0].m == 6) ? 1 : 0;
+  // the bundle scan takes the bundled reads when the program has one and no
+  // hit counters are asked for (a parity/debug output of the per-read scan)
+  const bool tscan = ctx->tjit_fn && batch->tplanes && batch->n_bundles && !out->hits;
   NtBatch B{batch->planes, batch->blk_off, batch->len, batch->win_off,
-            batch->exc_off, batch->exc_pos, batch->exc_code, batch->n_reads};
+            batch->exc_off, batch->exc_pos, batch->exc_code, batch->n_reads,
+            tscan ? batch->list : nullptr, tscan ? batch->n_list : 0,
+            tscan ? batch->tplanes : nullptr, batch->bnd_read, batch->bnd_stripe, tscan ? batch->n_bundles : 0};
+  if (tscan && batch->n_list && !batch->list) return fail(ctx, NT_E_ARG, "n_list > 0 without a list");
+  const uint64_t n_scan = tscan ? batch->n_list : batch->n_reads;  // reads of the per-read scan
   NtOut O{out->win_counts, out->start, out->end, out->density, out->flags, out->hits};
   hipError_t e;
   if (!ctx->lds_limit_set) {
@@ -666,6 +690,7 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
   uint64_t nsub = 1;
   if (const char* v = std::getenv("NT_SUBBATCH")) nsub = std::max<uint64_t>(1, std::strtoull(v, nullptr, 10));
   nsub = std::min<uint64_t>(nsub, std::max<uint64_t>(1, batch->n_reads / 256));
+  if (tscan) nsub = 1;
   int bpc_cap = 0;
   if (const char* v = std::getenv("NT_SCAN_WAVES")) bpc_cap = std::atoi(v);
   if (nsub > 1 && !ctx->call_stream) {
@@ -676,7 +701,7 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
       return hip_fail(ctx, e, "hipEventCreate");
   }
   // read queues: two per sub-batch (LDS and global-scratch launches), zeroed on the stream
-  if ((e = ctx->queue.ensure(2 * NT_QUEUE_WORDS * 8 * nsub)) != hipSuccess) return hip_fail(ctx, e, "hipMalloc(queue)");
+  if ((e = ctx->queue.ensure((2 * nsub + 1) * NT_QUEUE_WORDS * 8)) != hipSuccess) return hip_fail(ctx, e, "hipMalloc(queue)");
   unsigned long long* queue = (unsigned long long*)ctx->queue.p;
   hipEvent_t* ev = nullptr;
   if (ctx->profile) {
@@ -689,7 +714,14 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
     ev = ctx->ev[ctx->n_ev++].data();
     (void)hipEventRecord(ev[0], ctx->stream);
   }
-  if ((e = hipMemsetAsync(queue, 0, 2 * NT_QUEUE_WORDS * 8 * nsub, ctx->stream)) != hipSuccess) return hip_fail(ctx, e, "hipMemsetAsync(queue)");
+  if ((e = hipMemsetAsync(queue, 0, (2 * nsub + 1) * NT_QUEUE_WORDS * 8, ctx->stream)) != hipSuccess) return hip_fail(ctx, e, "hipMemsetAsync(queue)");
+  if (tscan) {  // the bundle scan first: one wave per bundle, exactly the resident blocks
+    const uint64_t tgrid = std::max<uint64_t>(1, std::min<uint64_t>((batch->n_bundles + 3) / 4,
+                                                                    (uint64_t)ctx->cu_count * ctx->tscan_bpc));
+    e = nt_tjit_launch(ctx->tjit_fn, (int)tgrid, ctx->stream, &B, &O, tmask, queue + 2 * nsub * NT_QUEUE_WORDS,
+                       ctx->thr_h[std::min<size_t>((size_t)L, ctx->thr_h.size() - 1)]);
+    if (e != hipSuccess) return hip_fail(ctx, e, "launch nt_tscan_jit");
+  }
   const uint32_t ww_lds = nt_dev_wave_words(noslots, nh, np, cap_nw);
   const size_t lds_bytes = (size_t)ww_lds * 4u * 4u;
   // exactly the resident blocks (the waves take reads from a queue)
@@ -725,8 +757,9 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
     if (Ok.hits) Ok.hits += (uint64_t)nh * r0;
     uint64_t* tmk = tmask + 2 * r0 * (uint64_t)np;  // aux_base(win_off, r, np) of the global read index
     unsigned long long* q = queue + 2 * NT_QUEUE_WORDS * k;
-    const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((nr + 3) / 4, (uint64_t)ctx->cu_count * bpc));
-    const QueuePlan qp = queue_plan(nr, batch->n_windows * (uint64_t)L / batch->n_reads, grid * 4);
+    const uint64_t ns = tscan ? n_scan : nr;  // queue positions of the per-read scan
+    const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((ns + 3) / 4, (uint64_t)ctx->cu_count * bpc));
+    const QueuePlan qp = queue_plan(std::max<uint64_t>(ns, 1), batch->n_windows * (uint64_t)L / batch->n_reads, grid * 4);
     const uint32_t claim = qp.claim, nstatic = qp.nstatic;
     // NT_DBG_CHECK_PLANES=<planes in 16-byte segments> (debugging, with the
     // scan JIT-built with -DNT_DBG_CHECK=1): address checks, report on stderr
@@ -737,7 +770,7 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
         (void)hipMemcpy(dbg, h, sizeof h, hipMemcpyHostToDevice);
       }
     }
-    if (dbg_skip_scan)
+    if (dbg_skip_scan || n_scan == 0)
       e = hipSuccess;
     else if (ctx->jit)
       e = nt_jit_launch(jit_lds, (int)grid, lds_bytes, ctx->stream, ctx->prog_dev,
@@ -756,7 +789,7 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
       (void)hipFree(dbg);
     }
     if (e != hipSuccess) return hip_fail(ctx, e, "launch nt_scan_kernel<lds>");
-    if (two) {
+    if (two && n_scan > 0) {
       if (ctx->jit)
         e = nt_jit_launch(jit_gmem, (int)grid_g, 0, ctx->stream, ctx->prog_dev, (const uint32_t*)ctx->thr.p,
                           &Bk, &Ok, tmk, q + NT_QUEUE_WORDS, (uint32_t)len_cap, 0xFFFFFFFFu, 1u, 0u, ww_g, (uint32_t*)ctx->scratch.p);
@@ -771,13 +804,16 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
     const uint64_t call_grid = std::max<uint64_t>(1, std::min<uint64_t>((call_lanes + 255) / 256, (uint64_t)ctx->cu_count * 64));
     if (nsub == 1) {
       if (ev) (void)hipEventRecord(ev[1], ctx->stream);
-      e = dbg_skip_call ? hipSuccess : nt_dev_launch_call(ctx->prog_dev, &Bk, &Ok, tmk, (int)call_grid, ctx->stream);
+      e = dbg_skip_call ? hipSuccess
+                        : nt_dev_launch_call(ctx->prog_dev, &Bk, &Ok, tmk, (const uint32_t*)ctx->thr.p,
+                                             (uint32_t)ctx->thr_h.size(), tscan ? 1 : 0, (int)call_grid, ctx->stream);
     } else {
       // calling kernel of this sub-batch on the call stream, after its scan
       if ((e = hipEventRecord(ctx->ev_scan, ctx->stream)) != hipSuccess ||
           (e = hipStreamWaitEvent(ctx->call_stream, ctx->ev_scan, 0)) != hipSuccess)
         return hip_fail(ctx, e, "stream dependency");
-      e = nt_dev_launch_call(ctx->prog_dev, &Bk, &Ok, tmk, (int)call_grid, ctx->call_stream);
+      e = nt_dev_launch_call(ctx->prog_dev, &Bk, &Ok, tmk, (const uint32_t*)ctx->thr.p, (uint32_t)ctx->thr_h.size(),
+                             0, (int)call_grid, ctx->call_stream);
     }
     if (e != hipSuccess) return hip_fail(ctx, e, "launch nt_call_kernel");
   }
@@ -789,6 +825,61 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
   }
   if (ev) (void)hipEventRecord(ev[2], ctx->stream);
   return NT_OK;
+}
+
+// Bundles of the bundle scan: the eligible reads (no non-ACGT letter, the
+// program covered by nt_tscan.h) sorted by length, longest first (ties in
+// input order), 32 to a bundle; a bundle's T-layout is ceil(ceil(n_max / L) /
+// 64) stripes of ceil(L/2) * 64 16-byte words, and must stay below 2^31 bytes
+// (the scan's buffer offsets): reads longer than that stay out.
+int nt_bundle_plan(nt_ctx* ctx, const uint32_t* len, const uint8_t* has_exc, uint64_t n_reads,
+                   uint32_t* bnd_read, uint64_t* bnd_stripe, uint64_t* n_bundles, uint32_t* list,
+                   uint64_t* n_list, uint64_t* tplane_bytes) {
+  if (!ctx || !n_bundles || !n_list || !tplane_bytes || (n_reads && (!len || !bnd_read || !bnd_stripe || !list)))
+    return NT_E_ARG;
+  if (!ctx->compiled) return fail(ctx, NT_E_STATE, "nt_compile() not called");
+  const uint64_t L = (uint64_t)ctx->prog.L, T = (L + 1) / 2;
+  const uint64_t stripe_bytes = T * 64 * 16;
+  const uint64_t max_stripes = ((1ull << 31) - 1) / stripe_bytes;
+  const bool ok = nt_tscan_eligible(ctx->prog);
+  std::vector<uint32_t> in;
+  in.reserve(n_reads);
+  uint64_t nl = 0;
+  for (uint64_t r = 0; r < n_reads; ++r) {
+    const uint64_t st = ((len[r] + L - 1) / L + 63) / 64;
+    if (ok && len[r] > 0 && !(has_exc && has_exc[r]) && st <= max_stripes) in.push_back((uint32_t)r);
+    else list[nl++] = (uint32_t)r;
+  }
+  std::stable_sort(in.begin(), in.end(), [&](uint32_t a, uint32_t b) { return len[a] > len[b]; });
+  const uint64_t nb = (in.size() + NT_BUNDLE - 1) / NT_BUNDLE;
+  uint64_t g = 0;
+  for (uint64_t b = 0; b < nb; ++b) {
+    bnd_stripe[b] = g;
+    for (uint64_t s = 0; s < NT_BUNDLE; ++s) {
+      const uint64_t i = b * NT_BUNDLE + s;
+      bnd_read[i] = i < in.size() ? in[i] : 0xFFFFFFFFu;
+    }
+    const uint64_t nmax = len[in[b * NT_BUNDLE]];
+    g += ((nmax + L - 1) / L + 63) / 64;
+  }
+  bnd_stripe[nb] = g;
+  *n_bundles = nb;
+  *n_list = nl;
+  *tplane_bytes = g * stripe_bytes;
+  return NT_OK;
+}
+
+int nt_bundle_layout(nt_ctx* ctx, const nt_batch* batch, uint32_t* tplanes, uint64_t tplane_bytes) {
+  if (!ctx || !batch || (batch->n_bundles && !tplanes)) return NT_E_ARG;
+  if (!ctx->compiled) return fail(ctx, NT_E_STATE, "nt_compile() not called");
+  if (batch->n_bundles == 0) return NT_OK;
+  (void)hipSetDevice(ctx->device);
+  hipError_t e = hipMemsetAsync(tplanes, 0, tplane_bytes, ctx->stream);
+  if (e != hipSuccess) return hip_fail(ctx, e, "hipMemsetAsync(tplanes)");
+  NtBatch B{batch->planes, batch->blk_off, batch->len, batch->win_off, nullptr, nullptr, nullptr, batch->n_reads,
+            nullptr, 0, tplanes, batch->bnd_read, batch->bnd_stripe, batch->n_bundles};
+  e = nt_dev_launch_bundle(&B, tplanes, ctx->prog.L, ctx->stream, ctx->cu_count);
+  return e == hipSuccess ? NT_OK : hip_fail(ctx, e, "launch nt_bundle_kernel");
 }
 
 int nt_set_profiling(nt_ctx* ctx, int on) {
@@ -821,7 +912,7 @@ int64_t nt_kernel_times(nt_ctx* ctx, double* scan_ms, double* call_ms) {
 // Pack a host chunk (2-bit planes + exception lists, --rc fused) and upload
 // it to the context's device buffers; B describes the device batch.
 static int upload_reads(nt_ctx* ctx, const char* const* seqs, const uint64_t* lens, uint64_t n_reads,
-                        nt_batch* B, uint64_t* max_len) {
+                        nt_batch* B, uint64_t* max_len, bool want_bundles) {
   const int L = ctx->prog.L;
   if (n_reads && (!seqs || !lens)) return fail(ctx, NT_E_ARG, "null reads");
   (void)hipSetDevice(ctx->device);
@@ -900,13 +991,46 @@ static int upload_reads(nt_ctx* ctx, const char* const* seqs, const uint64_t* le
     // the exception lists are pageable vectors: finish their copies before they go
     if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess) return hip_fail(ctx, e, "hipStreamSynchronize");
   }
+  // the bundle layout of the batch (bundle scan), built on the device
+  uint64_t nb = 0, nl = 0, tpb = 0;
+  std::vector<uint32_t> h_bread, h_list;
+  std::vector<uint64_t> h_bstripe;
+  if (ctx->tjit_fn && want_bundles) {
+    std::vector<uint8_t> hx(n_reads);
+    for (uint64_t r = 0; r < n_reads; ++r) hx[r] = cnt[r] > 0;
+    h_bread.resize((n_reads + NT_BUNDLE - 1) / NT_BUNDLE * NT_BUNDLE + NT_BUNDLE);
+    h_bstripe.resize((n_reads + NT_BUNDLE - 1) / NT_BUNDLE + 2);
+    h_list.resize(n_reads + 1);
+    int rc = nt_bundle_plan(ctx, h_len, hx.data(), n_reads, h_bread.data(), h_bstripe.data(), &nb, h_list.data(),
+                            &nl, &tpb);
+    if (rc) return rc;
+    h_bread.resize(nb * NT_BUNDLE);
+    h_bstripe.resize(nb + 1);
+    h_list.resize(nl);
+  }
+  if (nb) {
+    NT_UP(bnd_read, h_bread);
+    NT_UP(bnd_stripe, h_bstripe);
+    if (nl) { NT_UP(list, h_list); }
+    if ((e = ctx->tplanes.ensure(tpb)) != hipSuccess) return hip_fail(ctx, e, "hipMalloc(tplanes)");
+    // the vectors are pageable: finish their copies before they go
+    if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess) return hip_fail(ctx, e, "hipStreamSynchronize");
+  }
 #undef NT_UP
 #undef NT_UP_PTR
   *B = nt_batch{(const uint32_t*)ctx->planes.p, (const uint64_t*)ctx->blk_off.p,
                 (const uint32_t*)ctx->len.p, (const uint64_t*)ctx->win_off.p,
                 te ? (const uint32_t*)ctx->exc_off.p : nullptr,
                 te ? (const uint32_t*)ctx->exc_pos.p : nullptr,
-                te ? (const uint8_t*)ctx->exc_code.p : nullptr, n_reads, tw};
+                te ? (const uint8_t*)ctx->exc_code.p : nullptr, n_reads, tw,
+                nb ? (const uint32_t*)ctx->tplanes.p : nullptr,
+                nb ? (const uint32_t*)ctx->bnd_read.p : nullptr,
+                nb ? (const uint64_t*)ctx->bnd_stripe.p : nullptr, nb,
+                nl && nb ? (const uint32_t*)ctx->list.p : nullptr, nb ? nl : 0};
+  if (nb) {
+    const int rc = nt_bundle_layout(ctx, B, (uint32_t*)ctx->tplanes.p, tpb);
+    if (rc) return rc;
+  }
   *max_len = ml;
   return NT_OK;
 }
@@ -927,7 +1051,8 @@ int nt_filter_call(nt_ctx* ctx, const nt_batch* batch, uint8_t* keep) {
   if (batch->n_reads == 0) return NT_OK;
   (void)hipSetDevice(ctx->device);
   NtBatch B{batch->planes, batch->blk_off, batch->len, batch->win_off,
-            batch->exc_off, batch->exc_pos, batch->exc_code, batch->n_reads};
+            batch->exc_off, batch->exc_pos, batch->exc_code, batch->n_reads,
+            nullptr, 0, nullptr, nullptr, nullptr, 0};
   const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((batch->n_reads + 255) / 256, (uint64_t)ctx->cu_count * 16));
   const hipError_t e = nt_dev_launch_filter(ctx->prog_dev, &B, keep, filter_threshold(ctx->prog.min_density),
                                             ctx->prog.right_edge, (int)grid, ctx->stream);
@@ -942,7 +1067,7 @@ int nt_filter_host(nt_ctx* ctx, const char* const* seqs, const uint64_t* lens, u
   if (n_reads == 0) return NT_OK;
   nt_batch B;
   uint64_t ml = 0;
-  int rc = upload_reads(ctx, seqs, lens, n_reads, &B, &ml);
+  int rc = upload_reads(ctx, seqs, lens, n_reads, &B, &ml, false);
   if (rc) return rc;
   hipError_t e;
   if ((e = ctx->flags.ensure(n_reads)) != hipSuccess) return hip_fail(ctx, e, "hipMalloc(flags)");
@@ -962,7 +1087,8 @@ int nt_analyze_host(nt_ctx* ctx, const char* const* seqs, const uint64_t* lens, 
   const int np = ctx->prog.n_pass;
   nt_batch B;
   uint64_t ml = 0;
-  int rc = upload_reads(ctx, seqs, lens, n_reads, &B, &ml);
+  // bundles only when the scan will use them (no hit counters requested)
+  int rc = upload_reads(ctx, seqs, lens, n_reads, &B, &ml, hits == nullptr);
   if (rc) return rc;
   const uint64_t tw = B.n_windows;
   hipError_t e;

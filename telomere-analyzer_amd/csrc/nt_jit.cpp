@@ -29,6 +29,7 @@ namespace {
 struct JitEntry {
   hipModule_t mod = nullptr;
   hipFunction_t fn[4] = {};  // [no hits ? 2 : 0] + [global scratch ? 1 : 0]
+  hipFunction_t tfn = nullptr;  // the bundle scan (nt_tscan.h), when the program has one
   std::string err;
 };
 
@@ -41,6 +42,26 @@ std::string pat_type(const NtPat& P) {
   return s + ">";
 }
 
+}  // namespace
+
+// The bundle scan (nt_tscan.h) covers programs whose patterns share one length
+// m >= 2 and whose TVRs share one length, with subseq_length L <= 170 (8-bit
+// window counts of the transposed output) and 2 (max m - 1) < L (the read's
+// last window, recounted by the calling kernel, holds every position whose
+// letters reach past the read end).  Others take the per-read scan only.
+bool nt_tscan_eligible(const NtProgram& P) {
+  if (P.n_pat < 1 || P.L > 170) return false;
+  int mp = P.pat[0].m, mt = P.n_tvr ? P.tvr[0].m : 0;
+  for (int i = 1; i < P.n_pat; ++i)
+    if (P.pat[i].m != mp) return false;
+  for (int i = 1; i < P.n_tvr; ++i)
+    if (P.tvr[i].m != mt) return false;
+  const int M = mp > mt ? mp : mt;
+  return mp >= 2 && 2 * (M - 1) < P.L;
+}
+
+namespace {
+
 std::string jit_source(const NtProgram& P) {
   std::string pats, tvrs;
   for (int i = 0; i < P.n_pat; ++i) pats += (i ? ", " : "") + pat_type(P.pat[i]);
@@ -52,8 +73,23 @@ std::string jit_source(const NtProgram& P) {
   s += "typedef __hip_internal::uint64_t uint64_t;\n";
   s += "typedef __hip_internal::int32_t int32_t;\n";
   s += "typedef __hip_internal::int64_t int64_t;\n";
-  s += "#include \"nt_scan.h\"\n";
+  s += "#include \"nt_tscan.h\"\n";
   s += "using JitSet = nt::CtSet<nt::CtList<" + pats + ">, nt::CtList<" + tvrs + ">>;\n";
+  if (nt_tscan_eligible(P)) {
+    s += "using TPats = nt::CtList<" + pats + ">;\nusing TTvrs = nt::CtList<" + tvrs + ">;\n";
+    s += "using TJit = nt::TProg<TPats, TTvrs, " + std::to_string(P.L) + ">;\n";
+    s += R"(
+#ifndef NT_TSCAN_WAVES_EU
+#define NT_TSCAN_WAVES_EU 3
+#endif
+extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT_TSCAN_WAVES_EU)))
+nt_tscan_jit(NtBatch B, NtOut O, uint64_t* __restrict__ tmask, unsigned long long* __restrict__ queue,
+             uint32_t thr_full) {
+  __shared__ uint32_t tsl[4 * nt::kTsLdsWords];
+  nt::tscan_bundles<TJit, TPats, TTvrs>(B, O, tmask, queue, thr_full, tsl + (threadIdx.x >> 6) * nt::kTsLdsWords);
+}
+)";
+  }
   s += R"(
 #ifdef NT_SCAN_WAVES_EU
 #define NT_SCAN_ATTR __attribute__((amdgpu_waves_per_eu(NT_SCAN_WAVES_EU)))
@@ -89,9 +125,9 @@ NT_JIT_KERNELS(nt_scan_jit_nh, false)
 
 bool compile(int device, const std::string& src, JitEntry& e) {
   hiprtcProgram prog;
-  const char* hdrs[] = {kJitCommon, kJitDevice, kJitScan};
-  const char* names[] = {"nt_common.h", "nt_device.h", "nt_scan.h"};
-  if (hiprtcCreateProgram(&prog, src.c_str(), "nt_scan_jit.hip", 3, hdrs, names) != HIPRTC_SUCCESS) {
+  const char* hdrs[] = {kJitCommon, kJitDevice, kJitScan, kJitTScan};
+  const char* names[] = {"nt_common.h", "nt_device.h", "nt_scan.h", "nt_tscan.h"};
+  if (hiprtcCreateProgram(&prog, src.c_str(), "nt_scan_jit.hip", 4, hdrs, names) != HIPRTC_SUCCESS) {
     e.err = "hiprtcCreateProgram failed";
     return false;
   }
@@ -142,6 +178,9 @@ bool compile(int device, const std::string& src, JitEntry& e) {
     e.err = std::string("hipModuleLoadData: ") + hipGetErrorString(he);
     return false;
   }
+  if (src.find("nt_tscan_jit(") != std::string::npos &&
+      hipModuleGetFunction(&e.tfn, e.mod, "nt_tscan_jit") != hipSuccess)
+    e.tfn = nullptr;
   return true;
 }
 
@@ -150,7 +189,8 @@ bool compile(int device, const std::string& src, JitEntry& e) {
 // Returns true with the four kernels of the program's pattern set (fn[i]:
 // i = [no hit counters ? 2 : 0] + [global scratch ? 1 : 0]), false (and a
 // message) when specialisation is off or failed.
-bool nt_jit_get(int device, const NtProgram& P, void* fn[4], std::string& err) {
+bool nt_jit_get(int device, const NtProgram& P, void* fn[4], void** tfn, std::string& err) {
+  if (tfn) *tfn = nullptr;
   const char* env = std::getenv("NT_JIT");
   if (env && env[0] == '0') {
     err = "NT_JIT=0";
@@ -171,7 +211,16 @@ bool nt_jit_get(int device, const NtProgram& P, void* fn[4], std::string& err) {
     return false;
   }
   for (int i = 0; i < 4; ++i) fn[i] = (void*)it->second.fn[i];
+  if (tfn) *tfn = (void*)it->second.tfn;
   return true;
+}
+
+hipError_t nt_tjit_launch(void* fn, int grid, hipStream_t stream, const NtBatch* B, const NtOut* O,
+                          uint64_t* tmask, unsigned long long* queue, uint32_t thr_full) {
+  NtBatch b = *B;
+  NtOut o = *O;
+  void* args[] = {&b, &o, &tmask, &queue, &thr_full};
+  return hipModuleLaunchKernel((hipFunction_t)fn, (unsigned)grid, 1, 1, 256, 1, 1, 0, stream, args, nullptr);
 }
 
 hipError_t nt_jit_launch(void* fn, int grid, size_t lds_bytes, hipStream_t stream,

@@ -662,6 +662,31 @@ __device__ __forceinline__ int search_left(const Lane& c, const Pw<K>& w, int st
   return new_start;
 }
 
+// The last window of a read scanned by the bundle scan (nt_tscan.h): that scan
+// does not mask the read ends, so the window holding them -- whose width may
+// differ from L, and into which split_telo may have merged a short last block
+// (NanoTel.R:199-227) -- is recounted here from the read's own planes (exact
+// out-of-bound rule at the end), and its window count, the checkpoint at
+// window nw (the read's total, when nw is a multiple of 16) and its bit of the
+// telomeric bitmask (threshold of its own width) are rewritten.  Idempotent
+// for reads of the per-read scan.
+__device__ __forceinline__ void call_fix_last(Lane& c, const uint32_t* __restrict__ thr, uint32_t thr_size) {
+  if (c.nw <= 0) return;
+  const int last = c.nw - 1, a = last * c.L;
+  const int exact = cov_count(c, a, c.n - 1);
+  const int old = c.cnt[last];
+  if (exact != old) {
+    const_cast<uint16_t*>(c.cnt)[last] = (uint16_t)exact;
+    if ((c.nw & 15) == 0) const_cast<uint32_t*>(c.ck)[c.nw >> 4] += (uint32_t)(exact - old);
+  }
+  const uint32_t w = (uint32_t)(c.n - a);
+  const bool tel = (uint32_t)exact >= thr[w < thr_size ? w : thr_size - 1];
+  uint64_t* tw = const_cast<uint64_t*>(c.tm) + (last >> 6);
+  const uint64_t m = 1ull << (last & 63), x = *tw;
+  const uint64_t y = tel ? (x | m) : (x & ~m);
+  if (y != x) *tw = y;
+}
+
 // find_telo_position_wraper (NanoTel.R:1080-1155) + density (NanoTel.R:1840).
 __device__ __forceinline__ void call_pass(Lane& c, int& out_s, int& out_e, double& out_d, uint32_t& err) {
   tm_preload(c);
@@ -748,7 +773,8 @@ __device__ __forceinline__ void call_pass(Lane& c, int& out_s, int& out_e, doubl
 #define NT_CALL_ATTR __attribute__((amdgpu_waves_per_eu(NT_CALL_WAVES_PER_EU)))
 __global__ void __launch_bounds__(256) NT_CALL_ATTR
 nt_call_kernel(const NtProgram* __restrict__ prog, NtBatch B, NtOut O,
-               const uint64_t* __restrict__ tmask) {
+               const uint64_t* __restrict__ tmask, const uint32_t* __restrict__ thr, uint32_t thr_size,
+               int fix_last) {
   const int np = prog->n_pass, L = prog->L;
 #if NT_CALL_TM_LDS
   __shared__ uint64_t tm_lds[kTmRegs * 256];
@@ -806,6 +832,7 @@ nt_call_kernel(const NtProgram* __restrict__ prog, NtBatch B, NtOut O,
         c.k = p == 0 ? 0 : 1;
         c.use_tvr = p == 2;
         c.raw = p == 0 && prog->raw_p1;
+        if (fix_last) call_fix_last(c, thr, thr_size);
         call_pass(c, s, e, d, flags);
         if (s == -1) flags |= 1u << (NT_FLAG_NA_SHIFT + p);
         w = e - s + 1;
@@ -884,6 +911,58 @@ nt_layout_kernel(uint64_t n_reads, uint64_t nblk, uint64_t read_len, uint64_t nw
     blk_off[r] = r * nblk;
     len[r] = (uint32_t)read_len;
     win_off[r] = r * nw;
+  }
+}
+
+// ================================================================ bundles
+//
+// The T-layout of the bundle scan (nt_common.h) from the per-read planes: one
+// wave per (bundle, 32 positions): lane s < 32 holds slot s's low-plane word,
+// lane 32 + s its high-plane word, so ballot(bit i) is the {lo, hi} pair of
+// position 32x + i for all 32 reads -- 32 ballots transpose the 32 x 32 bit
+// blocks of both planes.  Positions past a read (and empty slots) are 0.
+// (the wait states: see writelane in nt_tscan.h)
+template <int kLane>
+__device__ __forceinline__ void writelane_k(uint32_t& v, uint32_t x) {
+  asm volatile("s_nop 4\n\tv_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(x), "i"(kLane));
+}
+
+__global__ void __launch_bounds__(256)
+nt_bundle_kernel(NtBatch B, uint32_t* __restrict__ tp, int L) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const uint64_t T = (uint64_t)(L + 1) / 2;
+  const uint64_t W = (uint64_t)gridDim.x * kNWaves;
+  const uint64_t w0 = (uint64_t)blockIdx.x * kNWaves + (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  for (uint64_t b = w0; b < B.n_bundles; b += W) {
+    const uint32_t r = B.bnd_read[b * NT_BUNDLE + (lane & 31)];
+    const bool occ = r != 0xFFFFFFFFu;
+    const uint32_t len = occ ? B.len[r] : 0u;
+    const uint64_t boff = occ ? B.blk_off[r] : 0ull;
+    const uint32_t nmax = (uint32_t)__builtin_amdgcn_readfirstlane((int)len);  // slot 0 = longest
+    const uint64_t g0 = uniform_u64(B.bnd_stripe[b]);
+    const uint64_t npos = (uint64_t)((nmax + L - 1) / L) * L;  // positions of the bundle's blocks
+    const uint2* blk = reinterpret_cast<const uint2*>(B.planes) + boff;
+    for (uint32_t x = 0; 32 * x < nmax; ++x) {
+      uint32_t wv = 0u;
+      if (32 * x < len) {
+        const uint2 v = blk[x];
+        wv = lane < 32 ? v.x : v.y;
+        if (32 * x + 32 > len) wv &= (1u << (len - 32 * x)) - 1u;
+      }
+      uint32_t lo = 0u, hi = 0u;
+      static_for<0, 32>([&](auto ii) {
+        constexpr int i = decltype(ii)::value;
+        const uint64_t bal = __ballot((wv >> i) & 1u);
+        writelane_k<i>(lo, (uint32_t)bal);
+        writelane_k<i>(hi, (uint32_t)(bal >> 32));
+      });
+      const uint64_t q = 32ull * x + lane;
+      if (lane < 32 && q < npos) {
+        const uint64_t kq = q / (uint64_t)L, o = q - kq * L;
+        const uint64_t word = (g0 + (kq >> 6)) * T * kWave + (o >> 1) * kWave + (kq & 63);  // 16-byte words
+        reinterpret_cast<uint2*>(tp)[word * 2 + (o & 1)] = make_uint2(lo, hi);
+      }
+    }
   }
 }
 
@@ -978,7 +1057,8 @@ nt_filter_kernel(const NtProgram* __restrict__ prog, NtBatch B, uint8_t* __restr
 extern "C" {
 
 hipError_t nt_dev_launch_call(const NtProgram* prog, const NtBatch* B, const NtOut* O,
-                              const uint64_t* tmask, int call_grid, hipStream_t stream);
+                              const uint64_t* tmask, const uint32_t* thr, uint32_t thr_size, int fix_last,
+                              int call_grid, hipStream_t stream);
 
 // per-wave scan scratch words for reads with at most nw_cap windows
 uint32_t nt_dev_wave_words(int single, int n_hits, int np, uint32_t nw_cap) {
@@ -1037,7 +1117,7 @@ hipError_t nt_dev_launch(const NtProgram* prog, const uint32_t* thr, const NtBat
   if (!done) return hipErrorInvalidValue;
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || call_grid <= 0) return e;
-  return nt_dev_launch_call(prog, B, O, tmask, call_grid, stream);
+  return nt_dev_launch_call(prog, B, O, tmask, thr, 0, 0, call_grid, stream);
 }
 
 // resident 256-thread blocks per CU of the scan variant (grid sizing)
@@ -1057,8 +1137,18 @@ int nt_dev_scan_blocks_per_cu(int single, int one, int m6, int lds, size_t lds_b
 }
 
 hipError_t nt_dev_launch_call(const NtProgram* prog, const NtBatch* B, const NtOut* O,
-                              const uint64_t* tmask, int call_grid, hipStream_t stream) {
-  hipLaunchKernelGGL(nt::nt_call_kernel, dim3(call_grid), dim3(256), 0, stream, prog, *B, *O, tmask);
+                              const uint64_t* tmask, const uint32_t* thr, uint32_t thr_size, int fix_last,
+                              int call_grid, hipStream_t stream) {
+  hipLaunchKernelGGL(nt::nt_call_kernel, dim3(call_grid), dim3(256), 0, stream, prog, *B, *O, tmask, thr,
+                     thr_size, fix_last);
+  return hipGetLastError();
+}
+
+hipError_t nt_dev_launch_bundle(const NtBatch* B, uint32_t* tp, int L, hipStream_t stream, int cu_count) {
+  uint64_t grid = (B->n_bundles + 3) / 4;
+  if (grid > (uint64_t)cu_count * 8) grid = (uint64_t)cu_count * 8;
+  if (grid == 0) grid = 1;
+  hipLaunchKernelGGL(nt::nt_bundle_kernel, dim3((uint32_t)grid), dim3(256), 0, stream, *B, tp, L);
   return hipGetLastError();
 }
 

@@ -331,6 +331,7 @@ struct GenericSet {  // any program: run-time lists
 template <int M, int... TT>
 struct CtPat {
   static constexpr int kM = M;
+  static constexpr int kTT[sizeof...(TT)] = {TT...};  // letter truth tables (nt_tscan.h)
   const NtPat* P;  // run-time twin (exception fix-ups)
   __device__ __forceinline__ int m() const { return M; }
   __device__ __forceinline__ uint32_t E(int j, uint32_t L, uint32_t H) const {
@@ -586,6 +587,7 @@ constexpr int kRing = NT_RING;  // prefetch depth in chunks (tuning knob)
 #define NT_WOFF_UNIFORM 0  // tuning knob (c10k 2 % slower with it)
 #endif
 struct ReadMeta {
+  uint64_t rid;         // read index (B.list[r] or r)
   uint32_t len;
   uint64_t boff, woff;  // block offset (uniform), window offset
   uint32_t e0, e1;      // exception list range (0, 0 without exceptions)
@@ -602,8 +604,10 @@ __device__ __forceinline__ uint64_t uniform_u64(uint64_t x) {
 }
 
 // The per-read metadata, all loads independent (one memory round trip).
-__device__ __forceinline__ ReadMeta load_meta(const NtBatch& B, uint64_t r) {
+__device__ __forceinline__ ReadMeta load_meta(const NtBatch& B, uint64_t i) {
   ReadMeta m;
+  const uint64_t r = B.list ? (uint64_t)B.list[i] : i;
+  m.rid = r;
   m.len = B.len[r];
   m.boff = uniform_u64(B.blk_off[r]);  // uniform: SGPR base
 #if NT_WOFF_UNIFORM
@@ -642,7 +646,7 @@ __device__ __forceinline__ void scan_reads(const NtProgram* __restrict__ prog,
   // per claim, 1.18 ms with the 8 queues).  A static round-robin share of
   // the reads before the queues (`nstatic` per wave, tuning) measured slower
   // at every fraction tried (1M x 50 kb: 5.1 ms at 3/4 static, 3.8 ms at 0).
-  const uint64_t nR = B.n_reads;
+  const uint64_t nR = B.list ? B.n_list : B.n_reads;  // queue positions (list entries)
   const uint64_t W = (uint64_t)gridDim.x * kNWaves;
   const uint64_t w = (uint64_t)blockIdx.x * kNWaves + (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const uint64_t st_n = (uint64_t)nstatic * W < nR ? nstatic : nR / W;
@@ -690,7 +694,7 @@ __device__ __forceinline__ void scan_reads(const NtProgram* __restrict__ prog,
     const bool skip = m.len <= len_lo || m.len > len_hi;
     const bool skip_n = rn >= nR || mn.len <= len_lo || mn.len > len_hi || (mn.boff & 1u);
     if (!skip && (m.boff & 1u)) {  // layout contract: 16-byte aligned segments
-      if (lane == 0) O.flags[r] = NT_FLAG_ERR_ALIGN;
+      if (lane == 0) O.flags[m.rid] = NT_FLAG_ERR_ALIGN;
     } else if (!skip) {
     const uint32_t n32 = m.len;
     const uint64_t boff = m.boff;
@@ -809,9 +813,9 @@ __device__ __forceinline__ void scan_reads(const NtProgram* __restrict__ prog,
       thr_last = thr[wl < tsz ? wl : tsz - 1];
     }
     const int nmw = aux_nmw(nw), nck = aux_nck(nw);
-    uint64_t* tmo = tmask + aux_base(m.woff, r, np);
+    uint64_t* tmo = tmask + aux_base(m.woff, m.rid, np);
     uint32_t* cko = reinterpret_cast<uint32_t*>(tmo + np * nmw);
-    const uint64_t ab = aux_base(m.woff, r, np);
+    const uint64_t ab = aux_base(m.woff, m.rid, np);
     // passes 0 and 1 together from the packed running counts (one LDS read
     // per window boundary), pass 2 after them
     for (int j = lane; j < nck; j += kWave) {
@@ -871,12 +875,12 @@ __device__ __forceinline__ void scan_reads(const NtProgram* __restrict__ prog,
 #pragma unroll
         for (int c = 0; c < S::kNHits; ++c) {
           const uint32_t v = wave_sum_u32(lane < kOwned ? st.acc[c] : 0u);
-          if (lane == 0) O.hits[r * (uint64_t)nh + c] = v;
+          if (lane == 0) O.hits[m.rid * (uint64_t)nh + c] = v;
         }
       } else {
         for (int c = 0; c < nh; ++c) {
           const uint32_t v = wave_sum_u32(lane < kOwned ? hitacc[c * kWave + lane] : 0u);
-          if (lane == 0) O.hits[r * (uint64_t)nh + c] = v;
+          if (lane == 0) O.hits[m.rid * (uint64_t)nh + c] = v;
         }
       }
     }

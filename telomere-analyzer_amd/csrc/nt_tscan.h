@@ -1,0 +1,776 @@
+// nt_tscan.h -- the bundle scan ("T-scan") of the NanoTel hot path on gfx950.
+//
+// The same outputs as scan_reads (nt_scan.h): per read and pass the covered
+// bases of every subseq_length window (analyze_subtelos / get_density_iranges
+// / get_sub_density, NanoTel.R:717-766, 308-397, 449-468), the telomeric-window
+// bitmask (class -5, NanoTel.R:749-758) and the running-count checkpoints the
+// calling kernel sums with -- computed from the T-layout (nt_common.h): reads
+// grouped 32 to a BUNDLE, every plane word holding ONE position of all 32
+// reads (bit s = slot s).  A shift by one position is then a register rename,
+// and the whole walk -- the letter tests of matchPattern, the 3-letter
+// majority combine (<= 1 mismatch, Biostrings' out-of-bound rule), the
+// coverage spread (trim + IRanges::reduce) and the per-window counts
+// (bit-sliced carry-save adders) -- is plain 3-input bit logic, which gfx950
+// issues at full rate (v_bitop3 / v_and / v_or / v_xor), where the per-read
+// layout spends its instructions on funnel shifts, DPP neighbour moves and
+// popcounts, all of them half rate (tools/valu_issue_bench.hip).
+//
+// Work split.  A wave claims a bundle from the per-XCD queues and walks its
+// stripes: lane k of stripe st owns block 64 st + k = positions [kL, kL + L),
+// i.e. split_telo window k of every read.  It walks positions [kL - H,
+// (k+1) L + H) (H = longest pattern - 1; the left halo feeds the coverage of
+// the block's first bases, the right halo the letter tests of its last
+// starts), fully unrolled at compile time (L and the patterns are baked into
+// the hiprtc build), and counts the covered bases of its block into 8 bit
+// planes per pass (acc[b] bit s = bit b of read s's count; counts <= L <= 170).
+//
+// Output, lane = window: the planes are transposed 8x8 within every byte, so
+// that a read's count is one shift-and-mask; the counts are stored as uint16
+// (one coalesced store per read: 64 windows x 2 bytes), the telomeric bits as
+// one ballot per read (count >= thr[L]), the checkpoints every 16 windows
+// from packed row sums.  The read ends are not masked (the T-layout holds A
+// past a read), so the LAST window of every read -- whose width may differ
+// from L, and into which split_telo may have merged a short last block
+// (NanoTel.R:220) -- is recounted exactly by the calling kernel from the
+// per-read planes (call_fix_last, nt_kernels.hip).
+#pragma once
+#include "nt_scan.h"
+
+namespace nt {
+
+// 3-input logic as v_bitop3 (full rate; hipcc picks the half-rate v_or3_b32
+// for a | b | c)
+__device__ __forceinline__ uint32_t or3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0xFE);
+}
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+__device__ __forceinline__ uint32_t and3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x80);
+}
+__device__ __forceinline__ uint32_t mj3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8);
+}
+
+// ----------------------------------------------------- compile-time lists
+
+constexpr int cmax() { return 0; }
+template <class... T>
+constexpr int cmax(int a, T... r) {
+  return a > cmax(r...) ? a : cmax(r...);
+}
+constexpr int cmin() { return 1 << 30; }
+template <class... T>
+constexpr int cmin(int a, T... r) {
+  return a < cmin(r...) ? a : cmin(r...);
+}
+
+template <class List>
+struct LInfo;
+template <class... P>
+struct LInfo<CtList<P...>> {
+  static constexpr int kN = sizeof...(P);
+  static constexpr int kMax = cmax(P::kM...);
+  static constexpr int kMin = cmin(P::kM...);
+};
+template <class List, int I>
+struct LAt;
+template <int I, class... P>
+struct LAt<CtList<P...>, I> {
+  using type = typename CtAt<I, P...>::type;
+};
+
+// Exact (a0) and <= 1 mismatch (a1) of one start from its kM letter words:
+// letters in groups of three, each group (all three, at least two) by one
+// v_bitop3 apiece, the groups chained with x1 = two & x1 & (all | x0) (= the
+// (x1 & all) | (x0 & two) of combine(), as x0 <= x1 and all <= two).
+template <int kM, bool kExact>
+__device__ __forceinline__ void tcombine(const uint32_t* q, uint32_t& a0, uint32_t& a1) {
+  if constexpr (kExact) {
+    uint32_t x = q[0];
+    int j = 1;
+    for (; j + 2 <= kM; j += 2) x = and3(x, q[j], q[j + 1]);
+    if (j < kM) x &= q[j];
+    a0 = x;
+    a1 = 0u;
+  } else {
+    uint32_t x0 = 0u, x1 = 0u;
+#pragma unroll
+    for (int g = 0; g < kM; g += 3) {
+      const int n = kM - g < 3 ? kM - g : 3;
+      uint32_t all, two;
+      if (n == 3) {
+        all = and3(q[g], q[g + 1], q[g + 2]);
+        two = mj3(q[g], q[g + 1], q[g + 2]);
+      } else if (n == 2) {
+        all = q[g] & q[g + 1];
+        two = q[g] | q[g + 1];
+      } else {
+        all = q[g];
+        two = 0xFFFFFFFFu;
+      }
+      if (g == 0) {
+        x0 = all;
+        x1 = two;
+      } else {
+        x1 = (n == 1) ? (x1 & (all | x0)) : and3(two, x1, all | x0);
+        x0 &= all;
+      }
+    }
+    a0 = x0;
+    a1 = x1;
+  }
+}
+
+// ------------------------------------------------------ the bundle program
+
+// Pats / Tvrs: CtList<CtPat<m, tt...>...> (every pattern of a list the same
+// length: the host routes other programs to scan_reads); kL: subseq_length.
+template <class Pats, class Tvrs, int kL_>
+struct TProg {
+  static constexpr int kL = kL_;
+  static constexpr int kNPat = LInfo<Pats>::kN, kNTvr = LInfo<Tvrs>::kN;
+  static constexpr int kMP = LInfo<Pats>::kMax, kMT = kNTvr ? LInfo<Tvrs>::kMax : 0;
+  static constexpr int kNP = kNTvr ? 3 : 2;
+  static constexpr int kM = kMP > kMT ? kMP : kMT;
+  static constexpr int kH = kM - 1;               // halo on each side
+  static constexpr int kLam = kH + (kH & 1);      // counting lag (even: loop runs start on slot boundaries)
+  static constexpr int kNPos = kL + 2 * kH;       // positions walked per block
+  static constexpr int kT = (kL + 1) / 2;         // 16-byte slots per block
+  // slots the walk loads, in position order: block k-1 (left halo), k, k+1
+  static constexpr int kS0 = kH ? (kL - 1) / 2 - (kL - kH) / 2 + 1 : 0;
+  static constexpr int kS1 = kT;
+  static constexpr int kS2 = kH ? (kH - 1) / 2 + 1 : 0;
+  static constexpr int kNS = kS0 + kS1 + kS2;
+  // position index i of the walk -> block (-1, 0, +1), offset in the block
+  static constexpr int rel(int i) { return i < kH ? -1 : (i < kH + kL ? 0 : 1); }
+  static constexpr int off(int i) { return i < kH ? kL - kH + i : (i < kH + kL ? i - kH : i - kH - kL); }
+  static constexpr int fslot(int i) {  // walk slot of position i
+    return rel(i) < 0 ? off(i) / 2 - (kL - kH) / 2 : (rel(i) == 0 ? kS0 + off(i) / 2 : kS0 + kS1 + off(i) / 2);
+  }
+  static constexpr int slot_rel(int f) { return f < kS0 ? -1 : (f < kS0 + kS1 ? 0 : 1); }
+  static constexpr int slot_t(int f) { return f < kS0 ? (kL - kH) / 2 + f : (f < kS0 + kS1 ? f - kS0 : f - kS0 - kS1); }
+  static constexpr int first_pos(int f) {  // first walk position that reads slot f
+    int i = 0;
+    while (i < kNPos && fslot(i) != f) ++i;
+    return i;
+  }
+};
+
+// Widths of the sliding-OR stages of the coverage spread for pattern length
+// m: w_0 = 1, each stage at most triples the width (one v_bitop3 per position
+// and stage; TTAGGG: 1 -> 3 -> 6).
+template <int kM>
+struct Spread {
+  static constexpr int width(int s) {
+    int w = 1;
+    for (int t = 0; t < s; ++t) w = 3 * w <= kM ? 3 * w : kM;
+    return w;
+  }
+  static constexpr int stages() {
+    int s = 0;
+    while (width(s) < kM) ++s;
+    return s;
+  }
+  static constexpr int kS = stages();
+};
+
+// Bit-sliced counter of 1-bit words (one per position; bit s = slot s):
+// acc[b] bit s = bit b of slot s's count.  Levels 0..3 add their words in
+// carry-save pairs with the level's accumulator (xor3 / majority: one
+// v_bitop3 each), the pair's carry is a word of the next level; level 4 and
+// up add by ripple (one word per 16 positions).  Push indices are per run.
+struct BitCount {
+  uint32_t acc[8];
+  uint32_t pend[4];
+  template <int Lvl>
+  __device__ __forceinline__ void ripple(uint32_t x) {
+#pragma unroll
+    for (int l = Lvl; l < 8; ++l) {
+      const uint32_t c = acc[l] & x;
+      acc[l] ^= x;
+      x = c;
+    }
+  }
+  template <int Lvl, int Idx>
+  __device__ __forceinline__ void push(uint32_t x) {
+    if constexpr (Lvl >= 4) {
+      ripple<Lvl>(x);
+    } else if constexpr (Idx % 2 == 0) {
+      pend[Lvl] = x;
+    } else {
+      const uint32_t a = pend[Lvl], c = acc[Lvl];
+      acc[Lvl] = xor3(a, x, c);
+      push<Lvl + 1, Idx / 2>(mj3(a, x, c));
+    }
+  }
+  // the run pushed Cnt words at level Lvl: fold a pending one upward
+  template <int Lvl, int Cnt>
+  __device__ __forceinline__ void flush() {
+    if constexpr (Lvl < 4) {
+      if constexpr (Cnt % 2 == 1) {
+        const uint32_t p = pend[Lvl];
+        const uint32_t c = acc[Lvl] & p;
+        acc[Lvl] ^= p;
+        push<Lvl + 1, Cnt / 2>(c);
+        flush<Lvl + 1, Cnt / 2 + 1>();
+      } else {
+        flush<Lvl + 1, Cnt / 2>();
+      }
+    }
+  }
+};
+
+// The letter truth tables a program tests (bit tt of the mask: some letter of
+// some pattern or TVR has truth table tt); each is one word per position.
+template <class List>
+struct LTests;
+template <class... P>
+struct LTests<CtList<P...>> {
+  template <class D>
+  static constexpr uint32_t one() {
+    uint32_t m = 0;
+    for (int j = 0; j < D::kM; ++j) m |= 1u << (D::kTT[j] & 15);
+    return m;
+  }
+  static constexpr uint32_t kMask = (0u | ... | one<P>());
+};
+
+// The per-lane pipeline of the walk: position by position, the letter tests
+// (one word per distinct truth table), the hits of the starts whose last
+// letter is the position (exact, <= 1 mismatch; TVRs exact), the sliding-OR
+// stages of the coverage spread and the count of the position kH back, whose
+// every covering start is then known.  Runs of N positions are unrolled; the
+// last HD values of every per-position array carry over to the next run
+// (entries no later step reads are dead).  The history holds TEST words, so
+// the out-of-bound mask of the first block exists in the prologue only.
+template <class TP, class Pats, class Tvrs>
+struct TPipe {
+  static constexpr int kM = TP::kM, kMP = TP::kMP, kMT = TP::kMT > 0 ? TP::kMT : 1;
+  static constexpr int kNTvr = TP::kNTvr, kNPat = TP::kNPat;
+  static constexpr int HD = 2 * kM;
+  static constexpr uint32_t kTests = LTests<Pats>::kMask | LTests<Tvrs>::kMask;
+  using SP = Spread<kMP>;
+  using ST = Spread<kMT>;
+  static constexpr int kSP = SP::kS, kST = ST::kS;
+  uint32_t hT[16][HD];
+  uint32_t h0[kSP + 1][HD], h1[kSP + 1][HD], ht[kST + 1][HD];
+  BitCount bc[3];
+
+  __device__ __forceinline__ void init() {
+#pragma unroll
+    for (int t = 0; t < HD; ++t) {
+#pragma unroll
+      for (int c = 0; c < 16; ++c) hT[c][t] = 0u;
+#pragma unroll
+      for (int s = 0; s <= kSP; ++s) h0[s][t] = h1[s][t] = 0u;
+#pragma unroll
+      for (int s = 0; s <= kST; ++s) ht[s][t] = 0u;
+    }
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+#pragma unroll
+      for (int b = 0; b < 8; ++b) bc[p].acc[b] = 0u;
+  }
+
+  // sliding-OR stage s at index x of a stage array (earlier entries are final)
+  template <class Sp, int s, int X, int NN>
+  __device__ __forceinline__ static uint32_t stage(const uint32_t (&w)[NN]) {
+    constexpr int a = Sp::width(s - 1), b = Sp::width(s);
+    if constexpr (3 * a <= b) return or3(w[X], w[X - a], w[X - 2 * a]);
+    else if constexpr (2 * a >= b) return w[X] | w[X - (b - a)];
+    else return or3(w[X], w[X - a], w[X - (b - a)]);
+  }
+
+  // one run of N positions; kCount: count position P - kH of every step
+  // (a run of 16 completes its carry-save pairs); kVarV: Vr masks positions
+  // get(ui) -> uint3 {lo, hi, valid mask} of position u, read at step u (after
+  // the hooks of the earlier steps: the ring slot may have been refilled)
+  template <int N, bool kCount, bool kVarV, class Get, class Hook>
+  __device__ __forceinline__ void run(Get&& get, Hook&& hook) {
+    constexpr int NN = HD + N;
+    uint32_t Ts[16][NN];
+    uint32_t a0[kSP + 1][NN], a1[kSP + 1][NN], at[kST + 1][NN];
+#pragma unroll
+    for (int t = 0; t < HD; ++t) {
+#pragma unroll
+      for (int c = 0; c < 16; ++c)
+        if ((kTests >> c) & 1u) Ts[c][t] = hT[c][t];
+#pragma unroll
+      for (int s = 0; s <= kSP; ++s) {
+        a0[s][t] = h0[s][t];
+        a1[s][t] = h1[s][t];
+      }
+#pragma unroll
+      for (int s = 0; s <= kST; ++s) at[s][t] = ht[s][t];
+    }
+    static_for<0, N>([&](auto ui) {
+      constexpr int u = decltype(ui)::value, x = HD + u;
+      const uint3 pl = get(ui);
+#pragma unroll
+      for (int c = 0; c < 16; ++c)
+        if ((kTests >> c) & 1u) Ts[c][x] = kVarV ? (tt_test(c, pl.x, pl.y) & pl.z) : tt_test(c, pl.x, pl.y);
+      hook(ui);  // the planes of position u are dead: e.g. refill its ring slot
+      {  // patterns: the start x - (kMP - 1)
+        constexpr int j0 = x - (kMP - 1);
+        uint32_t e0 = 0u, e1 = 0u;
+        static_for<0, kNPat>([&](auto pi) {
+          using D = typename LAt<Pats, decltype(pi)::value>::type;
+          uint32_t q[kMP];
+#pragma unroll
+          for (int j = 0; j < kMP; ++j) q[j] = Ts[D::kTT[j] & 15][j0 + j];
+          uint32_t b0, b1;
+          tcombine<kMP, false>(q, b0, b1);
+          e0 |= b0;
+          e1 |= b1;
+        });
+        a0[0][x] = e0;
+        a1[0][x] = e1;
+        static_for<1, kSP + 1>([&](auto si) {
+          constexpr int s = decltype(si)::value;
+          a0[s][x] = stage<SP, s, x>(a0[s - 1]);
+          a1[s][x] = stage<SP, s, x>(a1[s - 1]);
+        });
+      }
+      if constexpr (kNTvr > 0) {  // TVRs (exact): the start x - (kMT - 1)
+        constexpr int j0 = x - (kMT - 1);
+        uint32_t e = 0u;
+        static_for<0, kNTvr>([&](auto ti) {
+          using D = typename LAt<Tvrs, decltype(ti)::value>::type;
+          uint32_t q[kMT];
+#pragma unroll
+          for (int j = 0; j < kMT; ++j) q[j] = Ts[D::kTT[j] & 15][j0 + j];
+          uint32_t b0, b1;
+          tcombine<kMT, true>(q, b0, b1);
+          e |= b0;
+        });
+        at[0][x] = e;
+        static_for<1, kST + 1>([&](auto si) {
+          constexpr int s = decltype(si)::value;
+          at[s][x] = stage<ST, s, x>(at[s - 1]);
+        });
+      }
+      if constexpr (kCount) {  // the coverage of position P - kLam
+        constexpr int kLam = TP::kLam;
+        constexpr int y0 = x - (kLam + 1 - kMP);
+        const uint32_t c1 = a1[kSP][y0];
+        bc[0].template push<0, u>(a0[kSP][y0]);
+        bc[1].template push<0, u>(c1);
+        if constexpr (kNTvr > 0) {
+          constexpr int yt = x - (kLam + 1 - kMT);
+          bc[2].template push<0, u>(c1 | at[kST][yt]);
+        }
+      }
+    });
+    if constexpr (kCount) {
+      bc[0].template flush<0, N>();
+      bc[1].template flush<0, N>();
+      if constexpr (kNTvr > 0) bc[2].template flush<0, N>();
+    }
+#pragma unroll
+    for (int t = 0; t < HD; ++t) {
+#pragma unroll
+      for (int c = 0; c < 16; ++c)
+        if ((kTests >> c) & 1u) hT[c][t] = Ts[c][N + t];
+#pragma unroll
+      for (int s = 0; s <= kSP; ++s) {
+        h0[s][t] = a0[s][N + t];
+        h1[s][t] = a1[s][N + t];
+      }
+#pragma unroll
+      for (int s = 0; s <= kST; ++s) ht[s][t] = at[s][N + t];
+    }
+  }
+};
+
+#ifndef NT_TS_PIN
+#define NT_TS_PIN 1
+#endif
+// 1: the epilogue prefetches the next stripe's first slots (the ring then
+// stays live across the output stage); 0: every stripe starts with prime()
+#ifndef NT_TS_XPRIME
+#define NT_TS_XPRIME 0
+#endif
+
+// The walk of one stripe's block per lane, as a continuous stream of 16-byte
+// slots with a register ring of 8 slots (loads issued 8 slots ahead, the
+// ring slot refilled right after the tests of its last position, across the
+// prologue / loop / epilogue and into the next stripe: no dependent memory
+// round trip inside a bundle).  Block k = 64 st + lane walks P = -kLam ..
+// kL + kLam - 1 relative to its start; the counts of the covered bases of
+// [0, kL) per pass go to acc.  P < 0 of block 0 are outside every read
+// (Biostrings' out-of-bound start -1, masked in the prologue); the read ends
+// are not masked -- the T-layout holds A there -- so the calling kernel
+// recounts the last window of every read (call_fix_last).
+template <class TP, class Pats, class Tvrs>
+struct TWalker {
+  static constexpr int kL = TP::kL, kLam = TP::kLam, kT = TP::kT;
+  static constexpr int U = 16, D = 8;
+  static constexpr int PA = -kLam, PB = kLam;         // prologue positions [PA, PB)
+  static constexpr int C = (kL - kLam) / U;           // loop runs: P in [kLam + U c, + U), all < kL
+  static constexpr int P1 = kLam + U * C, P2 = kL + kLam;  // epilogue positions [P1, P2)
+  static constexpr int NP0 = PB - PA, NE = P2 - P1;
+  static constexpr int rel(int P) { return P < 0 ? -1 : (P < kL ? 0 : 1); }
+  static constexpr int off(int P) { return P - rel(P) * kL; }
+  static constexpr int key(int P) { return (rel(P) + 1) * 65536 + off(P) / 2; }
+  // slot index of position P within its static segment [a, P]
+  static constexpr int sidx(int a, int P) {
+    int j = 0;
+    for (int q = a + 1; q <= P; ++q) j += key(q) != key(q - 1);
+    return j;
+  }
+  static constexpr int NA = sidx(PA, PB - 1) + 1;      // prologue slots
+  static constexpr int NEs = sidx(P1, P2 - 1) + 1;     // epilogue slots
+  static constexpr int NS0 = NA + 8 * C + NEs;
+  static constexpr int NS = (NS0 + D - 1) / D * D;    // stream slots per stripe (padded)
+  // first position of segment slot j of the segment starting at a
+  static constexpr int spos(int a, int b, int j) {
+    for (int q = a; q < b; ++q)
+      if (sidx(a, q) == j) return q;
+    return b;
+  }
+  // static stream slot f (not a loop slot): kind 0 = slot (rel, t), 1 = pad (no load)
+  static constexpr int srel(int f) {
+    return f < NA ? rel(spos(PA, PB, f)) : (f >= NA + 8 * C && f < NS0 ? rel(spos(P1, P2, f - NA - 8 * C)) : 2);
+  }
+  static constexpr int st_(int f) {
+    return f < NA ? off(spos(PA, PB, f)) / 2 : (f >= NA + 8 * C && f < NS0 ? off(spos(P1, P2, f - NA - 8 * C)) / 2 : 0);
+  }
+
+  __amdgpu_buffer_rsrc_t rs;
+  int vb[3];   // byte offset of block k + r's slot 0 (r = -1, 0, 1) in this stripe; < 0 / past the end: zeros
+  int vbn[3];  // the same in the next stripe
+  uint4 S[D];  // the ring: stream slot f sits in S[f % D]
+  TPipe<TP, Pats, Tvrs> pp;
+
+  __device__ __forceinline__ uint4 ld(int voff, int soff) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0);
+#if NT_TS_PIN
+    __builtin_amdgcn_sched_barrier(0);  // keep the load where it is issued (8 slots ahead)
+#endif
+    return make_uint4(v[0], v[1], v[2], v[3]);
+  }
+  // load static stream slot f (of this stripe, or of the next one when f >= NS)
+  template <int F>
+  __device__ __forceinline__ void load_static() {
+    constexpr bool nxt = F >= NS;
+    constexpr int f = nxt ? F - NS : F;
+    if constexpr (f >= NA && f < NA + 8 * C) {  // a loop slot (only run 0's, from the prime)
+      constexpr int so = (kLam / 2 + (f - NA)) * 1024;
+      S[F % D] = ld(nxt ? vbn[1] : vb[1], so);
+    } else if constexpr (srel(f) == 2) {
+      S[F % D] = make_uint4(0u, 0u, 0u, 0u);
+    } else {
+      constexpr int r = srel(f), so = st_(f) * 1024;
+      S[F % D] = ld(nxt ? vbn[r + 1] : vb[r + 1], so);
+    }
+  }
+  // the first D stream slots of a bundle's first stripe
+  __device__ __forceinline__ void prime() {
+    static_for<0, D>([&](auto fi) { load_static<decltype(fi)::value>(); });
+  }
+  __device__ __forceinline__ void set_stripe(int st, int lane, bool active) {
+#pragma unroll
+    for (int r = -1; r <= 1; ++r) {
+      const int lr = lane + r;
+      const int stl = st + (lr >> 6);  // arithmetic shift: -1 for lane 0, r = -1
+      const int o = (stl * kT * kWave + (lr & (kWave - 1))) * 16;  // < 0: out of range (zeros)
+      vb[r + 1] = active ? o : -1;
+      vbn[r + 1] = active ? o + kT * kWave * 16 : -1;
+    }
+  }
+
+  // one stripe: counts into acc (the ring then holds the next stripe's first slots)
+  __device__ __forceinline__ void walk(bool first, uint32_t (&acc)[3][8]) {
+    pp.init();
+    {  // prologue: static slots
+      auto get = [&](auto ii) {
+        constexpr int i = decltype(ii)::value, P = PA + i, f = sidx(PA, P);
+        const uint4 v = S[f % D];
+        return (off(P) & 1) ? make_uint3(v.z, v.w, (P < 0 && first) ? 0u : 0xFFFFFFFFu)
+                            : make_uint3(v.x, v.y, (P < 0 && first) ? 0u : 0xFFFFFFFFu);
+      };
+      pp.template run<NP0, false, true>(get, [&](auto ui) {
+        constexpr int i = decltype(ui)::value, P = PA + i;
+        if constexpr (i == NP0 - 1 || key(P + 1) != key(P)) load_static<sidx(PA, P) + D>();
+      });
+    }
+#pragma nounroll
+    for (int c = 0; c < C; ++c) {  // loop runs: stream slots NA + 8c + i
+      auto get = [&](auto ui) {
+        constexpr int u = decltype(ui)::value;
+        const uint4 v = S[(NA + (u >> 1)) % D];
+        return (u & 1) ? make_uint3(v.z, v.w, 0u) : make_uint3(v.x, v.y, 0u);
+      };
+      const bool last = c == C - 1;
+      pp.template run<U, true, false>(get, [&](auto ui) {
+        constexpr int u = decltype(ui)::value;
+        if constexpr (u & 1) {  // slot i = u / 2 consumed: refill with stream slot NA + 8 (c + 1) + i
+          constexpr int i = u >> 1, fe = NA + 8 * C + i;  // the target when c is the last run
+          constexpr int re = fe < NS0 ? srel(fe) : 2;
+          constexpr int soe = fe < NS0 ? st_(fe) * 1024 : 0;
+          const int vo_loop = vb[1], so_loop = (kLam / 2 + 8 * (c + 1) + i) * 1024;
+          int vo, so;
+          if constexpr (fe < NS && re != 2) {
+            vo = last ? vb[re + 1] : vo_loop;
+            so = last ? soe : so_loop;
+          } else {
+            vo = last ? -1 : vo_loop;
+            so = so_loop;
+          }
+          S[(NA + i) % D] = ld(vo, so);
+        }
+      });
+    }
+    {  // epilogue: static slots; the refills reach into the next stripe
+      auto get = [&](auto ii) {
+        constexpr int i = decltype(ii)::value, P = P1 + i, f = NA + 8 * C + sidx(P1, P);
+        const uint4 v = S[f % D];
+        return (off(P) & 1) ? make_uint3(v.z, v.w, 0u) : make_uint3(v.x, v.y, 0u);
+      };
+      pp.template run<NE, true, false>(get, [&](auto ui) {
+        constexpr int i = decltype(ui)::value, P = P1 + i;
+        if constexpr (i == NE - 1 || key(P + 1) != key(P)) {
+          constexpr int f = NA + 8 * C + sidx(P1, P);
+          if constexpr (NT_TS_XPRIME || f + D < NS) load_static<f + D>();
+          if constexpr (NT_TS_XPRIME && i == NE - 1) {  // the pad slots of the stream: their refills too
+            static_for<f + 1, NS>([&](auto gi) { load_static<decltype(gi)::value + D>(); });
+          }
+        }
+      });
+    }
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+#pragma unroll
+      for (int b = 0; b < 8; ++b) acc[p][b] = pp.bc[p].acc[b];
+  }
+};
+
+// 8x8 bit transpose inside every byte of 8 words: afterwards byte g of word j
+// holds bit b (of word b before) = bit b of the count of slot 8 g + j.
+__device__ __forceinline__ void transpose8(uint32_t (&a)[8]) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const uint32_t t = ((a[r] >> 4) ^ a[r + 4]) & 0x0F0F0F0Fu;
+    a[r + 4] ^= t;
+    a[r] ^= t << 4;
+  }
+#pragma unroll
+  for (int r = 0; r < 8; r += (r & 1) ? 3 : 1) {  // 0, 1, 4, 5
+    const uint32_t t = ((a[r] >> 2) ^ a[r + 2]) & 0x33333333u;
+    a[r + 2] ^= t;
+    a[r] ^= t << 2;
+  }
+#pragma unroll
+  for (int r = 0; r < 8; r += 2) {
+    const uint32_t t = ((a[r] >> 1) ^ a[r + 1]) & 0x55555555u;
+    a[r + 1] ^= t;
+    a[r] ^= t << 1;
+  }
+}
+
+// v[kLane] = x (x wave-uniform): one v_writelane_b32.  hipcc inserts no wait
+// states around inline asm, and x is usually an SGPR pair a v_cmp (a ballot)
+// has just written: the VALU-writes-SGPR -> v_writelane-reads-it hazard needs
+// them (missing, bits of the ballot were lost), so kWait puts them in.
+template <int kLane, bool kWait = true>
+__device__ __forceinline__ void writelane(uint32_t& v, uint32_t x) {
+  if constexpr (kWait)
+    asm volatile("s_nop 4\n\tv_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(x), "i"(kLane));
+  else
+    asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(x), "i"(kLane));
+}
+
+// Per-slot metadata of the bundle being scanned (per-wave LDS, written once
+// per bundle): not held in registers across the walk.
+struct TSlot {
+  uint32_t len, nw, r, occ;
+  uint32_t wb_lo, wb_hi;  // index of pass 0's window counts (win_off * np)
+  uint32_t ab_lo, ab_hi;  // aux_base(win_off, r, np): telomeric bitmasks, then checkpoints
+  uint32_t run[3];        // covered bases of the windows before this stripe, per pass
+  uint32_t pad;
+};
+constexpr int kTsSlotWords = 12;
+// v[lane] = x (x, lane wave-uniform SGPRs): v_writelane_b32 with the wait
+// states of writelane()
+// (a run-time lane select goes through M0: two SGPR operands break the
+// constant-bus limit)
+__device__ __forceinline__ void writelane_s(uint32_t& v, uint32_t x, int lane) {
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 4\n\tv_writelane_b32 %0, %1, m0" : "+v"(v) : "s"(x), "s"(lane) : "m0");
+}
+
+// per-wave LDS of the bundle scan (uint32 words): slots, row totals [row][16]
+constexpr int kTsLdsWords = NT_BUNDLE * kTsSlotWords + 4 * 16;
+
+__device__ __forceinline__ uint64_t u64of(uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32) | lo; }
+
+// The bundle scan: every bundle of the batch, one wave per bundle (claimed
+// from 8 per-XCD queues).
+template <class TP, class Pats, class Tvrs>
+__device__ __forceinline__ void tscan_bundles(const NtBatch& B, const NtOut& O, uint64_t* __restrict__ tmask,
+                                              unsigned long long* __restrict__ queue,
+                                              uint32_t thr_full, uint32_t* wlds) {
+  constexpr int kL = TP::kL, kNP = TP::kNP, kT = TP::kT;
+  const int lane = threadIdx.x & (kWave - 1);
+  TSlot* sl = reinterpret_cast<TSlot*>(wlds);
+  uint32_t* rowtot = wlds + NT_BUNDLE * kTsSlotWords;
+  const uint64_t nb = B.n_bundles;
+  uint32_t qi = blockIdx.x % NT_QUEUES, qtried = 0;
+  auto claim = [&]() -> uint64_t {
+    while (qtried < NT_QUEUES) {
+      const uint64_t q0 = nb * qi / NT_QUEUES, q1 = nb * (qi + 1) / NT_QUEUES;
+      unsigned long long v = 0;
+      if (lane == 0) v = atomicAdd(queue + qi * NT_QUEUE_STRIDE, 1ull);
+      const uint64_t o = uniform_u64(v);
+      if (o < q1 - q0) return q0 + o;
+      qi = qi + 1 == NT_QUEUES ? 0 : qi + 1;
+      ++qtried;
+    }
+    return nb;
+  };
+  for (uint64_t b = claim(); b < nb; b = claim()) {
+    // ---- slot metadata into LDS (lanes 0..31 = slots)
+    uint32_t occ, n_max;
+    {
+      const uint32_t r = B.bnd_read[b * NT_BUNDLE + (lane & 31)];
+      const bool o = r != 0xFFFFFFFFu;
+      const uint32_t len = o ? B.len[r] : 0u;
+      const uint64_t wo = o ? B.win_off[r] : 0ull;
+      if (lane < NT_BUNDLE) {
+        TSlot t;
+        t.len = len;
+        t.nw = (uint32_t)split_window_count(len, kL);
+        t.r = r;
+        t.occ = o ? 1u : 0u;
+        const uint64_t wb = wo * kNP, ab = aux_base(wo, r, kNP);
+        t.wb_lo = (uint32_t)wb;
+        t.wb_hi = (uint32_t)(wb >> 32);
+        t.ab_lo = (uint32_t)ab;
+        t.ab_hi = (uint32_t)(ab >> 32);
+        t.run[0] = t.run[1] = t.run[2] = 0u;
+        t.pad = 0u;
+        sl[lane] = t;
+      }
+      occ = (uint32_t)__ballot(o && lane < NT_BUNDLE);
+      n_max = (uint32_t)__builtin_amdgcn_readfirstlane((int)len);  // slot 0 = the longest
+    }
+    const int nblk = ((int)n_max + kL - 1) / kL;
+    const int nst = (nblk + kWave - 1) / kWave;
+    const uint64_t g0 = uniform_u64(B.bnd_stripe[b]), g1 = uniform_u64(B.bnd_stripe[b + 1]);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint32_t*>(B.tplanes) + g0 * (uint64_t)kT * kWave * 4, (short)0,
+        (int)((g1 - g0) * (uint64_t)kT * kWave * 16), 0x00020000);
+    wave_sync();
+    TWalker<TP, Pats, Tvrs> wk;
+    wk.rs = rs;
+    wk.set_stripe(0, lane, lane < nblk);
+    if (NT_TS_XPRIME) wk.prime();
+    for (int st = 0; st < nst; ++st) {
+      const int k = st * kWave + lane;  // this lane's block = window
+      if (!NT_TS_XPRIME) wk.prime();
+      uint32_t acc[3][8];
+#if NT_TS_DBG_NOWALK  // timing experiments only: results are wrong
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+#pragma unroll
+        for (int b = 0; b < 8; ++b) acc[p][b] = (uint32_t)(k * 0x9E3779B9u) >> (p + b);
+#else
+      wk.walk(k == 0, acc);
+#endif
+#if NT_TS_DBG_NOOUT  // timing experiments only: results are wrong
+      {
+        uint32_t x = 0;
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+#pragma unroll
+          for (int b = 0; b < 8; ++b) x ^= acc[p][b] * (b + 1);
+        if (x == 0x1234567u) O.flags[0] = 1;
+        continue;
+      }
+#endif
+      wk.set_stripe(st + 1, lane, k + kWave < nblk);  // lanes past the bundle's last block load nothing
+      // ---- outputs, lane = window k, one pass at a time
+#pragma unroll
+      for (int p = 0; p < kNP; ++p) {
+        uint32_t W[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) W[t] = acc[p][t];
+        transpose8(W);
+        uint32_t tmv = 0u, RS[16];
+#pragma unroll
+        for (int t = 0; t < 16; ++t) RS[t] = 0u;
+        // the slots' window counts and count offsets, lane s = slot s (one LDS
+        // round trip; v_readlane per slot below).  No branch per slot: the
+        // counts go out through a buffer resource per slot whose range ends at
+        // the read's last window (the stores past it are dropped), so the
+        // slots' instructions interleave freely.
+        const TSlot& ms = sl[lane & (NT_BUNDLE - 1)];
+        const uint32_t m_nw = ms.occ ? ms.nw : 0u, m_wlo = ms.wb_lo, m_whi = ms.wb_hi;
+        const int k0 = st * kWave;
+        static_for<0, 4>([&](auto gi) {
+          constexpr int g = decltype(gi)::value;
+          // slots are sorted by length: none of 8 g.. has a window here when 8 g has none
+          if (__builtin_amdgcn_readlane((int)m_nw, 8 * g) <= k0) return;
+          static_for<0, 8>([&](auto ji) {
+            constexpr int j = decltype(ji)::value, s = 8 * g + j;
+            const int nw = __builtin_amdgcn_readlane((int)m_nw, s);
+            const uint64_t wb = u64of((uint32_t)__builtin_amdgcn_readlane((int)m_wlo, s),
+                                      (uint32_t)__builtin_amdgcn_readlane((int)m_whi, s));
+            // windows here (kept in SGPRs: a VGPR operand would make the store a waterfall loop)
+            const int nwin = __builtin_amdgcn_readfirstlane(nw - k0 < 0 ? 0 : (nw - k0 > kWave ? kWave : nw - k0));
+            const uint64_t wp = uniform_u64(reinterpret_cast<uint64_t>(O.win_counts + wb + (uint64_t)p * nw + k0));
+            const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+                reinterpret_cast<uint16_t*>(wp), (short)0, 2 * nwin, 0x00020000);
+            const uint32_t c = (W[j] >> (8 * g)) & 0xFFu;
+            __builtin_amdgcn_raw_buffer_store_b16((unsigned short)c, wr, 2 * lane, 0, 0);
+            const bool valid = lane < nwin;
+            const uint64_t tb = __ballot(valid && c >= thr_full);
+            writelane<2 * s>(tmv, (uint32_t)tb);
+            writelane<2 * s + 1, false>(tmv, (uint32_t)(tb >> 32));
+            // packed row-sum word s & 15, half s >> 4
+            RS[s & 15] |= (valid ? c : 0u) << (16 * (s >> 4));
+          });
+        });
+        // telomeric bitmask word st of every read: lane 2s + h = half h of read s's
+        {
+          const TSlot& t = sl[lane >> 1];
+          if (t.occ && st * kWave < (int)t.nw)
+            reinterpret_cast<uint32_t*>(tmask + u64of(t.ab_lo, t.ab_hi) + (uint64_t)p * aux_nmw((int)t.nw) + st)[lane & 1] =
+                tmv;
+        }
+        // checkpoints: covered bases before windows 16 j, from the row sums
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+          uint32_t v = RS[t];
+          v += dpp0<kDppRowShr + 1, 0xf>(v);
+          v += dpp0<kDppRowShr + 2, 0xf>(v);
+          v += dpp0<kDppRowShr + 4, 0xf>(v);
+          v += dpp0<kDppRowShr + 8, 0xf>(v);
+          if ((lane & 15) == 15) rowtot[(lane >> 4) * 16 + t] = v;
+        }
+        wave_sync();
+        if (lane < NT_BUNDLE && sl[lane].occ) {
+          const TSlot& t = sl[lane];
+          const int nw = (int)t.nw;
+          uint32_t* ck = reinterpret_cast<uint32_t*>(tmask + u64of(t.ab_lo, t.ab_hi) + (uint64_t)kNP * aux_nmw(nw)) +
+                         p * aux_nck(nw);
+          uint32_t cum = t.run[p];
+#pragma unroll
+          for (int jr = 0; jr < 4; ++jr) {
+            const int jj = st * 4 + jr;
+            if (16 * jj < nw) ck[jj] = cum;
+            cum += (rowtot[jr * 16 + (lane & 15)] >> (16 * (lane >> 4))) & 0xFFFFu;
+          }
+          sl[lane].run[p] = cum;
+          // the checkpoint at window nw (the read's total) when nw is a multiple of 16
+          if (st == nst - 1 && (nw & 15) == 0) ck[nw >> 4] = cum;
+        }
+        wave_sync();
+      }
+    }
+    wave_sync();
+  }
+}
+
+}  // namespace nt

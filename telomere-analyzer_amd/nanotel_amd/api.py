@@ -57,6 +57,8 @@ class NanoTel:
         # scan kernel specialised for these patterns at run time (hiprtc), or
         # the ahead-of-time kernels (NT_JIT=0 / hiprtc unavailable)
         self.jit = bool(info.jit)
+        # bundled reads take the bundle scan (the reads transposed 32 to a bundle)
+        self.tscan = bool(info.tscan)
         self.subseq_length = int(subseq_length)
 
     # ------------------------------------------------------------------
@@ -181,14 +183,46 @@ class NanoTel:
 
     # ------------------------------------------------------------------
     def scan_call_device(self, planes, blk_off, lengths, win_off, n_reads, n_windows, max_len, start,
-                         end, density, flags, win_counts, hits=0, exc_off=0, exc_pos=0, exc_code=0):
+                         end, density, flags, win_counts, hits=0, exc_off=0, exc_pos=0, exc_code=0,
+                         bundles=None):
         """Device-resident hot path: all pointer arguments are device pointers
-        (ints); n_windows = sum of window counts.  Asynchronous on the context
-        stream (see set_stream)."""
-        B = NtBatch(planes, blk_off, lengths, win_off, exc_off or None, exc_pos or None,
-                    exc_code or None, int(n_reads), int(n_windows))
+        (ints); n_windows = sum of window counts.  bundles: a DeviceBundles
+        (bundle_plan + bundle_layout_device) or None (per-read scan only).
+        Asynchronous on the context stream (see set_stream)."""
+        B = self._batch(planes, blk_off, lengths, win_off, n_reads, n_windows, exc_off, exc_pos, exc_code,
+                        bundles)
         O = NtOut(win_counts or None, start, end, density, flags, hits or None)
         _check(lib().nt_scan_call(self._h, ctypes.byref(B), ctypes.byref(O), int(max_len)), self._h)
+
+    @staticmethod
+    def _batch(planes, blk_off, lengths, win_off, n_reads, n_windows, exc_off=0, exc_pos=0, exc_code=0,
+               bundles=None):
+        b = bundles
+        return NtBatch(planes, blk_off, lengths, win_off, exc_off or None, exc_pos or None,
+                       exc_code or None, int(n_reads), int(n_windows),
+                       b.tplanes if b else None, b.bnd_read if b else None, b.bnd_stripe if b else None,
+                       b.n_bundles if b else 0, (b.list or None) if b else None, b.n_list if b else 0)
+
+    def bundle_plan(self, lengths, has_exc=None):
+        """nt_bundle_plan on host arrays: returns a BundlePlan (numpy arrays)."""
+        ln = np.ascontiguousarray(lengths, np.uint32)
+        n = ln.size
+        nbmax = (n + 31) // 32
+        bread = np.zeros(max(1, nbmax * 32), np.uint32)
+        bstripe = np.zeros(nbmax + 1, np.uint64)
+        lst = np.zeros(max(1, n), np.uint32)
+        hx = None if has_exc is None else np.ascontiguousarray(has_exc, np.uint8)
+        nb, nl, tpb = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        _check(lib().nt_bundle_plan(self._h, ln.ctypes.data, None if hx is None else hx.ctypes.data, n,
+                                    bread.ctypes.data, bstripe.ctypes.data, ctypes.byref(nb), lst.ctypes.data,
+                                    ctypes.byref(nl), ctypes.byref(tpb)), self._h)
+        return BundlePlan(bread[:nb.value * 32], bstripe[:nb.value + 1], lst[:nl.value], tpb.value)
+
+    def bundle_layout_device(self, planes, blk_off, lengths, win_off, n_reads, n_windows, bundles):
+        """nt_bundle_layout: write bundles.tplanes (device) from the per-read planes."""
+        B = self._batch(planes, blk_off, lengths, win_off, n_reads, n_windows, bundles=bundles)
+        _check(lib().nt_bundle_layout(self._h, ctypes.byref(B), bundles.tplanes, int(bundles.tplane_bytes)),
+               self._h)
 
     def synth_device(self, sp, n_reads, planes_ptr):
         _check(lib().nt_synth_device(self._h, ctypes.byref(sp), int(n_reads), planes_ptr), self._h)
@@ -196,6 +230,23 @@ class NanoTel:
     def uniform_layout_device(self, n_reads, read_len, blk_off_ptr, len_ptr, win_off_ptr):
         _check(lib().nt_uniform_layout_device(self._h, int(n_reads), int(read_len), self.subseq_length,
                                               blk_off_ptr, len_ptr, win_off_ptr), self._h)
+
+
+class BundlePlan:
+    """Host result of nt_bundle_plan: bnd_read (n_bundles*32 u32), bnd_stripe
+    (n_bundles+1 u64), list (the reads left to the per-read scan), tplane_bytes."""
+
+    def __init__(self, bnd_read, bnd_stripe, lst, tplane_bytes):
+        self.bnd_read, self.bnd_stripe, self.list, self.tplane_bytes = bnd_read, bnd_stripe, lst, tplane_bytes
+        self.n_bundles = len(bnd_stripe) - 1 if len(bnd_stripe) else 0
+
+
+class DeviceBundles:
+    """Device pointers (ints) of a bundle layout for scan_call_device."""
+
+    def __init__(self, tplanes, bnd_read, bnd_stripe, n_bundles, lst, n_list, tplane_bytes):
+        self.tplanes, self.bnd_read, self.bnd_stripe, self.n_bundles = tplanes, bnd_read, bnd_stripe, n_bundles
+        self.list, self.n_list, self.tplane_bytes = lst, n_list, tplane_bytes
 
 
 def synth_params(seed=20260501, first_read=0, read_len=50000, p_tract=0.5, sub_rate=0.02,

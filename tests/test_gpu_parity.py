@@ -33,6 +33,17 @@ def _nt(jit=True, **kw):
     return nt
 
 
+def _check_both(nt, seqs, orow, **kw):
+    """The per-read scan (hit counters asked for: a parity output only it
+    produces) and, for a program the bundle scan covers, the bundle scan (no
+    hit counters: the reads transposed 32 to a bundle), both against the oracle."""
+    res = nt.analyze(seqs, want_windows=True, want_hits=True)
+    compare(nt, res, orow, **kw)
+    res2 = nt.analyze(seqs, want_windows=True, want_hits=False)
+    compare(nt, res2, orow, check_hits=False, **kw)
+    return res, res2
+
+
 def _example():
     return O.read_fasta(os.path.join(GOLD, "sample.fasta"))
 
@@ -68,8 +79,8 @@ def test_example_golden_through_hip():
     names, seqs = _example()
     for legacy in (True, False):
         nt = _nt(patterns="TTAGGG", min_density=0.6, legacy_no_ext=legacy)
-        res = nt.analyze(seqs, want_windows=True, want_hits=True)
-        compare(nt, res, oracle_rows(seqs, "TTAGGG", legacy=legacy))
+        assert nt.tscan
+        _check_both(nt, seqs, oracle_rows(seqs, "TTAGGG", legacy=legacy))
         nt.close()
     # the committed golden itself (legacy) through the HIP path
     import csv
@@ -89,8 +100,7 @@ def test_synthetic_generator_reads():
         sp = synth_params(read_len=read_len, rc_layout=rc_layout, variant_rate=var)
         seqs = [synth_read_ascii(sp, i) for i in range(24)]
         nt = _nt(patterns="TTAGGG", rc=rc_layout)
-        res = nt.analyze(seqs, want_windows=True, want_hits=True)
-        compare(nt, res, oracle_rows(seqs, "TTAGGG", rc=rc_layout))
+        res, _ = _check_both(nt, seqs, oracle_rows(seqs, "TTAGGG", rc=rc_layout))
         assert res["telomeric"].sum() > 0
 
 
@@ -106,8 +116,8 @@ def test_baseline_config_reads(cfg):
     sp = synth_params(read_len=cfg["read_len"], rc_layout=cfg["rc"], variant_rate=cfg["variant"], first_read=4242)
     seqs = [synth_read_ascii(sp, i) for i in range(64)]
     nt = _nt(patterns=cfg["patterns"], tvr_patterns=cfg["tvr"], rc=cfg["rc"])
-    res = nt.analyze(seqs, want_windows=True, want_hits=True)
-    compare(nt, res, oracle_rows(seqs, cfg["patterns"], tvr=cfg["tvr"], rc=cfg["rc"]))
+    assert nt.tscan
+    res, _ = _check_both(nt, seqs, oracle_rows(seqs, cfg["patterns"], tvr=cfg["tvr"], rc=cfg["rc"]))
     assert 0 < res["telomeric"].sum() < 64
 
 
@@ -140,10 +150,10 @@ def test_random_reads(cfg, jit):
         seqs.append(_telo_read(rng, n, motif=motif, where=where,
                                exc=0.002 if i % 5 == 0 else 0.0, lower=0.01 if i % 7 == 0 else 0.0))
     nt = _nt(jit=jit, **cfg)
-    res = nt.analyze(seqs, want_windows=True, want_hits=True)
+    assert nt.tscan == jit
     orow = oracle_rows(seqs, cfg["patterns"], tvr=cfg.get("tvr_patterns"), L=cfg.get("subseq_length", 100),
                        min_density=cfg.get("min_density", 0.6), right_edge=right, rc=cfg.get("rc", False))
-    compare(nt, res, orow)
+    _check_both(nt, seqs, orow)
 
 
 @pytest.mark.parametrize("jit", [True, False], ids=["jit", "aot"])
@@ -154,8 +164,7 @@ def test_iupac_subject_letters_and_tiny_reads(jit):
         seqs.append(_telo_read(rng, n, tract=(0, n), exc=0.05))
     for pats in ("TTAGGG", "YYAGGG", "TTAGGG TCAGGG", "NNNNNN"):
         nt = _nt(jit=jit, patterns=pats, tvr_patterns="TGAGGG")
-        res = nt.analyze(seqs, want_windows=True, want_hits=True)
-        compare(nt, res, oracle_rows(seqs, pats, tvr="TGAGGG"))
+        _check_both(nt, seqs, oracle_rows(seqs, pats, tvr="TGAGGG"))
 
 
 @pytest.mark.parametrize("jit", [True, False], ids=["jit", "aot"])
@@ -166,8 +175,7 @@ def test_long_reads_global_scratch_path(jit):
             _telo_read(rng, 181000, where="right", tract=(5000, 9000))]
     for pats, tvr in (("TTAGGG", "TTGGGG"), ("TTAGGG", None)):
         nt = _nt(jit=jit, patterns=pats, tvr_patterns=tvr)
-        res = nt.analyze(seqs, want_windows=True, want_hits=True)
-        compare(nt, res, oracle_rows(seqs, pats, tvr=tvr))
+        _check_both(nt, seqs, oracle_rows(seqs, pats, tvr=tvr))
 
 
 @pytest.mark.parametrize("right", [False, True], ids=["left_edge", "right_edge"])
@@ -183,8 +191,7 @@ def test_reads_with_9_to_16_bitmask_words(right):
         seqs.append(_telo_read(rng, n, motif=motif, where=["left", "right", "mid"][i % 3], tract=(2000, 15000)))
     for tvr in (None, "TTGGGG"):
         nt = _nt(patterns=motif, tvr_patterns=tvr, check_right_edge=right)
-        res = nt.analyze(seqs, want_windows=True, want_hits=True)
-        compare(nt, res, oracle_rows(seqs, motif, tvr=tvr, right_edge=right))
+        res, _ = _check_both(nt, seqs, oracle_rows(seqs, motif, tvr=tvr, right_edge=right))
         assert res["telomeric"].sum() > 0
 
 
@@ -279,6 +286,53 @@ def test_device_resident_path_matches_host_path(jit):
     assert np.array_equal(t["wc"].cpu().numpy().view(np.uint16), res["win_counts"])
     assert np.array_equal(t["hits"].cpu().numpy().view(np.uint32).reshape(n, -1), res["hits"])
     compare(nt, res, oracle_rows(seqs[:6], "TTAGGG"))
+
+
+def _device_bundles(nt, t, n, read_len):
+    """The bench's bundle layout of a device batch (host plan, device transpose)."""
+    import torch
+    from nanotel_amd.api import DeviceBundles
+    plan = nt.bundle_plan(np.full(n, read_len, np.uint32))
+    d = dict(bnd_read=torch.from_numpy(plan.bnd_read.view(np.int32)).cuda(),
+             bnd_stripe=torch.from_numpy(plan.bnd_stripe.view(np.int64)).cuda(),
+             tplanes=torch.empty(max(1, plan.tplane_bytes // 4), dtype=torch.int32, device="cuda"))
+    b = DeviceBundles(d["tplanes"].data_ptr(), d["bnd_read"].data_ptr(), d["bnd_stripe"].data_ptr(),
+                      plan.n_bundles, 0, 0, plan.tplane_bytes)
+    nt.bundle_layout_device(t["planes"].data_ptr(), t["blk_off"].data_ptr(), t["lens"].data_ptr(),
+                            t["win_off"].data_ptr(), n, n * t["nw"], b)
+    nt.synchronize()
+    return b, d
+
+
+@pytest.mark.parametrize("read_len", [50000, 10000, 6450, 3001])
+def test_device_bundle_scan_matches_per_read_scan(read_len):
+    # the bench's path: device-generated reads, bundle layout on the device,
+    # bundle scan; against the per-read scan of the same batch (hit counters
+    # asked for) on every output, and the oracle on a sample
+    from nanotel_amd import synth_params, synth_read_ascii
+    n = 160  # 5 bundles
+    sp = synth_params(read_len=read_len, first_read=900)
+    nt = _nt(patterns="TTAGGG")
+    assert nt.tscan
+    t = _device_batch(nt, sp, n, read_len)
+    _run_device(nt, t, n, read_len)
+    ref = {k: t[k].clone() for k in ("start", "end", "dens", "flags", "wc")}
+    for k in ref:
+        t[k].zero_()
+    b, keep = _device_bundles(nt, t, n, read_len)
+    nt.scan_call_device(t["planes"].data_ptr(), t["blk_off"].data_ptr(), t["lens"].data_ptr(),
+                        t["win_off"].data_ptr(), n, n * t["nw"], read_len, t["start"].data_ptr(),
+                        t["end"].data_ptr(), t["dens"].data_ptr(), t["flags"].data_ptr(), t["wc"].data_ptr(),
+                        bundles=b)
+    nt.synchronize()
+    import torch
+    for k in ref:
+        assert torch.equal(t[k], ref[k]), k
+    seqs = [synth_read_ascii(sp, i) for i in range(0, n, 23)]
+    res = {"start": t["start"].cpu().numpy().reshape(n, 3)[::23], "end": t["end"].cpu().numpy().reshape(n, 3)[::23],
+           "density": t["dens"].cpu().numpy().reshape(n, 3)[::23], "flags": t["flags"].cpu().numpy()[::23]}
+    res["telomeric"] = (res["flags"] & 1) != 0
+    compare(nt, res, oracle_rows(seqs, "TTAGGG"), check_windows=False, check_hits=False)
 
 
 def test_odd_block_offset_is_reported():

@@ -1,0 +1,57 @@
+#!/usr/bin/env python3
+"""Compile the hiprtc source of the pattern-specialised kernels on the CPU
+(no GPU needed: hiprtc only drives the compiler) and print the log -- the
+same headers and options nt_jit.cpp uses, for a pattern type list such as
+"nt::CtPat<6,8,8,1,4,4,4>".  Catches JIT-only failures (hiprtc has no libc
+headers) before a GPU run.
+
+usage: tools/hiprtc_check.py "nt::CtPat<6,8,8,1,4,4,4>" [tvr list] [L] [extra options...]
+"""
+import ctypes
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "..", "telomere-analyzer_amd", "csrc")
+
+
+def main():
+    pats = sys.argv[1]
+    tvrs = sys.argv[2] if len(sys.argv) > 2 else ""
+    L = sys.argv[3] if len(sys.argv) > 3 else "100"
+    extra = sys.argv[4:]
+    src = "".join(f"typedef __hip_internal::{t} {t};\n" for t in
+                  ("uint8_t", "uint16_t", "uint32_t", "uint64_t", "int32_t", "int64_t"))
+    src += '#include "nt_tscan.h"\n'
+    src += f"using TPats = nt::CtList<{pats}>;\nusing TTvrs = nt::CtList<{tvrs}>;\n"
+    src += f"using TJit = nt::TProg<TPats, TTvrs, {L}>;\n"
+    src += """
+extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3)))
+nt_tscan_jit(NtBatch B, NtOut O, uint64_t* __restrict__ tmask, unsigned long long* __restrict__ queue,
+             uint32_t thr_full) {
+  __shared__ uint32_t tsl[4 * nt::kTsLdsWords];
+  nt::tscan_bundles<TJit, TPats, TTvrs>(B, O, tmask, queue, thr_full, tsl + (threadIdx.x >> 6) * nt::kTsLdsWords);
+}
+"""
+    names = ["nt_common.h", "nt_device.h", "nt_scan.h", "nt_tscan.h"]
+    hdrs = [open(os.path.join(CSRC, n), "rb").read() for n in names]
+    lib = ctypes.CDLL("/opt/rocm/lib/libhiprtc.so")
+    prog = ctypes.c_void_p()
+    arr = ctypes.c_char_p * 4
+    rc = lib.hiprtcCreateProgram(ctypes.byref(prog), src.encode(), b"nt_scan_jit.hip", 4,
+                                 arr(*hdrs), arr(*[n.encode() for n in names]))
+    assert rc == 0, rc
+    opts = [b"--offload-arch=gfx950", b"-O3", b"-std=c++17", b"-ffp-contract=off", b"-mllvm",
+            b"-amdgpu-sched-strategy=max-ilp"] + [x.encode() for x in extra]
+    rc = lib.hiprtcCompileProgram(prog, len(opts), (ctypes.c_char_p * len(opts))(*opts))
+    n = ctypes.c_size_t()
+    lib.hiprtcGetProgramLogSize(prog, ctypes.byref(n))
+    log = ctypes.create_string_buffer(n.value + 1)
+    lib.hiprtcGetProgramLog(prog, log)
+    print(log.value.decode(errors="replace")[-4000:])
+    print("hiprtc rc", rc)
+    sys.exit(0 if rc == 0 else 1)
+
+
+if __name__ == "__main__":
+    main()
