@@ -145,7 +145,7 @@ def main():
 
     import torch
     import torch.distributed as dist
-    from nanotel_amd import NanoTel, read_blocks, synth_params, window_count
+    from nanotel_amd import NanoTel, read_blocks, synth_params, window_count, window_rows
 
     cfg = dict(CONFIGS[args.config])
     if args.reads:
@@ -174,7 +174,8 @@ def main():
     blk_off = torch.empty(n, dtype=torch.int64, device=dev)
     lens = torch.empty(n, dtype=torch.int32, device=dev)
     win_off = torch.empty(n, dtype=torch.int64, device=dev)
-    wc = torch.empty(n * nw * npass, dtype=torch.int16, device=dev)
+    rows = window_rows(nw)  # padded count rows (16-byte aligned, nt_common.h)
+    wc = torch.empty(n * rows * npass, dtype=torch.int16, device=dev)
     start = torch.empty(n * 3, dtype=torch.int32, device=dev)
     end = torch.empty(n * 3, dtype=torch.int32, device=dev)
     dens = torch.empty(n * 3, dtype=torch.float64, device=dev)
@@ -196,12 +197,12 @@ def main():
         bundles = DeviceBundles(tpl.data_ptr(), bread.data_ptr(), bstripe.data_ptr(), plan.n_bundles, 0, 0,
                                 plan.tplane_bytes)
         nt.bundle_layout_device(planes.data_ptr(), blk_off.data_ptr(), lens.data_ptr(), win_off.data_ptr(),
-                                n, n * nw, bundles)
+                                n, n * rows, bundles)
     torch.cuda.synchronize(dev)
 
     def step():
         nt.scan_call_device(planes.data_ptr(), blk_off.data_ptr(), lens.data_ptr(), win_off.data_ptr(),
-                            n, n * nw, L, start.data_ptr(), end.data_ptr(), dens.data_ptr(),
+                            n, n * rows, L, start.data_ptr(), end.data_ptr(), dens.data_ptr(),
                             flags.data_ptr(), wc.data_ptr(), bundles=bundles)
 
     for _ in range(args.warmup):

@@ -85,12 +85,12 @@ typedef struct {
   const uint32_t* planes;
   const uint64_t* blk_off;  /* [n_reads] first 32-base block of each read (even) */
   const uint32_t* len;      /* [n_reads] */
-  const uint64_t* win_off;  /* [n_reads] prefix sum of split_telo window counts */
+  const uint64_t* win_off;  /* [n_reads] prefix sum of the window ROWS nt_window_rows(nw) of the reads */
   const uint32_t* exc_off;  /* [n_reads+1] or NULL: non-ACGT letters */
   const uint32_t* exc_pos;
   const uint8_t* exc_code;
   uint64_t n_reads;
-  uint64_t n_windows;       /* sum of split_telo window counts (win_counts has n_windows*n_pass) */
+  uint64_t n_windows;       /* sum of the window rows (win_counts has n_windows*n_pass entries) */
   /* Bundle scan (optional): the reads transposed 32 to a bundle
    * (nt_bundle_plan + nt_bundle_layout).  tplanes == NULL: every read takes the
    * per-read scan.  Else the bundled reads take the bundle scan and the reads
@@ -105,7 +105,7 @@ typedef struct {
 
 /* Device-resident outputs (device pointers). */
 typedef struct {
-  uint16_t* win_counts; /* [sum windows * n_pass] or NULL */
+  uint16_t* win_counts; /* [n_windows * n_pass]: pass p of read r at win_off[r]*n_pass + p*rows(r); 128-B aligned base */
   int32_t* start;       /* [n_reads*3] */
   int32_t* end;         /* [n_reads*3] */
   double* density;      /* [n_reads*3] */
@@ -139,6 +139,9 @@ int nt_compile(nt_ctx* ctx, const nt_params* params, nt_program_info* info);
 
 /* --- host packing (A14 reverseComplement fused when params.rc) ----------- */
 int64_t nt_window_count(int64_t n, int32_t subseq_length);
+/* The window-count row of a read and pass: nw rounded up to a multiple of 64
+ * (whole 128-byte lines; the padding windows hold unspecified values). */
+uint64_t nt_window_rows(int64_t nw);
 /* 32-base blocks of a read's slot in the plane buffer: 2*ceil(n/64).  Slots
  * start at EVEN block offsets (the scan loads 64-base segments, 16 bytes). */
 uint64_t nt_read_blocks(uint64_t n);

@@ -9,8 +9,14 @@
 //   ambiguity codes, '-', '+', '.') are stored as A in the planes and listed in
 //   a per-read exception list (position, Biostrings DNA code) -- see
 //   DESIGN.md "Exceptions".
-// Window counts: uint16 at win_counts[win_off[r]*n_pass + p*nw(r) + i]
-//   (covered bases of window i of pass p; nw = split_telo window count).
+// Window counts: uint16 at win_counts[win_off[r]*n_pass + p*NT_WIN_ROWS(nw(r)) + i]
+//   (covered bases of window i of pass p; nw = split_telo window count).  A
+//   read's rows are padded to a multiple of 64 windows and win_off[r] is the
+//   prefix sum of the PADDED counts, so every 64-window block of a row is one
+//   128-byte line (the scans store whole lines: a partly written line costs a
+//   read-modify-write in the memory system) and 16-byte aligned for the bundle
+//   scan's 8-count stores; the padding windows [nw, NT_WIN_ROWS(nw)) hold
+//   unspecified values.
 #pragma once
 #ifndef __HIPCC_RTC__
 #include <stdint.h>
@@ -20,6 +26,7 @@
 #define NT_MAX_M 18       // testit::assert(str_length(pattern) <= 18), NanoTel.R:589,647
 #define NT_MAX_TVR_M 32   // TVRs are only length-limited by the 32-bit start words
 #define NT_MAX_PASS 3
+#define NT_WIN_ROWS(nw) (((nw) + 63) & ~63ull)  // windows of a padded count row
 
 // Scan read queues (see scan_reads): per launch, NT_QUEUES u64 counters
 // NT_QUEUE_STRIDE u64 apart (own 256-byte line each), zeroed before the launch

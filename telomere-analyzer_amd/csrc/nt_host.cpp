@@ -368,6 +368,7 @@ int nt_synchronize(nt_ctx* ctx) {
 }
 
 int64_t nt_window_count(int64_t n, int32_t subseq_length) { return window_count(n, subseq_length); }
+uint64_t nt_window_rows(int64_t nw) { return nw <= 0 ? 0 : NT_WIN_ROWS((uint64_t)nw); }
 
 uint64_t nt_read_blocks(uint64_t n) { return read_blocks(n); }
 
@@ -467,6 +468,8 @@ int nt_compile(nt_ctx* ctx, const nt_params* prm, nt_program_info* info) {
   if (ctx->tjit_fn && std::getenv("NT_TSCAN") && std::getenv("NT_TSCAN")[0] == '0') ctx->tjit_fn = nullptr;
   if (ctx->tjit_fn) {
     ctx->tscan_bpc = nt_jit_blocks_per_cu(ctx->tjit_fn, 0);
+    if (const char* v = std::getenv("NT_TSCAN_BPC"))  // tuning experiments: fewer resident blocks per CU
+      ctx->tscan_bpc = std::min(ctx->tscan_bpc, std::atoi(v));
     if (ctx->tscan_bpc <= 0) ctx->tjit_fn = nullptr;
   }
   if (info) {
@@ -513,7 +516,7 @@ int nt_pack_count(const char* const* seqs, const uint64_t* lens, uint64_t n_read
       return bad[r] == 2 ? NT_E_EMPTY_READ : NT_E_LETTER;
     }
     tb += read_blocks(lens[r]);
-    tw += (uint64_t)window_count((int64_t)lens[r], subseq_length);
+    tw += NT_WIN_ROWS((uint64_t)window_count((int64_t)lens[r], subseq_length));
     te += exc[r];
     ml = std::max(ml, lens[r]);
   }
@@ -591,7 +594,7 @@ int nt_pack_reads(const char* const* seqs, const uint64_t* lens, uint64_t n_read
     win_off[r] = w;
     len[r] = (uint32_t)lens[r];
     b += read_blocks(lens[r]);
-    w += (uint64_t)window_count((int64_t)lens[r], subseq_length);
+    w += NT_WIN_ROWS((uint64_t)window_count((int64_t)lens[r], subseq_length));
   }
   if (exc_off) {
     std::vector<uint64_t> cnt(n_reads, 0);
@@ -648,6 +651,9 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
   // the bundle scan takes the bundled reads when the program has one and no
   // hit counters are asked for (a parity/debug output of the per-read scan)
   const bool tscan = ctx->tjit_fn && batch->tplanes && batch->n_bundles && !out->hits;
+  // the bundle scan stores 8 window counts at once: padded rows (nt_common.h) from a 16-byte aligned base
+  if (tscan && (reinterpret_cast<uintptr_t>(out->win_counts) & 15))
+    return fail(ctx, NT_E_ARG, "win_counts must be 16-byte aligned for the bundle scan");
   NtBatch B{batch->planes, batch->blk_off, batch->len, batch->win_off,
             batch->exc_off, batch->exc_pos, batch->exc_code, batch->n_reads,
             tscan ? batch->list : nullptr, tscan ? batch->n_list : 0,
@@ -935,7 +941,7 @@ static int upload_reads(nt_ctx* ctx, const char* const* seqs, const uint64_t* le
     h_win[r] = tw;
     h_len[r] = (uint32_t)lens[r];
     tb += read_blocks(lens[r]);
-    tw += (uint64_t)window_count((int64_t)lens[r], L);
+    tw += NT_WIN_ROWS((uint64_t)window_count((int64_t)lens[r], L));
     ml = std::max(ml, lens[r]);
   }
   const size_t pw = 2 * tb + 2;
@@ -1200,7 +1206,7 @@ int nt_uniform_layout_device(nt_ctx* ctx, uint64_t n_reads, uint64_t read_len, i
   if (!ctx || read_len == 0 || read_len > 0xFFFFFFFFull) return NT_E_ARG;
   (void)hipSetDevice(ctx->device);
   const uint64_t nblk = read_blocks(read_len);
-  const uint64_t nw = (uint64_t)window_count((int64_t)read_len, subseq_length);
+  const uint64_t nw = NT_WIN_ROWS((uint64_t)window_count((int64_t)read_len, subseq_length));  // padded rows
   hipError_t e = nt_dev_launch_uniform_layout(n_reads, nblk, read_len, nw, blk_off_dev, len_dev,
                                               win_off_dev, ctx->stream);
   return e == hipSuccess ? NT_OK : hip_fail(ctx, e, "launch nt_layout_kernel");

@@ -80,7 +80,7 @@ std::string jit_source(const NtProgram& P) {
     s += "using TJit = nt::TProg<TPats, TTvrs, " + std::to_string(P.L) + ">;\n";
     s += R"(
 #ifndef NT_TSCAN_WAVES_EU
-#define NT_TSCAN_WAVES_EU 3
+#define NT_TSCAN_WAVES_EU 2
 #endif
 extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT_TSCAN_WAVES_EU)))
 nt_tscan_jit(NtBatch B, NtOut O, uint64_t* __restrict__ tmask, unsigned long long* __restrict__ queue,

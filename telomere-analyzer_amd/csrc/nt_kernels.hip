@@ -826,7 +826,7 @@ nt_call_kernel(const NtProgram* __restrict__ prog, NtBatch B, NtOut O,
         const uint64_t woff = B.win_off[r];
         const uint64_t* tmr = tmask + aux_base(woff, r, np);
         const uint32_t* ckr = reinterpret_cast<const uint32_t*>(tmr + np * aux_nmw(c.nw));
-        c.cnt = O.win_counts + woff * np + (uint64_t)p * c.nw;
+        c.cnt = O.win_counts + woff * np + (uint64_t)p * NT_WIN_ROWS((uint64_t)c.nw);
         c.tm = tmr + p * c.nmw;
         c.ck = ckr + p * aux_nck(c.nw);
         c.k = p == 0 ? 0 : 1;
@@ -921,7 +921,9 @@ nt_layout_kernel(uint64_t n_reads, uint64_t nblk, uint64_t read_len, uint64_t nw
 // lane 32 + s its high-plane word, so ballot(bit i) is the {lo, hi} pair of
 // position 32x + i for all 32 reads -- 32 ballots transpose the 32 x 32 bit
 // blocks of both planes.  Positions past a read (and empty slots) are 0.
-// (the wait states: see writelane in nt_tscan.h)
+// (hipcc inserts no wait states around inline asm, and x is an SGPR pair a
+// v_cmp -- a ballot -- has just written: the VALU-writes-SGPR ->
+// v_writelane-reads-it hazard needs them; without, ballot bits were lost)
 template <int kLane>
 __device__ __forceinline__ void writelane_k(uint32_t& v, uint32_t x) {
   asm volatile("s_nop 4\n\tv_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(x), "i"(kLane));

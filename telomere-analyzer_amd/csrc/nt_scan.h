@@ -805,6 +805,7 @@ __device__ __forceinline__ void scan_reads(const NtProgram* __restrict__ prog,
 
     // ------------------------------------------------ window outputs
     uint16_t* wout = O.win_counts + m.woff * np;
+    const int nr = (int)NT_WIN_ROWS(nw);  // the padded row of a pass
     // telomeric window (class -5) iff !(count / width < min_density) iff
     // count >= thr[width] (exact, host-computed); the last window may be wider
     uint32_t thr_last = thr_full;
@@ -839,13 +840,13 @@ __device__ __forceinline__ void scan_reads(const NtProgram* __restrict__ prog,
         const uint2 a0 = cum01[i], a1 = cum01[i + 1];
         c0 = a1.x - a0.x;
         c1 = a1.y - a0.y;
-        if (dbg_ok(dbg, 1, m.woff * np + (uint64_t)(nw + i), r)) {
+        if (dbg_ok(dbg, 1, m.woff * np + (uint64_t)(nr + i), r)) {
           wout[i] = (uint16_t)c0;
-          wout[nw + i] = (uint16_t)c1;
+          wout[nr + i] = (uint16_t)c1;
         }
         if (np == 3) {
           c2 = cum2[i + 1] - cum2[i];
-          if (dbg_ok(dbg, 1, m.woff * np + (uint64_t)(2 * nw + i), r)) wout[2 * nw + i] = (uint16_t)c2;
+          if (dbg_ok(dbg, 1, m.woff * np + (uint64_t)(2 * nr + i), r)) wout[2 * nr + i] = (uint16_t)c2;
         }
       }
       // (counts are 0 past the read's windows; the mask only matters for a zero threshold)

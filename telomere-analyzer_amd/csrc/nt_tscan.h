@@ -389,6 +389,12 @@ struct TPipe {
 #endif
 // 1: the epilogue prefetches the next stripe's first slots (the ring then
 // stays live across the output stage); 0: every stripe starts with prime()
+#ifndef NT_TS_DBG_NOAUX  // timing experiments only: no telomeric bitmasks / checkpoints
+#define NT_TS_DBG_NOAUX 0
+#endif
+#ifndef NT_TS_DBG_NOCNT
+#define NT_TS_DBG_NOCNT 0
+#endif
 #ifndef NT_TS_XPRIME
 #define NT_TS_XPRIME 0
 #endif
@@ -570,38 +576,65 @@ __device__ __forceinline__ void transpose8(uint32_t (&a)[8]) {
   }
 }
 
-// v[kLane] = x (x wave-uniform): one v_writelane_b32.  hipcc inserts no wait
-// states around inline asm, and x is usually an SGPR pair a v_cmp (a ballot)
-// has just written: the VALU-writes-SGPR -> v_writelane-reads-it hazard needs
-// them (missing, bits of the ballot were lost), so kWait puts them in.
-template <int kLane, bool kWait = true>
-__device__ __forceinline__ void writelane(uint32_t& v, uint32_t x) {
-  if constexpr (kWait)
-    asm volatile("s_nop 4\n\tv_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(x), "i"(kLane));
-  else
-    asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(x), "i"(kLane));
-}
-
 // Per-slot metadata of the bundle being scanned (per-wave LDS, written once
-// per bundle): not held in registers across the walk.
+// per bundle): not held in registers across the walk.  {nw, wb} first: one
+// ds_read_b128 gives a slot's count row.
 struct TSlot {
-  uint32_t len, nw, r, occ;
+  uint32_t nw;            // windows (0: empty slot)
   uint32_t wb_lo, wb_hi;  // index of pass 0's window counts (win_off * np)
+  uint32_t len;
   uint32_t ab_lo, ab_hi;  // aux_base(win_off, r, np): telomeric bitmasks, then checkpoints
+  uint32_t r, occ;
   uint32_t run[3];        // covered bases of the windows before this stripe, per pass
   uint32_t pad;
 };
 constexpr int kTsSlotWords = 12;
-// v[lane] = x (x, lane wave-uniform SGPRs): v_writelane_b32 with the wait
-// states of writelane()
-// (a run-time lane select goes through M0: two SGPR operands break the
-// constant-bus limit)
-__device__ __forceinline__ void writelane_s(uint32_t& v, uint32_t x, int lane) {
-  asm volatile("s_mov_b32 m0, %2\n\ts_nop 4\n\tv_writelane_b32 %0, %1, m0" : "+v"(v) : "s"(x), "s"(lane) : "m0");
+
+// per-wave LDS of the bundle scan (uint32 words): the slots; the count
+// transpose of the output stage (row s = slot s, 16 words = the 64 windows of
+// the stripe, 4 to a word: byte b = window 4 q + b of word q); and the
+// telomeric bitmask words / checkpoints of kTsF stripes, written out together
+// (whole runs of a read's row instead of 4-byte pieces: a partly written line
+// costs a read-modify-write in the memory system)
+constexpr int kTsCtWords = NT_BUNDLE * 16;
+template <int kNP>
+struct TsAux {
+  static constexpr int kF = kNP == 3 ? 4 : 8;                 // stripes per flush
+  static constexpr int kTmWords = kNP * NT_BUNDLE * kF * 2;   // [p][s][stripe] u64
+  static constexpr int kCkWords = kNP * NT_BUNDLE * 4 * kF;   // [p][s][4 stripe + g] u32
+};
+constexpr int kTsLdsWords = NT_BUNDLE * kTsSlotWords + kTsCtWords + 3072;  // >= TsAux<2, 3> words
+static_assert(TsAux<2>::kTmWords + TsAux<2>::kCkWords <= 3072, "LDS");
+static_assert(TsAux<3>::kTmWords + TsAux<3>::kCkWords <= 3072, "LDS");
+
+// 4x4 byte transpose inside every quad of lanes: lane i of the quad gets byte
+// i of the quad's four words (byte i' from lane i') -- two DPP exchanges
+__device__ __forceinline__ uint32_t quad_byte_transpose(uint32_t x, uint32_t sel2, uint32_t sel1) {
+  const uint32_t p2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xf, 0xf, false);  // lane ^ 2
+  x = __builtin_amdgcn_perm(p2, x, sel2);
+  const uint32_t p1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xf, 0xf, false);  // lane ^ 1
+  return __builtin_amdgcn_perm(p1, x, sel1);
 }
 
-// per-wave LDS of the bundle scan (uint32 words): slots, row totals [row][16]
-constexpr int kTsLdsWords = NT_BUNDLE * kTsSlotWords + 4 * 16;
+// 32x32 bit transpose inside each half wave: lane 32 h + s gets bit s of the
+// half's lanes (bit i from lane 32 h + i) -- five butterfly exchanges
+__device__ __forceinline__ uint32_t half_bit_transpose(uint32_t a, int lane) {
+#define NT_BT_STAGE(J, M, XCHG)                                  \
+  {                                                             \
+    const uint32_t pv = (XCHG);                                 \
+    const bool hi = (lane & (J)) != 0;                          \
+    const uint32_t sh = hi ? (pv >> (J)) : (pv << (J));         \
+    const uint32_t mm = hi ? ~(uint32_t)(M) : (uint32_t)(M);    \
+    a = (a & mm) | (sh & ~mm);                                  \
+  }
+  NT_BT_STAGE(16, 0x0000FFFFu, (uint32_t)__builtin_amdgcn_ds_swizzle((int)a, 0x401F))
+  NT_BT_STAGE(8, 0x00FF00FFu, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)a, 0x128, 0xf, 0xf, false))
+  NT_BT_STAGE(4, 0x0F0F0F0Fu, (uint32_t)__builtin_amdgcn_ds_swizzle((int)a, 0x101F))
+  NT_BT_STAGE(2, 0x33333333u, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)a, 0x4E, 0xf, 0xf, false))
+  NT_BT_STAGE(1, 0x55555555u, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)a, 0xB1, 0xf, 0xf, false))
+#undef NT_BT_STAGE
+  return a;
+}
 
 __device__ __forceinline__ uint64_t u64of(uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32) | lo; }
 
@@ -614,7 +647,14 @@ __device__ __forceinline__ void tscan_bundles(const NtBatch& B, const NtOut& O, 
   constexpr int kL = TP::kL, kNP = TP::kNP, kT = TP::kT;
   const int lane = threadIdx.x & (kWave - 1);
   TSlot* sl = reinterpret_cast<TSlot*>(wlds);
-  uint32_t* rowtot = wlds + NT_BUNDLE * kTsSlotWords;
+  uint32_t* ct = wlds + NT_BUNDLE * kTsSlotWords;  // the count transpose
+  using Aux = TsAux<kNP>;
+  uint32_t* tmb = ct + kTsCtWords;     // bitmask words of the flush
+  uint32_t* ckb = tmb + Aux::kTmWords;  // checkpoints of the flush
+  // quad_byte_transpose selectors (v_perm: bytes 0-3 from x, 4-7 from the partner)
+  const uint32_t sel2 = (lane & 2) ? 0x03020706u : 0x05040100u;
+  const uint32_t sel1 = (lane & 1) ? 0x03070105u : 0x06020400u;
+  const int ms = lane & (NT_BUNDLE - 1), mh = lane >> 5;  // output lane = slot ms, windows 32 mh..
   const uint64_t nb = B.n_bundles;
   uint32_t qi = blockIdx.x % NT_QUEUES, qtried = 0;
   auto claim = [&]() -> uint64_t {
@@ -640,7 +680,7 @@ __device__ __forceinline__ void tscan_bundles(const NtBatch& B, const NtOut& O, 
       if (lane < NT_BUNDLE) {
         TSlot t;
         t.len = len;
-        t.nw = (uint32_t)split_window_count(len, kL);
+        t.nw = o ? (uint32_t)split_window_count(len, kL) : 0u;
         t.r = r;
         t.occ = o ? 1u : 0u;
         const uint64_t wb = wo * kNP, ab = aux_base(wo, r, kNP);
@@ -678,6 +718,7 @@ __device__ __forceinline__ void tscan_bundles(const NtBatch& B, const NtOut& O, 
 #else
       wk.walk(k == 0, acc);
 #endif
+      wk.set_stripe(st + 1, lane, k + kWave < nblk);  // lanes past the bundle's last block load nothing
 #if NT_TS_DBG_NOOUT  // timing experiments only: results are wrong
       {
         uint32_t x = 0;
@@ -689,85 +730,110 @@ __device__ __forceinline__ void tscan_bundles(const NtBatch& B, const NtOut& O, 
         continue;
       }
 #endif
-      wk.set_stripe(st + 1, lane, k + kWave < nblk);  // lanes past the bundle's last block load nothing
-      // ---- outputs, lane = window k, one pass at a time
+      // ---- outputs.  Lane k holds the counts of window k of the stripe for
+      // the 32 slots, bit-sliced.  A byte transpose (in registers, then LDS)
+      // gives row s = slot s's 64 counts: out as whole 128-byte lines (8 lanes
+      // per slot), and at lane 32 h + s (windows 32 h ..) for the checkpoint
+      // sums; the telomeric bits come from a bit-sliced compare and a bit
+      // transpose.  Bitmask words and checkpoints wait in LDS for the flush.
+      const TSlot& mt = sl[ms];
+      const int m_nw = (int)mt.nw;
+      const int k0 = st * kWave + 32 * mh;  // this lane's first window
+      const int nv = m_nw - k0 < 0 ? 0 : (m_nw - k0 > 32 ? 32 : m_nw - k0);  // its windows in the read
+      const int fs = st % Aux::kF;          // the stripe's place in the flush buffers
 #pragma unroll
       for (int p = 0; p < kNP; ++p) {
         uint32_t W[8];
 #pragma unroll
         for (int t = 0; t < 8; ++t) W[t] = acc[p][t];
-        transpose8(W);
-        uint32_t tmv = 0u, RS[16];
+        // telomeric: count >= thr_full, bit-sliced over the slots (bit s = slot s)
+        uint32_t ge = ~0u;
 #pragma unroll
-        for (int t = 0; t < 16; ++t) RS[t] = 0u;
-        // the slots' window counts and count offsets, lane s = slot s (one LDS
-        // round trip; v_readlane per slot below).  No branch per slot: the
-        // counts go out through a buffer resource per slot whose range ends at
-        // the read's last window (the stores past it are dropped), so the
-        // slots' instructions interleave freely.
-        const TSlot& ms = sl[lane & (NT_BUNDLE - 1)];
-        const uint32_t m_nw = ms.occ ? ms.nw : 0u, m_wlo = ms.wb_lo, m_whi = ms.wb_hi;
-        const int k0 = st * kWave;
-        static_for<0, 4>([&](auto gi) {
-          constexpr int g = decltype(gi)::value;
-          // slots are sorted by length: none of 8 g.. has a window here when 8 g has none
-          if (__builtin_amdgcn_readlane((int)m_nw, 8 * g) <= k0) return;
-          static_for<0, 8>([&](auto ji) {
-            constexpr int j = decltype(ji)::value, s = 8 * g + j;
-            const int nw = __builtin_amdgcn_readlane((int)m_nw, s);
-            const uint64_t wb = u64of((uint32_t)__builtin_amdgcn_readlane((int)m_wlo, s),
-                                      (uint32_t)__builtin_amdgcn_readlane((int)m_whi, s));
-            // windows here (kept in SGPRs: a VGPR operand would make the store a waterfall loop)
-            const int nwin = __builtin_amdgcn_readfirstlane(nw - k0 < 0 ? 0 : (nw - k0 > kWave ? kWave : nw - k0));
-            const uint64_t wp = uniform_u64(reinterpret_cast<uint64_t>(O.win_counts + wb + (uint64_t)p * nw + k0));
-            const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
-                reinterpret_cast<uint16_t*>(wp), (short)0, 2 * nwin, 0x00020000);
-            const uint32_t c = (W[j] >> (8 * g)) & 0xFFu;
-            __builtin_amdgcn_raw_buffer_store_b16((unsigned short)c, wr, 2 * lane, 0, 0);
-            const bool valid = lane < nwin;
-            const uint64_t tb = __ballot(valid && c >= thr_full);
-            writelane<2 * s>(tmv, (uint32_t)tb);
-            writelane<2 * s + 1, false>(tmv, (uint32_t)(tb >> 32));
-            // packed row-sum word s & 15, half s >> 4
-            RS[s & 15] |= (valid ? c : 0u) << (16 * (s >> 4));
-          });
-        });
-        // telomeric bitmask word st of every read: lane 2s + h = half h of read s's
-        {
-          const TSlot& t = sl[lane >> 1];
-          if (t.occ && st * kWave < (int)t.nw)
-            reinterpret_cast<uint32_t*>(tmask + u64of(t.ab_lo, t.ab_hi) + (uint64_t)p * aux_nmw((int)t.nw) + st)[lane & 1] =
-                tmv;
+        for (int t = 0; t < 8; ++t) {
+          const uint32_t tm = ((thr_full >> t) & 1u) ? ~0u : 0u;
+          ge = (W[t] & ge) | (~tm & (W[t] | ge));
         }
-        // checkpoints: covered bases before windows 16 j, from the row sums
+        if (thr_full > 255u) ge = 0u;
+        transpose8(W);  // W[j] byte g = count of slot 8 g + j
+        // lane 4 q + i: W[j] byte b = count of slot 8 i + j, window 4 q + b
 #pragma unroll
-        for (int t = 0; t < 16; ++t) {
-          uint32_t v = RS[t];
-          v += dpp0<kDppRowShr + 1, 0xf>(v);
-          v += dpp0<kDppRowShr + 2, 0xf>(v);
-          v += dpp0<kDppRowShr + 4, 0xf>(v);
-          v += dpp0<kDppRowShr + 8, 0xf>(v);
-          if ((lane & 15) == 15) rowtot[(lane >> 4) * 16 + t] = v;
-        }
+        for (int j = 0; j < 8; ++j) W[j] = quad_byte_transpose(W[j], sel2, sel1);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ct[(8 * (lane & 3) + j) * 16 + (lane >> 2)] = W[j];
+        const uint32_t tb = half_bit_transpose(ge, lane) & (nv >= 32 ? ~0u : ((1u << nv) - 1u));
+        tmb[((p * NT_BUNDLE + ms) * Aux::kF + fs) * 2 + mh] = tb;
         wave_sync();
-        if (lane < NT_BUNDLE && sl[lane].occ) {
-          const TSlot& t = sl[lane];
-          const int nw = (int)t.nw;
-          uint32_t* ck = reinterpret_cast<uint32_t*>(tmask + u64of(t.ab_lo, t.ab_hi) + (uint64_t)kNP * aux_nmw(nw)) +
-                         p * aux_nck(nw);
-          uint32_t cum = t.run[p];
+        // window counts: store c covers slots 8 c .. 8 c + 7, lane 8 i + q = 16
+        // bytes (windows 8 q ..) of slot 8 c + i: one line per slot
 #pragma unroll
-          for (int jr = 0; jr < 4; ++jr) {
-            const int jj = st * 4 + jr;
-            if (16 * jj < nw) ck[jj] = cum;
-            cum += (rowtot[jr * 16 + (lane & 15)] >> (16 * (lane >> 4))) & 0xFFFFu;
+        for (int c = 0; c < 4; ++c) {
+          const int s = 8 * c + (lane >> 3), q = lane & 7, kq = st * kWave + 8 * q;
+          const uint4 m = *reinterpret_cast<const uint4*>(sl + s);  // nw, wb_lo, wb_hi
+          const uint2 x = *reinterpret_cast<const uint2*>(ct + s * 16 + 2 * q);
+          if (kq < (int)m.x && !NT_TS_DBG_NOCNT) {
+            uint16_t* w = O.win_counts + u64of(m.y, m.z) + (uint64_t)p * NT_WIN_ROWS((uint64_t)m.x) + kq;
+            *reinterpret_cast<uint4*>(w) =
+                make_uint4(__builtin_amdgcn_perm(0u, x.x, 0x0C010C00u), __builtin_amdgcn_perm(0u, x.x, 0x0C030C02u),
+                           __builtin_amdgcn_perm(0u, x.y, 0x0C010C00u), __builtin_amdgcn_perm(0u, x.y, 0x0C030C02u));
           }
-          sl[lane].run[p] = cum;
-          // the checkpoint at window nw (the read's total) when nw is a multiple of 16
-          if (st == nst - 1 && (nw & 15) == 0) ck[nw >> 4] = cum;
+        }
+        // checkpoints: covered bases before windows 16 jj, jj = 4 st + g
+        const uint4 va = *reinterpret_cast<const uint4*>(ct + ms * 16 + 8 * mh);
+        const uint4 vb = *reinterpret_cast<const uint4*>(ct + ms * 16 + 8 * mh + 4);
+        uint32_t ga = 0u, gb = 0u;
+        ga = __builtin_amdgcn_udot4(va.x, 0x01010101u, ga, false);
+        ga = __builtin_amdgcn_udot4(va.y, 0x01010101u, ga, false);
+        ga = __builtin_amdgcn_udot4(va.z, 0x01010101u, ga, false);
+        ga = __builtin_amdgcn_udot4(va.w, 0x01010101u, ga, false);
+        gb = __builtin_amdgcn_udot4(vb.x, 0x01010101u, gb, false);
+        gb = __builtin_amdgcn_udot4(vb.y, 0x01010101u, gb, false);
+        gb = __builtin_amdgcn_udot4(vb.z, 0x01010101u, gb, false);
+        gb = __builtin_amdgcn_udot4(vb.w, 0x01010101u, gb, false);
+        const uint32_t mine = ga + gb;
+        const uint32_t other = (uint32_t)__shfl_xor((int)mine, 32, kWave);
+        const uint32_t run = mt.run[p];
+        const uint32_t c0 = run + (mh ? other : 0u);  // before window k0
+        uint32_t* ckr = ckb + (p * NT_BUNDLE + ms) * 4 * Aux::kF + 4 * fs + 2 * mh;
+        ckr[0] = c0;
+        ckr[1] = c0 + ga;
+        // the read's total when its windows end with the bundle's last stripe
+        // (no later stripe holds that checkpoint)
+        if (mh && st == nst - 1 && 16 * ((k0 >> 4) + 2) == m_nw && !NT_TS_DBG_NOAUX)
+          reinterpret_cast<uint32_t*>(tmask + u64of(mt.ab_lo, mt.ab_hi) + (uint64_t)kNP * aux_nmw(m_nw))[
+              p * aux_nck(m_nw) + (m_nw >> 4)] = c0 + mine;
+        wave_sync();  // every lane has read ct and run[p]
+        if (mh == 0) sl[ms].run[p] = run + mine + other;
+      }
+      // ---- flush the bitmask words and checkpoints of stripes st0 .. st
+      if ((fs == Aux::kF - 1 || st == nst - 1) && !NT_TS_DBG_NOAUX) {
+        wave_sync();
+        const int st0 = st - fs;
+#pragma unroll
+        for (int p = 0; p < kNP; ++p) {
+          // bitmask words: lane -> (slot, stripe), kF consecutive u64 per slot
+#pragma unroll
+          for (int i = 0; i < NT_BUNDLE * Aux::kF / kWave; ++i) {
+            const int e = i * kWave + lane, s = e / Aux::kF, w = e % Aux::kF, sw = st0 + w;
+            const TSlot& t = sl[s];
+            const int nw = (int)t.nw;
+            if (w <= fs && sw * kWave < nw)
+              tmask[u64of(t.ab_lo, t.ab_hi) + (uint64_t)p * aux_nmw(nw) + sw] =
+                  *reinterpret_cast<const uint64_t*>(tmb + ((p * NT_BUNDLE + s) * Aux::kF + w) * 2);
+          }
+          // checkpoints: lane -> (slot, jj), 4 kF consecutive u32 per slot
+#pragma unroll
+          for (int i = 0; i < NT_BUNDLE * 4 * Aux::kF / kWave; ++i) {
+            const int e = i * kWave + lane, s = e / (4 * Aux::kF), g = e % (4 * Aux::kF), jj = 4 * st0 + g;
+            const TSlot& t = sl[s];
+            const int nw = (int)t.nw;
+            if (g < 4 * (fs + 1) && nw > 0 && 16 * jj <= nw)
+              reinterpret_cast<uint32_t*>(tmask + u64of(t.ab_lo, t.ab_hi) + (uint64_t)kNP * aux_nmw(nw))[
+                  p * aux_nck(nw) + jj] = ckb[(p * NT_BUNDLE + s) * 4 * Aux::kF + g];
+          }
         }
         wave_sync();
       }
+      wave_sync();
     }
     wave_sync();
   }

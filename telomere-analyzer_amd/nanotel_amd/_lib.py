@@ -88,6 +88,7 @@ SIGNATURES = {
     "nt_synchronize": (ctypes.c_int, [_P]),
     "nt_compile": (ctypes.c_int, [_P, ctypes.POINTER(NtParams), ctypes.POINTER(NtProgramInfo)]),
     "nt_window_count": (ctypes.c_int64, [ctypes.c_int64, ctypes.c_int32]),
+    "nt_window_rows": (ctypes.c_uint64, [ctypes.c_int64]),
     "nt_read_blocks": (ctypes.c_uint64, [ctypes.c_uint64]),
     "nt_pack_count": (ctypes.c_int, [_P, _P, ctypes.c_uint64, ctypes.c_int32, _U64P, _U64P, _U64P,
                                      _U64P, _U64P]),

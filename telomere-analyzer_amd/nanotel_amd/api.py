@@ -25,6 +25,14 @@ def window_count(n, subseq_length=100):
     return lib().nt_window_count(int(n), int(subseq_length))
 
 
+def window_rows(nw):
+    """Windows of a read's padded count row (nw rounded up to a multiple of 64;
+    scalar or numpy array): the win_counts / win_off layout, nt_common.h."""
+    if isinstance(nw, np.ndarray):
+        return (nw + 63) // 64 * 64
+    return lib().nt_window_rows(int(nw))
+
+
 def read_blocks(n):
     """32-base blocks of a read's slot in the plane buffer (2*ceil(n/64));
     slots start at even block offsets (16-byte segments)."""
@@ -133,9 +141,10 @@ class NanoTel:
         wc = None
         if want_windows:
             nw = np.array([window_count(int(x), self.subseq_length) for x in lens], np.int64)
+            rows = window_rows(nw)  # padded rows (nt_common.h): 16-byte aligned
             win_off = np.zeros(n, np.int64)
-            win_off[1:] = np.cumsum(nw)[:-1]
-            wc = np.zeros(max(1, int(nw.sum()) * self.n_pass), np.uint16)
+            win_off[1:] = np.cumsum(rows)[:-1]
+            wc = np.zeros(max(1, int(rows.sum()) * self.n_pass), np.uint16)
             out["win_off"] = win_off
             out["n_windows"] = nw
         hits = np.zeros((n, max(1, self.n_hits)), np.uint32) if want_hits else None
@@ -178,7 +187,7 @@ class NanoTel:
     def window_counts(self, res, read, p):
         """Window counts of pass p for read `read` from an analyze(want_windows) result."""
         nw = int(res["n_windows"][read])
-        off = int(res["win_off"][read]) * self.n_pass + p * nw
+        off = int(res["win_off"][read]) * self.n_pass + p * int(window_rows(nw))
         return res["win_counts"][off:off + nw]
 
     # ------------------------------------------------------------------
@@ -186,7 +195,7 @@ class NanoTel:
                          end, density, flags, win_counts, hits=0, exc_off=0, exc_pos=0, exc_code=0,
                          bundles=None):
         """Device-resident hot path: all pointer arguments are device pointers
-        (ints); n_windows = sum of window counts.  bundles: a DeviceBundles
+        (ints); n_windows = sum of the window rows (window_rows).  bundles: a DeviceBundles
         (bundle_plan + bundle_layout_device) or None (per-read scan only).
         Asynchronous on the context stream (see set_stream)."""
         B = self._batch(planes, blk_off, lengths, win_off, n_reads, n_windows, exc_off, exc_pos, exc_code,

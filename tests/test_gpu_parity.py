@@ -236,15 +236,16 @@ def test_device_synth_matches_host_generator():
 def _device_batch(nt, sp, n, read_len, L=100):
     """Synthetic reads generated on the device + the uniform layout (bench path)."""
     import torch
-    from nanotel_amd import read_blocks, window_count
+    from nanotel_amd import read_blocks, window_count, window_rows
     nblk = read_blocks(read_len)
     nw = window_count(read_len, L)
+    rows = window_rows(nw)  # padded count rows (nt_common.h)
     t = dict(
         planes=torch.zeros(n * nblk * 2, dtype=torch.int32, device="cuda"),
         blk_off=torch.empty(n, dtype=torch.int64, device="cuda"),
         lens=torch.empty(n, dtype=torch.int32, device="cuda"),
         win_off=torch.empty(n, dtype=torch.int64, device="cuda"),
-        wc=torch.zeros(n * nw * nt.n_pass, dtype=torch.int16, device="cuda"),
+        wc=torch.zeros(n * rows * nt.n_pass, dtype=torch.int16, device="cuda"),
         start=torch.empty(n * 3, dtype=torch.int32, device="cuda"),
         end=torch.empty(n * 3, dtype=torch.int32, device="cuda"),
         dens=torch.empty(n * 3, dtype=torch.float64, device="cuda"),
@@ -254,13 +255,19 @@ def _device_batch(nt, sp, n, read_len, L=100):
     nt.synth_device(sp, n, t["planes"].data_ptr())
     nt.uniform_layout_device(n, read_len, t["blk_off"].data_ptr(), t["lens"].data_ptr(),
                              t["win_off"].data_ptr())
-    t["nw"] = nw
+    t["nw"], t["rows"] = nw, rows
     return t
+
+
+def _valid_counts(t, n, n_pass, wc=None):
+    """The window counts of a uniform batch without the row padding: (n, n_pass, nw)."""
+    wc = t["wc"] if wc is None else wc
+    return wc.reshape(n, n_pass, t["rows"])[:, :, :t["nw"]]
 
 
 def _run_device(nt, t, n, read_len):
     nt.scan_call_device(t["planes"].data_ptr(), t["blk_off"].data_ptr(), t["lens"].data_ptr(),
-                        t["win_off"].data_ptr(), n, n * t["nw"], read_len, t["start"].data_ptr(),
+                        t["win_off"].data_ptr(), n, n * t["rows"], read_len, t["start"].data_ptr(),
                         t["end"].data_ptr(), t["dens"].data_ptr(), t["flags"].data_ptr(),
                         t["wc"].data_ptr(), hits=t["hits"].data_ptr())
     nt.synchronize()
@@ -283,7 +290,8 @@ def test_device_resident_path_matches_host_path(jit):
     assert np.array_equal(t["dens"].cpu().numpy().reshape(n, 3).view(np.uint64),
                           res["density"].view(np.uint64))
     assert np.array_equal(t["flags"].cpu().numpy(), res["flags"])
-    assert np.array_equal(t["wc"].cpu().numpy().view(np.uint16), res["win_counts"])
+    assert np.array_equal(_valid_counts(t, n, nt.n_pass).cpu().numpy().view(np.uint16),
+                          res["win_counts"].reshape(n, nt.n_pass, -1)[:, :, :t["nw"]])
     assert np.array_equal(t["hits"].cpu().numpy().view(np.uint32).reshape(n, -1), res["hits"])
     compare(nt, res, oracle_rows(seqs[:6], "TTAGGG"))
 
@@ -299,7 +307,7 @@ def _device_bundles(nt, t, n, read_len):
     b = DeviceBundles(d["tplanes"].data_ptr(), d["bnd_read"].data_ptr(), d["bnd_stripe"].data_ptr(),
                       plan.n_bundles, 0, 0, plan.tplane_bytes)
     nt.bundle_layout_device(t["planes"].data_ptr(), t["blk_off"].data_ptr(), t["lens"].data_ptr(),
-                            t["win_off"].data_ptr(), n, n * t["nw"], b)
+                            t["win_off"].data_ptr(), n, n * t["rows"], b)
     nt.synchronize()
     return b, d
 
@@ -321,13 +329,16 @@ def test_device_bundle_scan_matches_per_read_scan(read_len):
         t[k].zero_()
     b, keep = _device_bundles(nt, t, n, read_len)
     nt.scan_call_device(t["planes"].data_ptr(), t["blk_off"].data_ptr(), t["lens"].data_ptr(),
-                        t["win_off"].data_ptr(), n, n * t["nw"], read_len, t["start"].data_ptr(),
+                        t["win_off"].data_ptr(), n, n * t["rows"], read_len, t["start"].data_ptr(),
                         t["end"].data_ptr(), t["dens"].data_ptr(), t["flags"].data_ptr(), t["wc"].data_ptr(),
                         bundles=b)
     nt.synchronize()
     import torch
     for k in ref:
-        assert torch.equal(t[k], ref[k]), k
+        if k == "wc":  # the padding windows are unspecified
+            assert torch.equal(_valid_counts(t, n, nt.n_pass), _valid_counts(t, n, nt.n_pass, ref[k])), k
+        else:
+            assert torch.equal(t[k], ref[k]), k
     seqs = [synth_read_ascii(sp, i) for i in range(0, n, 23)]
     res = {"start": t["start"].cpu().numpy().reshape(n, 3)[::23], "end": t["end"].cpu().numpy().reshape(n, 3)[::23],
            "density": t["dens"].cpu().numpy().reshape(n, 3)[::23], "flags": t["flags"].cpu().numpy()[::23]}
@@ -367,7 +378,7 @@ def test_offsets_beyond_32_bits(jit):
     boff, woff = 1 << 31, 1 << 32  # blocks of 8 bytes, windows
     blk, win = t["blk_off"] + boff, t["win_off"] + woff
     nt.scan_call_device(t["planes"].data_ptr() - boff * 8, blk.data_ptr(), t["lens"].data_ptr(), win.data_ptr(),
-                        n, woff + n * t["nw"], read_len, t["start"].data_ptr(), t["end"].data_ptr(),
+                        n, woff + n * t["rows"], read_len, t["start"].data_ptr(), t["end"].data_ptr(),
                         t["dens"].data_ptr(), t["flags"].data_ptr(), t["wc"].data_ptr() - woff * nt.n_pass * 2)
     nt.synchronize()
     for k in keys:

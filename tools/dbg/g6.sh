@@ -1,0 +1,7 @@
+set -o pipefail
+mkdir -p gpurun_out/g6
+for v in "-DNT_TS_DBG_NOCNT=1" ""; do
+  n=$(echo "x$v" | tr -c 'a-zA-Z0-9' '_')
+  NT_JIT_OPTS="$v" timeout -k 10 200 python bench.py --no-cpu-baseline > gpurun_out/g6/$n.log 2>&1 || { tail -5 gpurun_out/g6/$n.log; exit 1; }
+  echo "$v: $(tail -1 gpurun_out/g6/$n.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); r=d["roofline"]; print(d["value"], r["kernel_avg_ms"], r["call_kernel_avg_ms"])')"
+done
