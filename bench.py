@@ -186,10 +186,21 @@ def main():
     # the bundle layout (the reads transposed 32 to a bundle, the bundle scan's
     # copy of them), built on the device before the timed region like the planes
     bundles, keep = None, []
+    scan_path = "per-read"
+    plan = None
     if nt.tscan and not args.per_read:
-        from nanotel_amd.api import DeviceBundles
         import numpy as np
         plan = nt.bundle_plan(np.full(n, L, np.uint32))
+        # the bundle layout is a second copy of the reads (the calling kernel
+        # reads the per-read planes): when both do not fit, the per-read scan
+        free, _ = torch.cuda.mem_get_info(dev)
+        if plan.tplane_bytes + (4 << 30) > free:
+            plan = None
+            scan_path = "per-read (bundle layout does not fit beside the planes)"
+    if plan is not None:
+        from nanotel_amd.api import DeviceBundles
+        import numpy as np
+        scan_path = "bundle"
         bread = torch.from_numpy(plan.bnd_read.view(np.int32)).to(dev)
         bstripe = torch.from_numpy(plan.bnd_stripe.view(np.int64)).to(dev)
         tpl = torch.empty(max(1, plan.tplane_bytes // 4), dtype=torch.int32, device=dev)
@@ -227,6 +238,7 @@ def main():
     step_ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)]
     n_calls, scan_ms, call_ms = nt.kernel_times()
     assert n_calls == args.steps
+    launches = nt.kernel_launches()  # the bundle scan runs in ranges: per-LAUNCH figures below
     if world > 1:
         t = torch.tensor([wall], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -235,9 +247,9 @@ def main():
     telo = int(((flags & 1) != 0).sum().item())
     total_bases = n * L * world * args.steps
     value = total_bases / wall / 1e9
-    scan_s = scan_ms / n_calls / 1e3
+    scan_s = scan_ms / launches / 1e3
     # no hit counters requested: the scan instance without them runs (no hit bytes)
-    scan_bytes = n * scan_bytes_per_read(L, npass, nw, 0)
+    scan_bytes = n * scan_bytes_per_read(L, npass, nw, 0) * n_calls // launches
     achieved = scan_bytes / scan_s / 1e9
     traffic = None
     if os.path.exists(args.traffic_json):
@@ -263,7 +275,7 @@ def main():
             "data": "synthetic (device counter-based generator, seed 20260501)",
             "config": {"workload": cfg["desc"], "reads_per_gpu": n, "read_len": L,
                        "patterns": cfg["patterns"], "subseq_length": 100, "min_density": 0.6,
-                       "passes": npass, "telomeric_reads_rank0": telo,
+                       "passes": npass, "telomeric_reads_rank0": telo, "scan_path": scan_path,
                        "parallelism": f"dp{world} (read shards)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
@@ -273,6 +285,7 @@ def main():
                                     "nt_scan_jit_nh_lds (scan specialised for the patterns, hiprtc)" if nt.jit
                                     else "nt::nt_scan_kernel (ahead-of-time scan)"),
                          "kernel_avg_ms": round(scan_s * 1e3, 4),
+                         "kernel_launches_per_step": launches // n_calls,
                          "algorithmic_bytes_per_launch": scan_bytes,
                          "call_kernel": "nt::nt_call_kernel",
                          "call_kernel_avg_ms": round(call_ms / n_calls, 4),

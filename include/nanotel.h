@@ -176,9 +176,15 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
  * the context stream around its scan kernel(s) and its calling kernel.
  * nt_kernel_times waits for them and returns the summed spans of the calls
  * since the previous nt_kernel_times (or nt_set_profiling); returns the
- * number of calls, or < 0. */
+ * number of calls, or < 0.  With the bundle scan in ranges (NT_TSUB), whose
+ * calling kernels run beside the next range's scan on a second stream,
+ * scan_ms sums the bundle-scan kernels' spans and call_ms is the remainder
+ * of the call (the calling not hidden behind them). */
 int nt_set_profiling(nt_ctx* ctx, int on);
 int64_t nt_kernel_times(nt_ctx* ctx, double* scan_ms, double* call_ms);
+/* Scan-kernel launches (bundle-scan ranges count one each) behind the last
+ * nt_kernel_times: scan_ms / this = the scan kernel's average launch. */
+int64_t nt_kernel_launches(const nt_ctx* ctx);
 
 /* Host-buffer convenience: pack (+rc), upload, scan+call, download, sync.
  * win_counts/hits optional.  Returns the first per-read error, if any. */

@@ -277,7 +277,12 @@ struct nt_ctx {
   hipStream_t call_stream = nullptr;  // sub-batched calling kernels (NT_SUBBATCH > 1)
   hipEvent_t ev_scan = nullptr, ev_call = nullptr;
   bool profile = false;  // HIP events around the scan and call kernels of every call
-  std::vector<std::array<hipEvent_t, 3>> ev;
+  // per recorded call: [0] start, [1] end of the scans (serial calling), [2]
+  // end, [3 + 2k], [4 + 2k] around bundle-scan range k (overlapped calling)
+  static constexpr int kMaxTsub = 16;
+  std::vector<std::array<hipEvent_t, 3 + 2 * kMaxTsub>> ev;
+  std::vector<int> ev_nt;  // bundle-scan ranges of each recorded call
+  int64_t last_launches = 0;  // scan-kernel launches of the last nt_kernel_times window
   size_t n_ev = 0;  // calls recorded since the last nt_kernel_times
   bool jit = false;  // hiprtc-specialised scan kernels (nt_jit.cpp)
   void* jit_fn[4] = {};  // [no hit counters ? 2 : 0] + [global scratch ? 1 : 0]
@@ -696,37 +701,86 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
   uint64_t nsub = 1;
   if (const char* v = std::getenv("NT_SUBBATCH")) nsub = std::max<uint64_t>(1, std::strtoull(v, nullptr, 10));
   nsub = std::min<uint64_t>(nsub, std::max<uint64_t>(1, batch->n_reads / 256));
-  if (tscan) nsub = 1;
+  // the bundle scan's sub-batches (bundle ranges): the calling kernel of range
+  // k runs on the call stream beside the bundle scan of range k+1 (the scan is
+  // bandwidth-bound, the calling latency-bound); NT_TSUB, default 2 (1M x 50 kb:
+  // 3.62 / 3.54 / 3.55 / 3.66 ms per batch at 1 / 2 / 4 / 8)
+  uint64_t tsub = 1;
+  if (tscan) {
+    nsub = 1;
+    tsub = 2;
+    if (const char* v = std::getenv("NT_TSUB")) tsub = std::max<uint64_t>(1, std::strtoull(v, nullptr, 10));
+    tsub = std::min<uint64_t>({tsub, std::max<uint64_t>(1, batch->n_bundles / 64), (uint64_t)nt_ctx::kMaxTsub});
+  }
   int bpc_cap = 0;
   if (const char* v = std::getenv("NT_SCAN_WAVES")) bpc_cap = std::atoi(v);
-  if (nsub > 1 && !ctx->call_stream) {
+  if ((nsub > 1 || tsub > 1) && !ctx->call_stream) {
     if ((e = hipStreamCreateWithFlags(&ctx->call_stream, hipStreamNonBlocking)) != hipSuccess)
       return hip_fail(ctx, e, "hipStreamCreate(call)");
     if ((e = hipEventCreateWithFlags(&ctx->ev_scan, hipEventDisableTiming)) != hipSuccess ||
         (e = hipEventCreateWithFlags(&ctx->ev_call, hipEventDisableTiming)) != hipSuccess)
       return hip_fail(ctx, e, "hipEventCreate");
   }
-  // read queues: two per sub-batch (LDS and global-scratch launches), zeroed on the stream
-  if ((e = ctx->queue.ensure((2 * nsub + 1) * NT_QUEUE_WORDS * 8)) != hipSuccess) return hip_fail(ctx, e, "hipMalloc(queue)");
+  // read queues: two per sub-batch (LDS and global-scratch launches) and one
+  // per bundle range, zeroed on the stream
+  const uint64_t nqueue = 2 * nsub + tsub;
+  if ((e = ctx->queue.ensure(nqueue * NT_QUEUE_WORDS * 8)) != hipSuccess) return hip_fail(ctx, e, "hipMalloc(queue)");
   unsigned long long* queue = (unsigned long long*)ctx->queue.p;
   hipEvent_t* ev = nullptr;
   if (ctx->profile) {
     if (ctx->n_ev == ctx->ev.size()) {
-      std::array<hipEvent_t, 3> a{};
+      std::array<hipEvent_t, 3 + 2 * nt_ctx::kMaxTsub> a{};
       for (hipEvent_t& x : a)
         if ((e = hipEventCreate(&x)) != hipSuccess) return hip_fail(ctx, e, "hipEventCreate");
       ctx->ev.push_back(a);
+      ctx->ev_nt.push_back(0);
     }
     ev = ctx->ev[ctx->n_ev++].data();
+    ctx->ev_nt[ctx->n_ev - 1] = 0;
     (void)hipEventRecord(ev[0], ctx->stream);
   }
-  if ((e = hipMemsetAsync(queue, 0, (2 * nsub + 1) * NT_QUEUE_WORDS * 8, ctx->stream)) != hipSuccess) return hip_fail(ctx, e, "hipMemsetAsync(queue)");
-  if (tscan) {  // the bundle scan first: one wave per bundle, exactly the resident blocks
-    const uint64_t tgrid = std::max<uint64_t>(1, std::min<uint64_t>((batch->n_bundles + 3) / 4,
-                                                                    (uint64_t)ctx->cu_count * ctx->tscan_bpc));
-    e = nt_tjit_launch(ctx->tjit_fn, (int)tgrid, ctx->stream, &B, &O, tmask, queue + 2 * nsub * NT_QUEUE_WORDS,
-                       ctx->thr_h[std::min<size_t>((size_t)L, ctx->thr_h.size() - 1)]);
-    if (e != hipSuccess) return hip_fail(ctx, e, "launch nt_tscan_jit");
+  if ((e = hipMemsetAsync(queue, 0, nqueue * NT_QUEUE_WORDS * 8, ctx->stream)) != hipSuccess) return hip_fail(ctx, e, "hipMemsetAsync(queue)");
+  // fault isolation (debugging): NT_DBG_SKIP_SCAN / NT_DBG_SKIP_CALL launch only the other kernel
+  const bool dbg_skip_scan = std::getenv("NT_DBG_SKIP_SCAN") != nullptr;
+  const bool dbg_skip_call = std::getenv("NT_DBG_SKIP_CALL") != nullptr;
+  if (tscan) {
+    // the bundle scan first: one wave per bundle, exactly the resident blocks
+    // (one per CU while a calling kernel runs beside it: room for its waves)
+    const uint32_t thr_full = ctx->thr_h[std::min<size_t>((size_t)L, ctx->thr_h.size() - 1)];
+    const int tbpc = tsub > 1 ? 1 : ctx->tscan_bpc;
+    for (uint64_t k = 0; k < tsub; ++k) {
+      const uint64_t b0 = batch->n_bundles * k / tsub, b1 = batch->n_bundles * (k + 1) / tsub;
+      NtBatch Bt = B;  // bundles [b0, b1): bnd_stripe stays absolute
+      Bt.bnd_read += NT_BUNDLE * b0;
+      Bt.bnd_stripe += b0;
+      Bt.n_bundles = b1 - b0;
+      const uint64_t tgrid = std::max<uint64_t>(1, std::min<uint64_t>((Bt.n_bundles + 3) / 4, (uint64_t)ctx->cu_count * tbpc));
+      if (ev) (void)hipEventRecord(ev[3 + 2 * k], ctx->stream);
+      e = nt_tjit_launch(ctx->tjit_fn, (int)tgrid, ctx->stream, &Bt, &O, tmask,
+                         queue + (2 * nsub + k) * NT_QUEUE_WORDS, thr_full);
+      if (e != hipSuccess) return hip_fail(ctx, e, "launch nt_tscan_jit");
+      if (ev) {
+        (void)hipEventRecord(ev[4 + 2 * k], ctx->stream);
+        ctx->ev_nt[ctx->n_ev - 1] = (int)(k + 1);
+      }
+      // its reads' calling (the bundles' slots; the last window of each recounted)
+      NtBatch Bc = B;
+      Bc.list = Bt.bnd_read;
+      Bc.n_list = NT_BUNDLE * Bt.n_bundles;
+      const uint64_t lanes = Bc.n_list * (np <= 2 ? 2u : 4u);
+      const int cgrid = (int)std::max<uint64_t>(1, std::min<uint64_t>((lanes + 255) / 256, (uint64_t)ctx->cu_count * 64));
+      hipStream_t cs = ctx->stream;
+      if (tsub > 1) {
+        if ((e = hipEventRecord(ctx->ev_scan, ctx->stream)) != hipSuccess ||
+            (e = hipStreamWaitEvent(ctx->call_stream, ctx->ev_scan, 0)) != hipSuccess)
+          return hip_fail(ctx, e, "stream dependency");
+        cs = ctx->call_stream;
+      }
+      if (!dbg_skip_call &&
+          (e = nt_dev_launch_call(ctx->prog_dev, &Bc, &O, tmask, (const uint32_t*)ctx->thr.p,
+                                  (uint32_t)ctx->thr_h.size(), 1, cgrid, cs)) != hipSuccess)
+        return hip_fail(ctx, e, "launch nt_call_kernel");
+    }
   }
   const uint32_t ww_lds = nt_dev_wave_words(noslots, nh, np, cap_nw);
   const size_t lds_bytes = (size_t)ww_lds * 4u * 4u;
@@ -737,9 +791,6 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
                      : nt_dev_scan_blocks_per_cu(single, one, m6, 1, lds_bytes);
   if (bpc <= 0) bpc = 1;
   if (bpc_cap > 0) bpc = std::min(bpc, bpc_cap);
-  // fault isolation (debugging): NT_DBG_SKIP_SCAN / NT_DBG_SKIP_CALL launch only the other kernel
-  const bool dbg_skip_scan = std::getenv("NT_DBG_SKIP_SCAN") != nullptr;
-  const bool dbg_skip_call = std::getenv("NT_DBG_SKIP_CALL") != nullptr;
   const uint32_t ww_g = nt_dev_wave_words(noslots, nh, np, max_nw);
   const uint64_t grid_g = std::max<uint64_t>(1, std::min<uint64_t>((batch->n_reads + 3) / 4, (uint64_t)ctx->cu_count * 2));
   if (two && (e = ctx->scratch.ensure(grid_g * 4 * (uint64_t)ww_g * 4)) != hipSuccess)
@@ -808,11 +859,19 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
     // one lane per (read, pass): 2 lanes per read, 4 with TVRs
     const uint64_t call_lanes = nr * (np <= 2 ? 2u : 4u);
     const uint64_t call_grid = std::max<uint64_t>(1, std::min<uint64_t>((call_lanes + 255) / 256, (uint64_t)ctx->cu_count * 64));
-    if (nsub == 1) {
+    if (tscan) {
+      // the reads of the per-read scan (the bundled ones are called above)
+      if (n_scan > 0 && !dbg_skip_call) {
+        const uint64_t lanes = n_scan * (np <= 2 ? 2u : 4u);
+        const int cgrid = (int)std::max<uint64_t>(1, std::min<uint64_t>((lanes + 255) / 256, (uint64_t)ctx->cu_count * 64));
+        e = nt_dev_launch_call(ctx->prog_dev, &Bk, &Ok, tmk, (const uint32_t*)ctx->thr.p, (uint32_t)ctx->thr_h.size(),
+                               0, cgrid, ctx->stream);
+      }
+    } else if (nsub == 1) {
       if (ev) (void)hipEventRecord(ev[1], ctx->stream);
       e = dbg_skip_call ? hipSuccess
                         : nt_dev_launch_call(ctx->prog_dev, &Bk, &Ok, tmk, (const uint32_t*)ctx->thr.p,
-                                             (uint32_t)ctx->thr_h.size(), tscan ? 1 : 0, (int)call_grid, ctx->stream);
+                                             (uint32_t)ctx->thr_h.size(), 0, (int)call_grid, ctx->stream);
     } else {
       // calling kernel of this sub-batch on the call stream, after its scan
       if ((e = hipEventRecord(ctx->ev_scan, ctx->stream)) != hipSuccess ||
@@ -823,7 +882,7 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
     }
     if (e != hipSuccess) return hip_fail(ctx, e, "launch nt_call_kernel");
   }
-  if (nsub > 1) {
+  if (nsub > 1 || tsub > 1) {
     if (ev) (void)hipEventRecord(ev[1], ctx->stream);  // end of the last scan
     if ((e = hipEventRecord(ctx->ev_call, ctx->call_stream)) != hipSuccess ||
         (e = hipStreamWaitEvent(ctx->stream, ctx->ev_call, 0)) != hipSuccess)
@@ -888,6 +947,8 @@ int nt_bundle_layout(nt_ctx* ctx, const nt_batch* batch, uint32_t* tplanes, uint
   return e == hipSuccess ? NT_OK : hip_fail(ctx, e, "launch nt_bundle_kernel");
 }
 
+int64_t nt_kernel_launches(const nt_ctx* ctx) { return ctx ? ctx->last_launches : NT_E_ARG; }
+
 int nt_set_profiling(nt_ctx* ctx, int on) {
   if (!ctx) return NT_E_ARG;
   ctx->profile = on != 0;
@@ -898,18 +959,33 @@ int nt_set_profiling(nt_ctx* ctx, int on) {
 int64_t nt_kernel_times(nt_ctx* ctx, double* scan_ms, double* call_ms) {
   if (!ctx || !ctx->profile) return NT_E_STATE;
   double a = 0.0, b = 0.0;
+  int64_t launches = 0;
   for (size_t i = 0; i < ctx->n_ev; ++i) {
+    launches += ctx->ev_nt[i] > 0 ? ctx->ev_nt[i] : 1;
     hipEvent_t* ev = ctx->ev[i].data();
     hipError_t e = hipEventSynchronize(ev[2]);
     if (e != hipSuccess) return hip_fail(ctx, e, "hipEventSynchronize");
     float x = 0.f, y = 0.f;
-    if ((e = hipEventElapsedTime(&x, ev[0], ev[1])) != hipSuccess) return hip_fail(ctx, e, "hipEventElapsedTime");
-    if ((e = hipEventElapsedTime(&y, ev[1], ev[2])) != hipSuccess) return hip_fail(ctx, e, "hipEventElapsedTime");
+    if (ctx->ev_nt[i] > 0) {  // bundle scan: its kernels' spans; the rest is calling not hidden behind them
+      float t = 0.f;
+      if ((e = hipEventElapsedTime(&t, ev[0], ev[2])) != hipSuccess) return hip_fail(ctx, e, "hipEventElapsedTime");
+      for (int k = 0; k < ctx->ev_nt[i]; ++k) {
+        float z = 0.f;
+        if ((e = hipEventElapsedTime(&z, ev[3 + 2 * k], ev[4 + 2 * k])) != hipSuccess)
+          return hip_fail(ctx, e, "hipEventElapsedTime");
+        x += z;
+      }
+      y = t - x;
+    } else {
+      if ((e = hipEventElapsedTime(&x, ev[0], ev[1])) != hipSuccess) return hip_fail(ctx, e, "hipEventElapsedTime");
+      if ((e = hipEventElapsedTime(&y, ev[1], ev[2])) != hipSuccess) return hip_fail(ctx, e, "hipEventElapsedTime");
+    }
     a += x;
     b += y;
   }
   if (scan_ms) *scan_ms = a;
   if (call_ms) *call_ms = b;
+  ctx->last_launches = launches;
   const int64_t n = (int64_t)ctx->n_ev;
   ctx->n_ev = 0;
   return n;

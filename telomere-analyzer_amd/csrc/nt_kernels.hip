@@ -783,12 +783,13 @@ nt_call_kernel(const NtProgram* __restrict__ prog, NtBatch B, NtOut O,
   __shared__ uint32_t pw_lds[20 * 256];
 #endif
   const int lg = np <= 2 ? 1 : 2;  // log2(G)
-  const uint64_t total = B.n_reads << lg;
+  // the reads: B.list[0 .. n_list) when given (~0u entries: none), else all
+  const uint64_t total = (B.list ? B.n_list : B.n_reads) << lg;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t base = blockIdx.x * (uint64_t)blockDim.x; base < total; base += stride) {
     const uint64_t idx = base + threadIdx.x;
-    const bool in = idx < total;  // whole waves stay in the loop for the shuffles
-    const uint64_t r = idx >> lg;
+    const uint64_t r = idx < total ? (B.list ? (uint64_t)B.list[idx >> lg] : idx >> lg) : 0;
+    const bool in = idx < total && r != 0xFFFFFFFFull;  // whole waves stay in the loop for the shuffles
     const int p = (int)(idx & ((1u << lg) - 1u));
     int s = -1, e = -1;
     double d = 0.0;

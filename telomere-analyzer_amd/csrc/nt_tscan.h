@@ -395,6 +395,12 @@ struct TPipe {
 #ifndef NT_TS_DBG_NOCNT
 #define NT_TS_DBG_NOCNT 0
 #endif
+#ifndef NT_TS_LOAD_AUX  // cache policy bits of the T-layout loads (experiments)
+#define NT_TS_LOAD_AUX 0
+#endif
+#ifndef NT_TS_NTSTORE  // non-temporal window-count stores (experiments)
+#define NT_TS_NTSTORE 1
+#endif
 #ifndef NT_TS_XPRIME
 #define NT_TS_XPRIME 0
 #endif
@@ -451,7 +457,7 @@ struct TWalker {
   TPipe<TP, Pats, Tvrs> pp;
 
   __device__ __forceinline__ uint4 ld(int voff, int soff) {
-    const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0);
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, NT_TS_LOAD_AUX);
 #if NT_TS_PIN
     __builtin_amdgcn_sched_barrier(0);  // keep the load where it is issued (8 slots ahead)
 #endif
@@ -772,9 +778,16 @@ __device__ __forceinline__ void tscan_bundles(const NtBatch& B, const NtOut& O, 
           const uint2 x = *reinterpret_cast<const uint2*>(ct + s * 16 + 2 * q);
           if (kq < (int)m.x && !NT_TS_DBG_NOCNT) {
             uint16_t* w = O.win_counts + u64of(m.y, m.z) + (uint64_t)p * NT_WIN_ROWS((uint64_t)m.x) + kq;
-            *reinterpret_cast<uint4*>(w) =
+            const uint4 v =
                 make_uint4(__builtin_amdgcn_perm(0u, x.x, 0x0C010C00u), __builtin_amdgcn_perm(0u, x.x, 0x0C030C02u),
                            __builtin_amdgcn_perm(0u, x.y, 0x0C010C00u), __builtin_amdgcn_perm(0u, x.y, 0x0C030C02u));
+#if NT_TS_NTSTORE
+            typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+            const u32x4 vv = {v.x, v.y, v.z, v.w};
+            __builtin_nontemporal_store(vv, reinterpret_cast<u32x4*>(w));
+#else
+            *reinterpret_cast<uint4*>(w) = v;
+#endif
           }
         }
         // checkpoints: covered bases before windows 16 jj, jj = 4 st + g

@@ -104,6 +104,11 @@ class NanoTel:
         n = _check(lib().nt_kernel_times(self._h, ctypes.byref(a), ctypes.byref(b)), self._h)
         return int(n), a.value, b.value
 
+    def kernel_launches(self):
+        """Scan-kernel launches behind the last kernel_times() (a bundle scan in
+        ranges launches once per range): scan_ms / this = one launch."""
+        return int(_check(lib().nt_kernel_launches(self._h), self._h))
+
     def synchronize(self):
         _check(lib().nt_synchronize(self._h), self._h)
 

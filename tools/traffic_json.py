@@ -21,7 +21,7 @@ def per_dispatch(path, counter, match):
 def main():
     out, config, reads, jit = sys.argv[1], sys.argv[2], int(sys.argv[3]), bool(int(sys.argv[4]))
     dest = sys.argv[5] if len(sys.argv) > 5 else "profiles/pmc_traffic.json"
-    is_scan = lambda k: "nt_scan" in k  # noqa: E731
+    is_scan = lambda k: "nt_scan" in k or "nt_tscan" in k  # noqa: E731 (per-read or bundle scan)
     is_call = lambda k: "nt_call_kernel" in k  # noqa: E731
     res = {"config": config, "reads": reads, "jit": jit,
            "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), per dispatch mean; "
