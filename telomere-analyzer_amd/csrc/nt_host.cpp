@@ -32,7 +32,8 @@ int nt_dev_scan_blocks_per_cu(int single, int one, int m6, int lds, size_t lds_b
 hipError_t nt_dev_launch_call(const NtProgram* prog, const NtBatch* B, const NtOut* O,
                               const uint64_t* tmask, const uint32_t* thr, uint32_t thr_size, int fix_last,
                               int call_grid, hipStream_t stream);
-hipError_t nt_dev_launch_bundle(const NtBatch* B, uint32_t* tp, int L, hipStream_t stream, int cu_count);
+hipError_t nt_dev_launch_bundle(const NtBatch* B, uint64_t n_stripes, uint32_t* tp, int L, uint32_t div_m,
+                                uint32_t div_s, hipStream_t stream, int cu_count);
 hipError_t nt_dev_launch_synth(const NtSynth* S, uint32_t* planes, uint64_t n_reads,
                                hipStream_t stream);
 hipError_t nt_dev_launch_filter(const NtProgram* prog, const NtBatch* B, uint8_t* keep,
@@ -939,11 +940,14 @@ int nt_bundle_layout(nt_ctx* ctx, const nt_batch* batch, uint32_t* tplanes, uint
   if (!ctx->compiled) return fail(ctx, NT_E_STATE, "nt_compile() not called");
   if (batch->n_bundles == 0) return NT_OK;
   (void)hipSetDevice(ctx->device);
-  hipError_t e = hipMemsetAsync(tplanes, 0, tplane_bytes, ctx->stream);
-  if (e != hipSuccess) return hip_fail(ctx, e, "hipMemsetAsync(tplanes)");
+  if (ctx->prog.L > 170) return fail(ctx, NT_E_ARG, "bundle layout: subseq_length > 170 has no bundle scan");
+  // the kernel writes every word of every stripe (zeros past the reads)
+  const uint64_t stripe_bytes = (uint64_t)((ctx->prog.L + 1) / 2) * 64 * 16;
+  if (tplane_bytes % stripe_bytes) return fail(ctx, NT_E_ARG, "tplane_bytes is not a whole number of stripes");
   NtBatch B{batch->planes, batch->blk_off, batch->len, batch->win_off, nullptr, nullptr, nullptr, batch->n_reads,
             nullptr, 0, tplanes, batch->bnd_read, batch->bnd_stripe, batch->n_bundles};
-  e = nt_dev_launch_bundle(&B, tplanes, ctx->prog.L, ctx->stream, ctx->cu_count);
+  hipError_t e = nt_dev_launch_bundle(&B, tplane_bytes / stripe_bytes, tplanes, ctx->prog.L, ctx->prog.div32_m,
+                                      ctx->prog.div32_s, ctx->stream, ctx->cu_count);
   return e == hipSuccess ? NT_OK : hip_fail(ctx, e, "launch nt_bundle_kernel");
 }
 

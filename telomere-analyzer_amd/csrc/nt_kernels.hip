@@ -918,54 +918,98 @@ nt_layout_kernel(uint64_t n_reads, uint64_t nblk, uint64_t read_len, uint64_t nw
 // ================================================================ bundles
 //
 // The T-layout of the bundle scan (nt_common.h) from the per-read planes: one
-// wave per (bundle, 32 positions): lane s < 32 holds slot s's low-plane word,
-// lane 32 + s its high-plane word, so ballot(bit i) is the {lo, hi} pair of
-// position 32x + i for all 32 reads -- 32 ballots transpose the 32 x 32 bit
-// blocks of both planes.  Positions past a read (and empty slots) are 0.
-// (hipcc inserts no wait states around inline asm, and x is an SGPR pair a
-// v_cmp -- a ballot -- has just written: the VALU-writes-SGPR ->
-// v_writelane-reads-it hazard needs them; without, ballot bits were lost)
-template <int kLane>
-__device__ __forceinline__ void writelane_k(uint32_t& v, uint32_t x) {
-  asm volatile("s_nop 4\n\tv_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(x), "i"(kLane));
-}
+// workgroup per bundle, its half stripes in turn (32 blocks = 32 L positions =
+// L plane words of each of the bundle's 32 reads).  The half stripe's words
+// of the 32 reads come into LDS by coalesced loads; then per step every lane
+// takes one {lo, hi} word of its read (lanes 0-31: word w of slot s, lanes
+// 32-63: word w + 1; the 4 waves every 4th step), masked past the read end,
+// and two 32 x 32 bit transposes inside each half wave turn
+// them into the 32-slot columns of 32 positions; these go to an LDS copy of
+// the half stripe's T-layout rows (row t: 32 words of 16 bytes, 8-byte halves
+// by position parity), written out as whole 512-byte row runs.  Every word of
+// every stripe is written (zeros past the reads): no memset first.
+constexpr int kBndRowWords = 132;  // LDS row stride (words): 128 + 4 spreads the banks
 
 __global__ void __launch_bounds__(256)
-nt_bundle_kernel(NtBatch B, uint32_t* __restrict__ tp, int L) {
-  const int lane = threadIdx.x & (kWave - 1);
-  const uint64_t T = (uint64_t)(L + 1) / 2;
-  const uint64_t W = (uint64_t)gridDim.x * kNWaves;
-  const uint64_t w0 = (uint64_t)blockIdx.x * kNWaves + (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-  for (uint64_t b = w0; b < B.n_bundles; b += W) {
-    const uint32_t r = B.bnd_read[b * NT_BUNDLE + (lane & 31)];
-    const bool occ = r != 0xFFFFFFFFu;
-    const uint32_t len = occ ? B.len[r] : 0u;
-    const uint64_t boff = occ ? B.blk_off[r] : 0ull;
-    const uint32_t nmax = (uint32_t)__builtin_amdgcn_readfirstlane((int)len);  // slot 0 = longest
-    const uint64_t g0 = uniform_u64(B.bnd_stripe[b]);
-    const uint64_t npos = (uint64_t)((nmax + L - 1) / L) * L;  // positions of the bundle's blocks
-    const uint2* blk = reinterpret_cast<const uint2*>(B.planes) + boff;
-    for (uint32_t x = 0; 32 * x < nmax; ++x) {
-      uint32_t wv = 0u;
-      if (32 * x < len) {
-        const uint2 v = blk[x];
-        wv = lane < 32 ? v.x : v.y;
-        if (32 * x + 32 > len) wv &= (1u << (len - 32 * x)) - 1u;
-      }
-      uint32_t lo = 0u, hi = 0u;
-      static_for<0, 32>([&](auto ii) {
-        constexpr int i = decltype(ii)::value;
-        const uint64_t bal = __ballot((wv >> i) & 1u);
-        writelane_k<i>(lo, (uint32_t)bal);
-        writelane_k<i>(hi, (uint32_t)(bal >> 32));
-      });
-      const uint64_t q = 32ull * x + lane;
-      if (lane < 32 && q < npos) {
-        const uint64_t kq = q / (uint64_t)L, o = q - kq * L;
-        const uint64_t word = (g0 + (kq >> 6)) * T * kWave + (o >> 1) * kWave + (kq & 63);  // 16-byte words
-        reinterpret_cast<uint2*>(tp)[word * 2 + (o & 1)] = make_uint2(lo, hi);
-      }
+nt_bundle_kernel(NtBatch B, uint32_t* __restrict__ tp, int L, uint32_t div_m, uint32_t div_s) {
+  extern __shared__ uint32_t lds[];
+  const int T = (L + 1) / 2;
+  const int R = 2 * L + 2;                // words per read in the input copy (bank spread)
+  uint32_t* in = lds;                     // [32][R]: the half stripe's plane words of each read
+  uint32_t* rows = lds + NT_BUNDLE * R;   // [T][kBndRowWords]: its T-layout rows
+  uint32_t* meta = rows + T * kBndRowWords;  // [32][4]: len, block offset lo / hi of each slot
+  const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x >> 6;
+  const int s = lane & 31, hh = lane >> 5;
+  const BitTr bt(lane);
+  for (uint64_t b = blockIdx.x; b < B.n_bundles; b += gridDim.x) {
+    const uint32_t r = B.bnd_read[b * NT_BUNDLE + s];
+    const int64_t len = r != 0xFFFFFFFFu ? (int64_t)B.len[r] : 0;
+    const uint64_t g0 = uniform_u64(B.bnd_stripe[b]), g1 = uniform_u64(B.bnd_stripe[b + 1]);
+    if (threadIdx.x < NT_BUNDLE) {
+      const uint64_t bo = r != 0xFFFFFFFFu ? B.blk_off[r] : 0ull;
+      *reinterpret_cast<uint4*>(meta + 4 * s) = make_uint4((uint32_t)len, (uint32_t)bo, (uint32_t)(bo >> 32), 0u);
     }
+    __syncthreads();
+    for (uint64_t u = 0; u < 2 * (g1 - g0); ++u) {  // half stripes of the bundle
+      const uint64_t G = g0 + (u >> 1);
+      const int h = (int)(u & 1);
+      const uint64_t w0 = (uint64_t)L * u;  // first plane word of the half stripe
+      // 1. the 32 reads' words [w0, w0 + L) into LDS, coalesced (8 bytes a
+      // thread), every load of the thread issued before the first is used
+      {
+        constexpr int kMaxE = (NT_BUNDLE * 170 + 255) / 256;  // L <= 170 (nt_tscan_eligible)
+        uint2 v[kMaxE];
+#pragma unroll
+        for (int k = 0; k < kMaxE; ++k) {
+          const uint32_t e = threadIdx.x + 256u * k;
+          v[k] = make_uint2(0u, 0u);
+          if (e < (uint32_t)(NT_BUNDLE * L)) {
+            const uint32_t rs = __umulhi(e, div_m) >> div_s, wd = e - rs * (uint32_t)L;
+            const uint4 m = *reinterpret_cast<const uint4*>(meta + 4 * rs);
+            if (32 * (int64_t)(w0 + wd) < (int64_t)m.x)  // (empty slots have len 0)
+              v[k] = reinterpret_cast<const uint2*>(B.planes)[(((uint64_t)m.z << 32) | m.y) + w0 + wd];
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < kMaxE; ++k) {
+          const uint32_t e = threadIdx.x + 256u * k;
+          if (e < (uint32_t)(NT_BUNDLE * L)) {
+            const uint32_t rs = __umulhi(e, div_m) >> div_s, wd = e - rs * (uint32_t)L;
+            *reinterpret_cast<uint2*>(in + rs * R + 2 * wd) = v[k];
+          }
+        }
+      }
+      if ((L & 1) && threadIdx.x < 32)  // odd L: the last row's second half holds no position
+        *reinterpret_cast<uint2*>(rows + (T - 1) * kBndRowWords + 4 * s + 2) = make_uint2(0u, 0u);
+      __syncthreads();
+      // 2. wave wv takes the steps wv, wv + 4, ... (step = 2 words: lanes 0-31
+      // the first, 32-63 the second): lane 32 hh + i gets the 32-read columns
+      // of position 32 wl + i
+      for (int w = 2 * wv; w < L; w += 8) {
+        const int wl = w + hh;
+        uint2 v = make_uint2(0u, 0u);
+        if (wl < L) {
+          v = *reinterpret_cast<const uint2*>(in + s * R + 2 * wl);
+          const int64_t nb = len - 32 * (int64_t)(w0 + wl);  // valid bases of the word
+          const uint32_t m = nb >= 32 ? ~0u : nb <= 0 ? 0u : ((1u << nb) - 1u);
+          v.x &= m;
+          v.y &= m;
+        }
+        const uint32_t cl = half_bit_transpose(v.x, lane, bt), ch = half_bit_transpose(v.y, lane, bt);
+        if (wl < L) {
+          const uint32_t p = 32u * (uint32_t)wl + (uint32_t)s;  // position in the half stripe
+          const uint32_t l = __umulhi(p, div_m) >> div_s, o = p - l * (uint32_t)L;
+          *reinterpret_cast<uint2*>(rows + (o >> 1) * kBndRowWords + 4 * l + 2 * (o & 1)) = make_uint2(cl, ch);
+        }
+      }
+      __syncthreads();
+      // 3. rows t: 32 words of 16 bytes at word (G T + t) 64 + 32 h + l
+      uint4* out = reinterpret_cast<uint4*>(tp) + G * (uint64_t)T * kWave + 32 * h;
+      for (int t = threadIdx.x >> 5; t < T; t += 8)
+        out[(uint64_t)t * kWave + s] = *reinterpret_cast<const uint4*>(rows + t * kBndRowWords + 4 * s);
+      __syncthreads();
+    }
+    __syncthreads();  // meta is rewritten for the next bundle
   }
 }
 
@@ -1147,11 +1191,14 @@ hipError_t nt_dev_launch_call(const NtProgram* prog, const NtBatch* B, const NtO
   return hipGetLastError();
 }
 
-hipError_t nt_dev_launch_bundle(const NtBatch* B, uint32_t* tp, int L, hipStream_t stream, int cu_count) {
-  uint64_t grid = (B->n_bundles + 3) / 4;
-  if (grid > (uint64_t)cu_count * 8) grid = (uint64_t)cu_count * 8;
-  if (grid == 0) grid = 1;
-  hipLaunchKernelGGL(nt::nt_bundle_kernel, dim3((uint32_t)grid), dim3(256), 0, stream, *B, tp, L);
+hipError_t nt_dev_launch_bundle(const NtBatch* B, uint64_t n_stripes, uint32_t* tp, int L, uint32_t div_m,
+                                uint32_t div_s, hipStream_t stream, int cu_count) {
+  // one workgroup per bundle (its half stripes in turn), a grid-stride loop over them
+  uint64_t grid = n_stripes ? B->n_bundles : 0;
+  if (grid > (uint64_t)cu_count * 16) grid = (uint64_t)cu_count * 16;
+  if (grid == 0) return hipSuccess;
+  const size_t lds = ((size_t)((L + 1) / 2) * nt::kBndRowWords + (size_t)NT_BUNDLE * (2 * L + 2) + 4 * NT_BUNDLE) * 4;
+  hipLaunchKernelGGL(nt::nt_bundle_kernel, dim3((uint32_t)grid), dim3(256), lds, stream, *B, tp, L, div_m, div_s);
   return hipGetLastError();
 }
 

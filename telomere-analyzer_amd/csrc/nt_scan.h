@@ -103,6 +103,49 @@ template <int kCtrl, int kRowMask>
 __device__ __forceinline__ uint32_t dpp0(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kCtrl, kRowMask, 0xf, false);
 }
+// 32x32 bit transpose inside each half wave: lane 32 h + s gets bit s of the
+// half's lanes (bit i from lane 32 h + i) -- five butterfly exchanges (lane ^
+// 16 by v_permlane16_swap, ^ 8 / ^ 2 / ^ 1 by DPP, ^ 4 by two DPP shifts),
+// each merged with one rotate and one bit-field select whose per-lane
+// operands (BitTr) are set once.
+struct BitTr {
+  uint32_t rot[5], keep[5];  // stage J = 16 >> i: rotate right by rot, keep the own bits in keep
+  __device__ __forceinline__ explicit BitTr(int lane) {
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      const int J = 16 >> i;
+      const uint32_t M = i == 0 ? 0x0000FFFFu : i == 1 ? 0x00FF00FFu : i == 2 ? 0x0F0F0F0Fu : i == 3 ? 0x33333333u : 0x55555555u;
+      const bool hi = (lane & J) != 0;
+      rot[i] = hi ? (uint32_t)J : (uint32_t)(32 - J);
+      keep[i] = hi ? ~M : M;
+    }
+  }
+};
+__device__ __forceinline__ uint32_t half_bit_transpose(uint32_t a, int lane, const BitTr& bt) {
+  uint32_t pv;
+  {
+    const auto r = __builtin_amdgcn_permlane16_swap(a, a, false, false);
+    pv = (lane & 16) ? r[0] : r[1];
+  }
+  a = (bt.keep[0] & a) | (~bt.keep[0] & __builtin_amdgcn_alignbit(pv, pv, bt.rot[0]));
+  pv = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)a, 0x128, 0xf, 0xf, false);  // row_ror:8 = lane ^ 8
+  a = (bt.keep[1] & a) | (~bt.keep[1] & __builtin_amdgcn_alignbit(pv, pv, bt.rot[1]));
+  {
+    const uint32_t up = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)a, 0x104, 0xf, 0xf, false);  // row_shl:4: lane + 4
+    const uint32_t dn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)a, 0x114, 0xf, 0xf, false);  // row_shr:4: lane - 4
+    pv = (lane & 4) ? dn : up;
+  }
+  a = (bt.keep[2] & a) | (~bt.keep[2] & __builtin_amdgcn_alignbit(pv, pv, bt.rot[2]));
+  pv = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)a, 0x4E, 0xf, 0xf, false);  // quad_perm 2301: lane ^ 2
+  a = (bt.keep[3] & a) | (~bt.keep[3] & __builtin_amdgcn_alignbit(pv, pv, bt.rot[3]));
+  pv = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)a, 0xB1, 0xf, 0xf, false);  // quad_perm 1032: lane ^ 1
+  a = (bt.keep[4] & a) | (~bt.keep[4] & __builtin_amdgcn_alignbit(pv, pv, bt.rot[4]));
+  return a;
+}
+__device__ __forceinline__ uint32_t half_bit_transpose(uint32_t a, int lane) {
+  return half_bit_transpose(a, lane, BitTr(lane));
+}
+
 // inclusive prefix sum over the 64 lanes
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
   v += dpp0<kDppRowShr + 1, 0xf>(v);

@@ -622,26 +622,6 @@ __device__ __forceinline__ uint32_t quad_byte_transpose(uint32_t x, uint32_t sel
   return __builtin_amdgcn_perm(p1, x, sel1);
 }
 
-// 32x32 bit transpose inside each half wave: lane 32 h + s gets bit s of the
-// half's lanes (bit i from lane 32 h + i) -- five butterfly exchanges
-__device__ __forceinline__ uint32_t half_bit_transpose(uint32_t a, int lane) {
-#define NT_BT_STAGE(J, M, XCHG)                                  \
-  {                                                             \
-    const uint32_t pv = (XCHG);                                 \
-    const bool hi = (lane & (J)) != 0;                          \
-    const uint32_t sh = hi ? (pv >> (J)) : (pv << (J));         \
-    const uint32_t mm = hi ? ~(uint32_t)(M) : (uint32_t)(M);    \
-    a = (a & mm) | (sh & ~mm);                                  \
-  }
-  NT_BT_STAGE(16, 0x0000FFFFu, (uint32_t)__builtin_amdgcn_ds_swizzle((int)a, 0x401F))
-  NT_BT_STAGE(8, 0x00FF00FFu, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)a, 0x128, 0xf, 0xf, false))
-  NT_BT_STAGE(4, 0x0F0F0F0Fu, (uint32_t)__builtin_amdgcn_ds_swizzle((int)a, 0x101F))
-  NT_BT_STAGE(2, 0x33333333u, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)a, 0x4E, 0xf, 0xf, false))
-  NT_BT_STAGE(1, 0x55555555u, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)a, 0xB1, 0xf, 0xf, false))
-#undef NT_BT_STAGE
-  return a;
-}
-
 __device__ __forceinline__ uint64_t u64of(uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32) | lo; }
 
 // The bundle scan: every bundle of the batch, one wave per bundle (claimed

@@ -50,6 +50,37 @@ def test_window_count_matches_oracle():
             assert window_count(n, L) == O.window_count(n, L), (n, L)
 
 
+def test_window_rows_padding():
+    # count rows padded to whole 128-byte lines (64 windows), C and numpy agree
+    from nanotel_amd import window_rows
+    nws = np.array([0, 1, 2, 63, 64, 65, 127, 128, 500, 501, 10 ** 6], np.int64)
+    got = window_rows(nws)
+    assert list(got) == [0, 64, 64, 64, 64, 128, 128, 128, 512, 512, 1000000]
+    assert all(window_rows(int(x)) == int(y) for x, y in zip(nws, got))
+
+
+def test_pack_reads_window_offsets_are_padded_rows():
+    import ctypes
+    from nanotel_amd import _lib, window_count, window_rows
+    L = _lib.lib()
+    seqs = [b"A" * 6450, b"C" * 99, b"G" * 150, b"T" * 12800]
+    n = len(seqs)
+    ptrs = (ctypes.c_char_p * n)(*seqs)
+    lens = np.array([len(s) for s in seqs], np.uint64)
+    tb, tw, te, ml, bad = (ctypes.c_uint64() for _ in range(5))
+    assert L.nt_pack_count(ctypes.cast(ptrs, ctypes.c_void_p), lens.ctypes.data, n, 100, ctypes.byref(tb),
+                           ctypes.byref(tw), ctypes.byref(te), ctypes.byref(ml), ctypes.byref(bad)) == 0
+    rows = [window_rows(window_count(len(x), 100)) for x in seqs]
+    assert tw.value == sum(rows)
+    planes = np.zeros(2 * tb.value, np.uint32)
+    blk, wo = np.zeros(n, np.uint64), np.zeros(n, np.uint64)
+    ln = np.zeros(n, np.uint32)
+    assert L.nt_pack_reads(ctypes.cast(ptrs, ctypes.c_void_p), lens.ctypes.data, n, 0, 100, planes.ctypes.data,
+                           blk.ctypes.data, ln.ctypes.data, wo.ctypes.data, None, None, None) == 0
+    assert list(wo) == [0, rows[0], rows[0] + rows[1], rows[0] + rows[1] + rows[2]]
+    assert all(int(w) % 64 == 0 for w in wo)
+
+
 @pytest.mark.parametrize("seed", range(6))
 def test_assign_serials_matches_oracle(seed):
     from nanotel_amd import assign_serials
