@@ -704,8 +704,9 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
   nsub = std::min<uint64_t>(nsub, std::max<uint64_t>(1, batch->n_reads / 256));
   // the bundle scan's sub-batches (bundle ranges): the calling kernel of range
   // k runs on the call stream beside the bundle scan of range k+1 (the scan is
-  // bandwidth-bound, the calling latency-bound); NT_TSUB, default 2 (1M x 50 kb:
-  // 3.62 / 3.54 / 3.55 / 3.66 ms per batch at 1 / 2 / 4 / 8)
+  // bandwidth-bound, the calling latency-bound); NT_TSUB ranges, default 2
+  // (1M x 50 kb, one box, two runs each: 3.43-3.45 ms per batch at 1, 3.30-3.33 at
+  // 2, 3.38-3.41 at 3 geometric ranges, ratio 0.3)
   uint64_t tsub = 1;
   if (tscan) {
     nsub = 1;
@@ -749,20 +750,41 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
     // (one per CU while a calling kernel runs beside it: room for its waves)
     const uint32_t thr_full = ctx->thr_h[std::min<size_t>((size_t)L, ctx->thr_h.size() - 1)];
     const int tbpc = tsub > 1 ? 1 : ctx->tscan_bpc;
+    // range sizes: geometric with NT_TRATIO (default 1 = equal).  Smaller later
+    // ranges leave less calling exposed at the end but measured no better: the
+    // calling beside a range's scan slows that scan (contention), 3.34-3.61 ms
+    // at 3 ranges, ratio 0.25
+    double ratio = 1.0;
+    if (const char* v = std::getenv("NT_TRATIO")) ratio = std::atof(v);
+    if (!(ratio > 0.0 && ratio <= 1.0)) ratio = 1.0;
+    std::vector<uint64_t> bb(tsub + 1, 0);
+    {
+      double tot = 0.0, acc = 0.0, wk = 1.0;
+      for (uint64_t k = 0; k < tsub; ++k, wk *= ratio) tot += wk;
+      wk = 1.0;
+      for (uint64_t k = 0; k < tsub; ++k, wk *= ratio) {
+        acc += wk;
+        bb[k + 1] = k + 1 == tsub ? batch->n_bundles
+                                  : std::min<uint64_t>(batch->n_bundles, (uint64_t)(batch->n_bundles * (acc / tot)));
+        bb[k + 1] = std::max(bb[k + 1], bb[k]);
+      }
+    }
     for (uint64_t k = 0; k < tsub; ++k) {
-      const uint64_t b0 = batch->n_bundles * k / tsub, b1 = batch->n_bundles * (k + 1) / tsub;
+      const uint64_t b0 = bb[k], b1 = bb[k + 1];
+      if (b1 == b0) continue;
       NtBatch Bt = B;  // bundles [b0, b1): bnd_stripe stays absolute
       Bt.bnd_read += NT_BUNDLE * b0;
       Bt.bnd_stripe += b0;
       Bt.n_bundles = b1 - b0;
       const uint64_t tgrid = std::max<uint64_t>(1, std::min<uint64_t>((Bt.n_bundles + 3) / 4, (uint64_t)ctx->cu_count * tbpc));
-      if (ev) (void)hipEventRecord(ev[3 + 2 * k], ctx->stream);
+      const int pe = ev ? ctx->ev_nt[ctx->n_ev - 1] : 0;  // event pair of this launch
+      if (ev) (void)hipEventRecord(ev[3 + 2 * pe], ctx->stream);
       e = nt_tjit_launch(ctx->tjit_fn, (int)tgrid, ctx->stream, &Bt, &O, tmask,
                          queue + (2 * nsub + k) * NT_QUEUE_WORDS, thr_full);
       if (e != hipSuccess) return hip_fail(ctx, e, "launch nt_tscan_jit");
       if (ev) {
-        (void)hipEventRecord(ev[4 + 2 * k], ctx->stream);
-        ctx->ev_nt[ctx->n_ev - 1] = (int)(k + 1);
+        (void)hipEventRecord(ev[4 + 2 * pe], ctx->stream);
+        ctx->ev_nt[ctx->n_ev - 1] = pe + 1;
       }
       // its reads' calling (the bundles' slots; the last window of each recounted)
       NtBatch Bc = B;
