@@ -346,6 +346,24 @@ def test_device_bundle_scan_matches_per_read_scan(read_len):
     compare(nt, res, oracle_rows(seqs, "TTAGGG"), check_windows=False, check_hits=False)
 
 
+@pytest.mark.parametrize("tvr", [None, "TGAGGG TTGGGG"], ids=["p2", "p3"])
+def test_bundle_ranges_with_mixed_lengths_and_exceptions(tvr):
+    # enough bundles for the two bundle-scan ranges (calling beside the scan),
+    # reads of many lengths (bundles sorted by length, ragged ends, reads of one
+    # window) and ~4 % of reads with N / IUPAC letters (left to the per-read scan)
+    rng = np.random.default_rng(20261016)
+    seqs = []
+    for i in range(4500):
+        n = int(rng.choice([int(rng.integers(1, 400)), int(rng.integers(400, 3000)), int(rng.integers(3000, 9000))]))
+        seqs.append(_telo_read(rng, n, where=["left", "right", "mid"][i % 3], tract=(50, 2500),
+                               exc=0.002 if i % 25 == 0 else 0.0))
+    pats = "TTAGGG TCAGGG" if tvr else "TTAGGG"
+    nt = _nt(patterns=pats, tvr_patterns=tvr)
+    assert nt.tscan
+    _check_both(nt, seqs, oracle_rows(seqs, pats, tvr=tvr))
+    nt.close()
+
+
 def test_odd_block_offset_is_reported():
     from nanotel_amd import synth_params
     from nanotel_amd._lib import ROW_DONE, ROW_ERR_ALIGN
