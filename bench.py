@@ -55,22 +55,23 @@ METRICS = {
 }
 
 
-def scan_bytes_per_read(read_len, n_pass, n_windows, n_hits):
+def scan_bytes_per_read(read_len, n_pass, n_windows, n_hits, count_bytes=2):
     """Algorithmic HBM bytes of the SCAN kernel per read:
     reads the 2-bit planes (ceil(n/4) B) + len (4) + blk_off (8) + win_off
-    (8); writes the uint16 window counts per pass, the telomeric-window
+    (8); writes the window counts per pass (count_bytes each: 1 when
+    subseq_length <= 170), the telomeric-window
     bitmask per pass (ceil(nw/64) u64), the running counts at every 16th
     window (u32, for the calling kernel) and the hit counters (u32)."""
     planes = (read_len + 3) // 4
-    return (planes + 4 + 8 + 8 + n_windows * n_pass * 2 + n_pass * 8 * ((n_windows + 63) // 64)
+    return (planes + 4 + 8 + 8 + n_windows * n_pass * count_bytes + n_pass * 8 * ((n_windows + 63) // 64)
             + n_pass * 4 * (n_windows // 16 + 1) + 4 * n_hits)
 
 
-def call_bytes_per_read(n_pass, n_windows):
+def call_bytes_per_read(n_pass, n_windows, count_bytes=2):
     """Algorithmic bytes of the CALLING kernel per read: len/blk_off/win_off,
     the window bitmasks and counts it walks (upper bound: all of them), and
     the row written (start/end int32 x3, density f64 x3, flags u8)."""
-    return (4 + 8 + 8 + n_pass * (8 * ((n_windows + 63) // 64) + 4 * (n_windows // 16 + 1) + 2 * n_windows)
+    return (4 + 8 + 8 + n_pass * (8 * ((n_windows + 63) // 64) + 4 * (n_windows // 16 + 1) + count_bytes * n_windows)
             + 3 * (4 + 4 + 8) + 1)
 
 
@@ -175,7 +176,7 @@ def main():
     lens = torch.empty(n, dtype=torch.int32, device=dev)
     win_off = torch.empty(n, dtype=torch.int64, device=dev)
     rows = window_rows(nw)  # padded count rows (16-byte aligned, nt_common.h)
-    wc = torch.empty(n * rows * npass, dtype=torch.int16, device=dev)
+    wc = torch.empty(n * rows * npass, dtype=torch.uint8 if nt.count_bytes == 1 else torch.int16, device=dev)
     start = torch.empty(n * 3, dtype=torch.int32, device=dev)
     end = torch.empty(n * 3, dtype=torch.int32, device=dev)
     dens = torch.empty(n * 3, dtype=torch.float64, device=dev)
@@ -249,7 +250,7 @@ def main():
     value = total_bases / wall / 1e9
     scan_s = scan_ms / launches / 1e3
     # no hit counters requested: the scan instance without them runs (no hit bytes)
-    scan_bytes = n * scan_bytes_per_read(L, npass, nw, 0) * n_calls // launches
+    scan_bytes = n * scan_bytes_per_read(L, npass, nw, 0, nt.count_bytes) * n_calls // launches
     achieved = scan_bytes / scan_s / 1e9
     traffic = None
     if os.path.exists(args.traffic_json):
@@ -289,7 +290,7 @@ def main():
                          "algorithmic_bytes_per_launch": scan_bytes,
                          "call_kernel": "nt::nt_call_kernel",
                          "call_kernel_avg_ms": round(call_ms / n_calls, 4),
-                         "call_bytes_per_launch": n * call_bytes_per_read(npass, nw),
+                         "call_bytes_per_launch": n * call_bytes_per_read(npass, nw, nt.count_bytes),
                          "step_event_avg_ms": round(sum(step_ms) / len(step_ms), 4)},
         }
         if world == 1 and not args.no_cpu_baseline:

@@ -76,6 +76,7 @@ typedef struct {
   int32_t jit;    /* 1: the scan runs as a kernel specialised for these patterns (hiprtc);
                      0: ahead-of-time kernels (NT_JIT=0 in the environment, or hiprtc failed) */
   int32_t tscan;  /* 1: bundled reads take the bundle scan (nt_tscan.h; NT_TSCAN=0 turns it off) */
+  int32_t count_bytes; /* bytes per window count in win_counts: 1 (subseq_length <= 170) or 2 */
 } nt_program_info;
 
 /* Device-resident read batch (device pointers).  Layout: see DESIGN.md
@@ -105,7 +106,8 @@ typedef struct {
 
 /* Device-resident outputs (device pointers). */
 typedef struct {
-  uint16_t* win_counts; /* [n_windows * n_pass]: pass p of read r at win_off[r]*n_pass + p*rows(r); 128-B aligned base */
+  void* win_counts;     /* [n_windows * n_pass] counts of count_bytes (uint8 / uint16): pass p of read r at
+                           win_off[r]*n_pass + p*rows(r); 128-B aligned base */
   int32_t* start;       /* [n_reads*3] */
   int32_t* end;         /* [n_reads*3] */
   double* density;      /* [n_reads*3] */
@@ -190,7 +192,7 @@ int64_t nt_kernel_launches(const nt_ctx* ctx);
  * win_counts/hits optional.  Returns the first per-read error, if any. */
 int nt_analyze_host(nt_ctx* ctx, const char* const* seqs, const uint64_t* lens, uint64_t n_reads,
                     int32_t* start, int32_t* end, double* density, uint8_t* flags,
-                    uint16_t* win_counts, uint32_t* hits);
+                    void* win_counts, uint32_t* hits);
 
 /* --- --use_filter pre-filter ----------------------------------------------
  * Replaces filter_reads(samples, patterns, do_rc = FALSE, right_edge) +

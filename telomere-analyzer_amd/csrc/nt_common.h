@@ -9,7 +9,9 @@
 //   ambiguity codes, '-', '+', '.') are stored as A in the planes and listed in
 //   a per-read exception list (position, Biostrings DNA code) -- see
 //   DESIGN.md "Exceptions".
-// Window counts: uint16 at win_counts[win_off[r]*n_pass + p*NT_WIN_ROWS(nw(r)) + i]
+// Window counts: uint8 (L <= 170: every window, the widened last one too, is
+//   under 256 bases -- NtProgram::cnt8) or uint16 at
+//   win_counts[win_off[r]*n_pass + p*NT_WIN_ROWS(nw(r)) + i]
 //   (covered bases of window i of pass p; nw = split_telo window count).  A
 //   read's rows are padded to a multiple of 64 windows and win_off[r] is the
 //   prefix sum of the PADDED counts, so every 64-window block of a row is one
@@ -80,6 +82,7 @@ struct NtProgram {
   uint32_t div32_m;       // floor(p / L) = umulhi(p, div32_m) >> div32_s, p < 2^31, L >= 2
   uint32_t div32_s;
   uint32_t thr_size;      // entries of the per-width telomeric threshold table
+  int32_t cnt8;           // window counts are uint8 (L <= 170), else uint16
   NtPat pat[NT_MAX_PAT];
   NtPat tvr[NT_MAX_PAT];
 };
@@ -113,7 +116,7 @@ struct NtBatch {
 };
 
 struct NtOut {
-  uint16_t* win_counts;  // see layout above (may be nullptr)
+  void* win_counts;      // uint8 or uint16 (cnt8), see layout above
   int32_t* start;        // [n_reads*3], 1-based, -1 = NA
   int32_t* end;          // [n_reads*3]
   double* density;       // [n_reads*3]

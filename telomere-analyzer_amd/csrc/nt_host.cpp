@@ -443,6 +443,9 @@ int nt_compile(nt_ctx* ctx, const nt_params* prm, nt_program_info* info) {
     thr[w] = c;  // w + 1 = never telomeric
   }
   P.thr_size = wmax + 1;
+  // 8-bit window counts when every window is under 256 bases: the last window
+  // (merged with a short tail by split_telo) is < 1.5 L wide
+  P.cnt8 = P.L <= 170 ? 1 : 0;
   for (int i = 0; i < P.n_pat + P.n_tvr; ++i) {
     NtPat& X = i < P.n_pat ? P.pat[i] : P.tvr[i - P.n_pat];
     for (int j = 0; j < X.m; ++j)
@@ -486,6 +489,7 @@ int nt_compile(nt_ctx* ctx, const nt_params* prm, nt_program_info* info) {
     info->raw_p1 = P.raw_p1;
     info->jit = ctx->jit ? 1 : 0;
     info->tscan = ctx->tjit_fn ? 1 : 0;
+    info->count_bytes = ctx->prog.cnt8 ? 1 : 2;
   }
   return NT_OK;
 }
@@ -717,7 +721,13 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
   int bpc_cap = 0;
   if (const char* v = std::getenv("NT_SCAN_WAVES")) bpc_cap = std::atoi(v);
   if ((nsub > 1 || tsub > 1) && !ctx->call_stream) {
-    if ((e = hipStreamCreateWithFlags(&ctx->call_stream, hipStreamNonBlocking)) != hipSuccess)
+    int prio = 0;  // NT_CALL_PRIO (tuning): the calling stream's priority, clamped to the device's range
+    if (const char* v = std::getenv("NT_CALL_PRIO")) {
+      int lo = 0, hi = 0;
+      (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+      prio = std::max(std::min(std::atoi(v), std::max(lo, hi)), std::min(lo, hi));
+    }
+    if ((e = hipStreamCreateWithPriority(&ctx->call_stream, hipStreamNonBlocking, prio)) != hipSuccess)
       return hip_fail(ctx, e, "hipStreamCreate(call)");
     if ((e = hipEventCreateWithFlags(&ctx->ev_scan, hipEventDisableTiming)) != hipSuccess ||
         (e = hipEventCreateWithFlags(&ctx->ev_call, hipEventDisableTiming)) != hipSuccess)
@@ -1188,7 +1198,7 @@ int nt_filter_host(nt_ctx* ctx, const char* const* seqs, const uint64_t* lens, u
 
 int nt_analyze_host(nt_ctx* ctx, const char* const* seqs, const uint64_t* lens, uint64_t n_reads,
                     int32_t* start, int32_t* end, double* density, uint8_t* flags,
-                    uint16_t* win_counts, uint32_t* hits) {
+                    void* win_counts, uint32_t* hits) {
   if (!ctx) return NT_E_ARG;
   if (!ctx->compiled) return fail(ctx, NT_E_STATE, "nt_compile() not called");
   if (n_reads == 0) return NT_OK;
@@ -1200,15 +1210,15 @@ int nt_analyze_host(nt_ctx* ctx, const char* const* seqs, const uint64_t* lens, 
   if (rc) return rc;
   const uint64_t tw = B.n_windows;
   hipError_t e;
-  const uint64_t nwc = tw * np;
-  if ((e = ctx->wc.ensure(std::max<uint64_t>(1, nwc) * 2)) != hipSuccess) return hip_fail(ctx, e, "hipMalloc(wc)");
+  const uint64_t nwc = tw * np, cb = ctx->prog.cnt8 ? 1 : 2;  // count entries, bytes per entry
+  if ((e = ctx->wc.ensure(std::max<uint64_t>(1, nwc) * cb)) != hipSuccess) return hip_fail(ctx, e, "hipMalloc(wc)");
   if ((e = ctx->start.ensure(n_reads * 3 * 4)) != hipSuccess) return hip_fail(ctx, e, "hipMalloc(start)");
   if ((e = ctx->end.ensure(n_reads * 3 * 4)) != hipSuccess) return hip_fail(ctx, e, "hipMalloc(end)");
   if ((e = ctx->dens.ensure(n_reads * 3 * 8)) != hipSuccess) return hip_fail(ctx, e, "hipMalloc(dens)");
   if ((e = ctx->flags.ensure(n_reads)) != hipSuccess) return hip_fail(ctx, e, "hipMalloc(flags)");
   const uint64_t nh = (uint64_t)ctx->prog.n_hits * n_reads;
   if ((e = ctx->hits.ensure(std::max<uint64_t>(1, nh) * 4)) != hipSuccess) return hip_fail(ctx, e, "hipMalloc(hits)");
-  nt_out O{(uint16_t*)ctx->wc.p, (int32_t*)ctx->start.p, (int32_t*)ctx->end.p,
+  nt_out O{ctx->wc.p, (int32_t*)ctx->start.p, (int32_t*)ctx->end.p,
            (double*)ctx->dens.p, (uint8_t*)ctx->flags.p, hits ? (uint32_t*)ctx->hits.p : nullptr};
   rc = nt_scan_call(ctx, &B, &O, ml);
   if (rc) return rc;
@@ -1220,7 +1230,7 @@ int nt_analyze_host(nt_ctx* ctx, const char* const* seqs, const uint64_t* lens, 
   NT_DOWN(end, end, n_reads * 3 * 4);
   NT_DOWN(density, dens, n_reads * 3 * 8);
   NT_DOWN(h_flags.data(), flags, n_reads);
-  if (win_counts && nwc) { NT_DOWN(win_counts, wc, nwc * 2); }
+  if (win_counts && nwc) { NT_DOWN(win_counts, wc, nwc * cb); }
   if (hits && nh) { NT_DOWN(hits, hits, nh * 4); }
 #undef NT_DOWN
   e = hipStreamSynchronize(ctx->stream);

@@ -75,7 +75,8 @@ constexpr int kTmRegs = NT_CALL_TM_LDS ? NT_CALL_TM_WORDS : 8;  // bitmask words
 struct Lane {
   ReadCtx rc;
   const NtProgram* prog;
-  const uint16_t* cnt;   // this pass's window counts
+  const void* cnt;       // this pass's window counts: uint8 when c8, else uint16
+  bool c8;
   const uint64_t* tm;    // this pass's telomeric-window bitmask
   const uint32_t* ck;    // this pass's running counts at every 16th window boundary
   int n, nw, nmw, L;
@@ -93,7 +94,9 @@ struct Lane {
 
 __device__ __forceinline__ int wstart(const Lane& c, int i) { return 1 + i * c.L; }
 __device__ __forceinline__ int wend(const Lane& c, int i) { return i == c.nw - 1 ? c.n : wstart(c, i) + c.L - 1; }
-__device__ __forceinline__ int wcount(const Lane& c, int i) { return c.cnt[i]; }
+__device__ __forceinline__ int wcount(const Lane& c, int i) {
+  return c.c8 ? (int)static_cast<const uint8_t*>(c.cnt)[i] : (int)static_cast<const uint16_t*>(c.cnt)[i];
+}
 __device__ __forceinline__ double wdens_of(const Lane& c, int i, int cnt) {
   return (double)cnt / (double)(wend(c, i) - wstart(c, i) + 1);
 }
@@ -348,12 +351,11 @@ __device__ __forceinline__ int cov_count2(const Lane& c, int x1, int y1, int x2,
 // Covered bases of windows [0, k) (0 <= k <= nw): the scan's checkpoint at
 // window 16*(k/16) plus at most 15 window counts (independent loads).
 __device__ __forceinline__ int cnt_before(const Lane& c, int k) {
-  const int r = k & 15;
-  const uint16_t* w = c.cnt + (k - r);
+  const int r = k & 15, k0 = k - r;
   int t = (int)c.ck[k >> 4];
 #pragma unroll
   for (int i = 0; i < 15; ++i)
-    if (i < r) t += w[i];
+    if (i < r) t += wcount(c, k0 + i);
   return t;
 }
 
@@ -674,9 +676,10 @@ __device__ __forceinline__ void call_fix_last(Lane& c, const uint32_t* __restric
   if (c.nw <= 0) return;
   const int last = c.nw - 1, a = last * c.L;
   const int exact = cov_count(c, a, c.n - 1);
-  const int old = c.cnt[last];
+  const int old = wcount(c, last);
   if (exact != old) {
-    const_cast<uint16_t*>(c.cnt)[last] = (uint16_t)exact;
+    if (c.c8) static_cast<uint8_t*>(const_cast<void*>(c.cnt))[last] = (uint8_t)exact;
+    else static_cast<uint16_t*>(const_cast<void*>(c.cnt))[last] = (uint16_t)exact;
     if ((c.nw & 15) == 0) const_cast<uint32_t*>(c.ck)[c.nw >> 4] += (uint32_t)(exact - old);
   }
   const uint32_t w = (uint32_t)(c.n - a);
@@ -827,7 +830,9 @@ nt_call_kernel(const NtProgram* __restrict__ prog, NtBatch B, NtOut O,
         const uint64_t woff = B.win_off[r];
         const uint64_t* tmr = tmask + aux_base(woff, r, np);
         const uint32_t* ckr = reinterpret_cast<const uint32_t*>(tmr + np * aux_nmw(c.nw));
-        c.cnt = O.win_counts + woff * np + (uint64_t)p * NT_WIN_ROWS((uint64_t)c.nw);
+        c.c8 = prog->cnt8 != 0;
+        c.cnt = static_cast<const uint8_t*>(O.win_counts) +
+                (woff * np + (uint64_t)p * NT_WIN_ROWS((uint64_t)c.nw)) * (c.c8 ? 1u : 2u);
         c.tm = tmr + p * c.nmw;
         c.ck = ckr + p * aux_nck(c.nw);
         c.k = p == 0 ? 0 : 1;

@@ -847,7 +847,10 @@ __device__ __forceinline__ void scan_reads(const NtProgram* __restrict__ prog,
     wave_sync();
 
     // ------------------------------------------------ window outputs
-    uint16_t* wout = O.win_counts + m.woff * np;
+    // the pass rows: uint8 or uint16 counts (prog->cnt8, uniform)
+    const bool c8 = prog->cnt8 != 0;
+    uint8_t* wout8 = reinterpret_cast<uint8_t*>(O.win_counts) + m.woff * np;
+    uint16_t* wout = reinterpret_cast<uint16_t*>(O.win_counts) + m.woff * np;
     const int nr = (int)NT_WIN_ROWS(nw);  // the padded row of a pass
     // telomeric window (class -5) iff !(count / width < min_density) iff
     // count >= thr[width] (exact, host-computed); the last window may be wider
@@ -873,7 +876,7 @@ __device__ __forceinline__ void scan_reads(const NtProgram* __restrict__ prog,
         cko[2 * nck + j] = nw == 0 ? 0u : cum2[i];
     }
     // 64 windows per step: counts from the running sums (one ds_read2 per
-    // lane), the u16 count stores and one ballot per pass against the full-width
+    // lane), the count stores and one ballot per pass against the full-width
     // threshold; the last window (wider) is re-tested once after its step.
     for (int ch = 0; ch < nmw; ++ch) {
       const int i = ch * 64 + lane;
@@ -884,12 +887,20 @@ __device__ __forceinline__ void scan_reads(const NtProgram* __restrict__ prog,
         c0 = a1.x - a0.x;
         c1 = a1.y - a0.y;
         if (dbg_ok(dbg, 1, m.woff * np + (uint64_t)(nr + i), r)) {
-          wout[i] = (uint16_t)c0;
-          wout[nr + i] = (uint16_t)c1;
+          if (c8) {
+            wout8[i] = (uint8_t)c0;
+            wout8[nr + i] = (uint8_t)c1;
+          } else {
+            wout[i] = (uint16_t)c0;
+            wout[nr + i] = (uint16_t)c1;
+          }
         }
         if (np == 3) {
           c2 = cum2[i + 1] - cum2[i];
-          if (dbg_ok(dbg, 1, m.woff * np + (uint64_t)(2 * nr + i), r)) wout[2 * nr + i] = (uint16_t)c2;
+          if (dbg_ok(dbg, 1, m.woff * np + (uint64_t)(2 * nr + i), r)) {
+            if (c8) wout8[2 * nr + i] = (uint8_t)c2;
+            else wout[2 * nr + i] = (uint16_t)c2;
+          }
         }
       }
       // (counts are 0 past the read's windows; the mask only matters for a zero threshold)

@@ -395,6 +395,9 @@ struct TPipe {
 #ifndef NT_TS_DBG_NOCNT
 #define NT_TS_DBG_NOCNT 0
 #endif
+#ifndef NT_TS_DBG_HALFCNT  // timing experiments only: half of the count stores
+#define NT_TS_DBG_HALFCNT 0
+#endif
 #ifndef NT_TS_LOAD_AUX  // cache policy bits of the T-layout loads (experiments)
 #define NT_TS_LOAD_AUX 0
 #endif
@@ -596,22 +599,23 @@ struct TSlot {
 };
 constexpr int kTsSlotWords = 12;
 
-// per-wave LDS of the bundle scan (uint32 words): the slots; the count
-// transpose of the output stage (row s = slot s, 16 words = the 64 windows of
-// the stripe, 4 to a word: byte b = window 4 q + b of word q); and the
-// telomeric bitmask words / checkpoints of kTsF stripes, written out together
-// (whole runs of a read's row instead of 4-byte pieces: a partly written line
-// costs a read-modify-write in the memory system)
-constexpr int kTsCtWords = NT_BUNDLE * 16;
+// per-wave LDS of the bundle scan (uint32 words): the slots; the count rows
+// of two stripes per pass (row s = slot s, 32 words = 128 windows, 4 to a
+// word: byte b = window 4 q + b of word q -- the uint8 counts, stored as
+// whole 128-byte lines every second stripe); and the telomeric bitmask words
+// / checkpoints of kF stripes, written out together (whole runs of a read's
+// row instead of 4-byte pieces: a partly written line costs a
+// read-modify-write in the memory system).  Under 20 KB: 2 waves / SIMD.
 template <int kNP>
 struct TsAux {
-  static constexpr int kF = kNP == 3 ? 4 : 8;                 // stripes per flush
+  static constexpr int kF = kNP == 3 ? 2 : 4;                 // stripes per flush (even)
+  static constexpr int kCtWords = kNP * NT_BUNDLE * 32;       // [p][s][2 stripes x 16 words]
   static constexpr int kTmWords = kNP * NT_BUNDLE * kF * 2;   // [p][s][stripe] u64
   static constexpr int kCkWords = kNP * NT_BUNDLE * 4 * kF;   // [p][s][4 stripe + g] u32
+  static constexpr int kWords = kCtWords + kTmWords + kCkWords;
 };
-constexpr int kTsLdsWords = NT_BUNDLE * kTsSlotWords + kTsCtWords + 3072;  // >= TsAux<2, 3> words
-static_assert(TsAux<2>::kTmWords + TsAux<2>::kCkWords <= 3072, "LDS");
-static_assert(TsAux<3>::kTmWords + TsAux<3>::kCkWords <= 3072, "LDS");
+constexpr int kTsLdsWords = NT_BUNDLE * kTsSlotWords + 4224;
+static_assert(TsAux<2>::kWords <= 4224 && TsAux<3>::kWords <= 4224, "LDS");
 
 // 4x4 byte transpose inside every quad of lanes: lane i of the quad gets byte
 // i of the quad's four words (byte i' from lane i') -- two DPP exchanges
@@ -631,11 +635,12 @@ __device__ __forceinline__ void tscan_bundles(const NtBatch& B, const NtOut& O, 
                                               unsigned long long* __restrict__ queue,
                                               uint32_t thr_full, uint32_t* wlds) {
   constexpr int kL = TP::kL, kNP = TP::kNP, kT = TP::kT;
+  static_assert(kL <= 170, "8-bit counts (nt_tscan_eligible)");
   const int lane = threadIdx.x & (kWave - 1);
   TSlot* sl = reinterpret_cast<TSlot*>(wlds);
-  uint32_t* ct = wlds + NT_BUNDLE * kTsSlotWords;  // the count transpose
+  uint32_t* ct = wlds + NT_BUNDLE * kTsSlotWords;  // the count rows
   using Aux = TsAux<kNP>;
-  uint32_t* tmb = ct + kTsCtWords;     // bitmask words of the flush
+  uint32_t* tmb = ct + Aux::kCtWords;  // bitmask words of the flush
   uint32_t* ckb = tmb + Aux::kTmWords;  // checkpoints of the flush
   // quad_byte_transpose selectors (v_perm: bytes 0-3 from x, 4-7 from the partner)
   const uint32_t sel2 = (lane & 2) ? 0x03020706u : 0x05040100u;
@@ -729,6 +734,8 @@ __device__ __forceinline__ void tscan_bundles(const NtBatch& B, const NtOut& O, 
       const int fs = st % Aux::kF;          // the stripe's place in the flush buffers
 #pragma unroll
       for (int p = 0; p < kNP; ++p) {
+        uint32_t* ctp = ct + p * NT_BUNDLE * 32;  // this pass's rows
+        const int half = (st & 1) * 16;            // this stripe's 16 words of a row
         uint32_t W[8];
 #pragma unroll
         for (int t = 0; t < 8; ++t) W[t] = acc[p][t];
@@ -745,34 +752,35 @@ __device__ __forceinline__ void tscan_bundles(const NtBatch& B, const NtOut& O, 
 #pragma unroll
         for (int j = 0; j < 8; ++j) W[j] = quad_byte_transpose(W[j], sel2, sel1);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) ct[(8 * (lane & 3) + j) * 16 + (lane >> 2)] = W[j];
+        for (int j = 0; j < 8; ++j) ctp[(8 * (lane & 3) + j) * 32 + half + (lane >> 2)] = W[j];
         const uint32_t tb = half_bit_transpose(ge, lane) & (nv >= 32 ? ~0u : ((1u << nv) - 1u));
         tmb[((p * NT_BUNDLE + ms) * Aux::kF + fs) * 2 + mh] = tb;
         wave_sync();
-        // window counts: store c covers slots 8 c .. 8 c + 7, lane 8 i + q = 16
-        // bytes (windows 8 q ..) of slot 8 c + i: one line per slot
+        // window counts (uint8: L <= 170), every second stripe: the rows' 128
+        // windows as whole lines, store c covers slots 8 c .. 8 c + 7, lane 8 i +
+        // q = the 16 bytes (windows 16 q ..) of slot 8 c + i
+        if ((st & 1) || st == nst - 1) {
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const int s = 8 * c + (lane >> 3), q = lane & 7, kq = st * kWave + 8 * q;
-          const uint4 m = *reinterpret_cast<const uint4*>(sl + s);  // nw, wb_lo, wb_hi
-          const uint2 x = *reinterpret_cast<const uint2*>(ct + s * 16 + 2 * q);
-          if (kq < (int)m.x && !NT_TS_DBG_NOCNT) {
-            uint16_t* w = O.win_counts + u64of(m.y, m.z) + (uint64_t)p * NT_WIN_ROWS((uint64_t)m.x) + kq;
-            const uint4 v =
-                make_uint4(__builtin_amdgcn_perm(0u, x.x, 0x0C010C00u), __builtin_amdgcn_perm(0u, x.x, 0x0C030C02u),
-                           __builtin_amdgcn_perm(0u, x.y, 0x0C010C00u), __builtin_amdgcn_perm(0u, x.y, 0x0C030C02u));
+          for (int c = 0; c < (NT_TS_DBG_HALFCNT ? 2 : 4); ++c) {  // (HALFCNT: timing only)
+            const int s = 8 * c + (lane >> 3), q = lane & 7, kq = (st >> 1) * 2 * kWave + 16 * q;
+            const uint4 m = *reinterpret_cast<const uint4*>(sl + s);  // nw, wb_lo, wb_hi
+            const uint4 x = *reinterpret_cast<const uint4*>(ctp + s * 32 + 4 * q);
+            if (kq < (int)m.x && !NT_TS_DBG_NOCNT) {
+              uint8_t* w = reinterpret_cast<uint8_t*>(O.win_counts) + u64of(m.y, m.z) +
+                           (uint64_t)p * NT_WIN_ROWS((uint64_t)m.x) + kq;
 #if NT_TS_NTSTORE
-            typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-            const u32x4 vv = {v.x, v.y, v.z, v.w};
-            __builtin_nontemporal_store(vv, reinterpret_cast<u32x4*>(w));
+              typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+              const u32x4 vv = {x.x, x.y, x.z, x.w};
+              __builtin_nontemporal_store(vv, reinterpret_cast<u32x4*>(w));
 #else
-            *reinterpret_cast<uint4*>(w) = v;
+              *reinterpret_cast<uint4*>(w) = x;
 #endif
+            }
           }
         }
         // checkpoints: covered bases before windows 16 jj, jj = 4 st + g
-        const uint4 va = *reinterpret_cast<const uint4*>(ct + ms * 16 + 8 * mh);
-        const uint4 vb = *reinterpret_cast<const uint4*>(ct + ms * 16 + 8 * mh + 4);
+        const uint4 va = *reinterpret_cast<const uint4*>(ctp + ms * 32 + half + 8 * mh);
+        const uint4 vb = *reinterpret_cast<const uint4*>(ctp + ms * 32 + half + 8 * mh + 4);
         uint32_t ga = 0u, gb = 0u;
         ga = __builtin_amdgcn_udot4(va.x, 0x01010101u, ga, false);
         ga = __builtin_amdgcn_udot4(va.y, 0x01010101u, ga, false);

@@ -47,7 +47,7 @@ class NtParams(ctypes.Structure):
 class NtProgramInfo(ctypes.Structure):
     _fields_ = [("n_pass", ctypes.c_int32), ("n_pat", ctypes.c_int32), ("n_tvr", ctypes.c_int32),
                 ("n_hits", ctypes.c_int32), ("raw_p1", ctypes.c_int32), ("jit", ctypes.c_int32),
-                ("tscan", ctypes.c_int32)]
+                ("tscan", ctypes.c_int32), ("count_bytes", ctypes.c_int32)]
 
 
 class NtBatch(ctypes.Structure):

@@ -67,6 +67,8 @@ class NanoTel:
         self.jit = bool(info.jit)
         # bundled reads take the bundle scan (the reads transposed 32 to a bundle)
         self.tscan = bool(info.tscan)
+        self.count_bytes = int(info.count_bytes)  # window counts: uint8 (subseq_length <= 170) or uint16
+        self.count_dtype = np.uint8 if self.count_bytes == 1 else np.uint16
         self.subseq_length = int(subseq_length)
 
     # ------------------------------------------------------------------
@@ -118,7 +120,7 @@ class NanoTel:
 
         Returns a dict of numpy arrays: start/end (n,3) int32 (1-based, -1 =
         no telomere), density (n,3) float64, flags (n,) uint8, width (n,3),
-        telomeric (n,) bool [, win_counts (flat uint16), win_off (n,) ]
+        telomeric (n,) bool [, win_counts (flat, count_dtype), win_off (n,) ]
         [, hits (n, n_hits) uint32].
         """
         bseqs = [s.encode() if isinstance(s, str) else bytes(s) for s in seqs]
@@ -149,7 +151,7 @@ class NanoTel:
             rows = window_rows(nw)  # padded rows (nt_common.h): 16-byte aligned
             win_off = np.zeros(n, np.int64)
             win_off[1:] = np.cumsum(rows)[:-1]
-            wc = np.zeros(max(1, int(rows.sum()) * self.n_pass), np.uint16)
+            wc = np.zeros(max(1, int(rows.sum()) * self.n_pass), self.count_dtype)
             out["win_off"] = win_off
             out["n_windows"] = nw
         hits = np.zeros((n, max(1, self.n_hits)), np.uint32) if want_hits else None

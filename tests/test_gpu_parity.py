@@ -245,7 +245,8 @@ def _device_batch(nt, sp, n, read_len, L=100):
         blk_off=torch.empty(n, dtype=torch.int64, device="cuda"),
         lens=torch.empty(n, dtype=torch.int32, device="cuda"),
         win_off=torch.empty(n, dtype=torch.int64, device="cuda"),
-        wc=torch.zeros(n * rows * nt.n_pass, dtype=torch.int16, device="cuda"),
+        wc=torch.zeros(n * rows * nt.n_pass, dtype=torch.uint8 if nt.count_bytes == 1 else torch.int16,
+                       device="cuda"),
         start=torch.empty(n * 3, dtype=torch.int32, device="cuda"),
         end=torch.empty(n * 3, dtype=torch.int32, device="cuda"),
         dens=torch.empty(n * 3, dtype=torch.float64, device="cuda"),
@@ -290,7 +291,7 @@ def test_device_resident_path_matches_host_path(jit):
     assert np.array_equal(t["dens"].cpu().numpy().reshape(n, 3).view(np.uint64),
                           res["density"].view(np.uint64))
     assert np.array_equal(t["flags"].cpu().numpy(), res["flags"])
-    assert np.array_equal(_valid_counts(t, n, nt.n_pass).cpu().numpy().view(np.uint16),
+    assert np.array_equal(_valid_counts(t, n, nt.n_pass).cpu().numpy().view(nt.count_dtype),
                           res["win_counts"].reshape(n, nt.n_pass, -1)[:, :, :t["nw"]])
     assert np.array_equal(t["hits"].cpu().numpy().view(np.uint32).reshape(n, -1), res["hits"])
     compare(nt, res, oracle_rows(seqs[:6], "TTAGGG"))
@@ -397,7 +398,7 @@ def test_offsets_beyond_32_bits(jit):
     blk, win = t["blk_off"] + boff, t["win_off"] + woff
     nt.scan_call_device(t["planes"].data_ptr() - boff * 8, blk.data_ptr(), t["lens"].data_ptr(), win.data_ptr(),
                         n, woff + n * t["rows"], read_len, t["start"].data_ptr(), t["end"].data_ptr(),
-                        t["dens"].data_ptr(), t["flags"].data_ptr(), t["wc"].data_ptr() - woff * nt.n_pass * 2)
+                        t["dens"].data_ptr(), t["flags"].data_ptr(), t["wc"].data_ptr() - woff * nt.n_pass * nt.count_bytes)
     nt.synchronize()
     for k in keys:
         assert torch.equal(t[k], ref[k]), k
