@@ -605,17 +605,19 @@ constexpr int kTsSlotWords = 12;
 // whole 128-byte lines every second stripe); and the telomeric bitmask words
 // / checkpoints of kF stripes, written out together (whole runs of a read's
 // row instead of 4-byte pieces: a partly written line costs a
-// read-modify-write in the memory system).  Under 20 KB: 2 waves / SIMD.
+// read-modify-write in the memory system).  22.5 KB at most: one workgroup
+// per CU (the scan runs at one wave per SIMD) leaves room for two of the
+// calling kernel's beside it.
 template <int kNP>
 struct TsAux {
-  static constexpr int kF = kNP == 3 ? 2 : 4;                 // stripes per flush (even)
+  static constexpr int kF = kNP == 3 ? 4 : 8;                 // stripes per flush (even)
   static constexpr int kCtWords = kNP * NT_BUNDLE * 32;       // [p][s][2 stripes x 16 words]
   static constexpr int kTmWords = kNP * NT_BUNDLE * kF * 2;   // [p][s][stripe] u64
   static constexpr int kCkWords = kNP * NT_BUNDLE * 4 * kF;   // [p][s][4 stripe + g] u32
   static constexpr int kWords = kCtWords + kTmWords + kCkWords;
 };
-constexpr int kTsLdsWords = NT_BUNDLE * kTsSlotWords + 4224;
-static_assert(TsAux<2>::kWords <= 4224 && TsAux<3>::kWords <= 4224, "LDS");
+constexpr int kTsLdsWords = NT_BUNDLE * kTsSlotWords + 5376;
+static_assert(TsAux<2>::kWords <= 5376 && TsAux<3>::kWords <= 5376, "LDS");
 
 // 4x4 byte transpose inside every quad of lanes: lane i of the quad gets byte
 // i of the quad's four words (byte i' from lane i') -- two DPP exchanges
