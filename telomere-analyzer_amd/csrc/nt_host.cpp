@@ -845,7 +845,7 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
     Ok.density += 3 * r0;
     Ok.flags += r0;
     if (Ok.hits) Ok.hits += (uint64_t)nh * r0;
-    uint64_t* tmk = tmask + 2 * r0 * (uint64_t)np;  // aux_base(win_off, r, np) of the global read index
+    uint64_t* tmk = tmask + 16 * r0 * (uint64_t)np;  // aux_base(win_off, r, np) of the global read index
     unsigned long long* q = queue + 2 * NT_QUEUE_WORDS * k;
     const uint64_t ns = tscan ? n_scan : nr;  // queue positions of the per-read scan
     const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((ns + 3) / 4, (uint64_t)ctx->cu_count * bpc));

@@ -1120,7 +1120,7 @@ uint32_t nt_dev_wave_words(int single, int n_hits, int np, uint32_t nw_cap) {
 
 // uint64 words of the telomeric-bitmask scratch for a batch
 uint64_t nt_dev_tmask_words(uint64_t total_windows, uint64_t n_reads, int np) {
-  return ((total_windows >> 4) + 2 * n_reads + 2) * (uint64_t)np;  // aux_base blocks
+  return ((total_windows >> 6) + 2 * n_reads + 2) * 8 * (uint64_t)np;  // aux_base blocks
 }
 
 // (single, lds, one-hot, compile-time m): m = 6 covers TTAGGG-style motifs

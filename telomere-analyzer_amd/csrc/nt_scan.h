@@ -56,10 +56,13 @@ __device__ __forceinline__ void wave_sync() {
 // units from aux_base(): the telomeric-window bitmasks (pass p at p * nmw,
 // nmw = ceil(nw / 64)), then the running covered-base counts at every 16th
 // window boundary as uint32 (pass p at p * nck, nck = nw / 16 + 1):
-// cnt16[p][j] = covered bases before window 16 j.  Block size <=
-// np * (nw / 16 + 2) words, and (win_off >> 4) + 2 r never reaches read r+1's.
+// cnt16[p][j] = covered bases before window 16 j.  With R = the read's rows /
+// 64 (win_off is a prefix sum of rows, multiples of 64) the block needs <=
+// np (3 R + 1) words and gets 8 np (R + 2): the blocks start 128-byte aligned
+// for np = 2 (64 with 3 passes), so the bundle scan's flush of a read's block
+// writes whole lines, not pieces of lines its neighbours write.
 __device__ __forceinline__ uint64_t aux_base(uint64_t win_off, uint64_t r, int np) {
-  return ((win_off >> 4) + 2 * r) * (uint64_t)np;
+  return ((win_off >> 6) + 2 * r) * 8 * (uint64_t)np;
 }
 __device__ __forceinline__ int aux_nmw(int nw) { return (nw + 63) >> 6; }
 __device__ __forceinline__ int aux_nck(int nw) { return (nw >> 4) + 1; }
