@@ -407,6 +407,9 @@ struct TPipe {
 #ifndef NT_TS_XPRIME
 #define NT_TS_XPRIME 0
 #endif
+#ifndef NT_TS_HALO  // 1: block halos from the neighbour lanes (TWalkerH), 0: loaded (TWalker)
+#define NT_TS_HALO 0
+#endif
 
 // The walk of one stripe's block per lane, as a continuous stream of 16-byte
 // slots with a register ring of 8 slots (loads issued 8 slots ahead, the
@@ -562,6 +565,125 @@ struct TWalker {
   }
 };
 
+// The walk without halo loads (NT_TS_HALO): a block's head slots (positions
+// [0, kLam)) and tail slots ([kL - kLam, kL)) are loaded once into registers
+// at the stripe start; the prologue takes the left neighbour's tail and the
+// epilogue the right neighbour's head from the next / previous lane by DPP
+// (wave_shr:1 / wave_shl:1), lane 0 and lane 63 from the previous / next
+// stripe's edge block (one uniform load each, the DPP's bound value).  The
+// ring streams the own slots in between: block slots kNH .. in order.  The
+// block halos are ~8 % of the T-layout reads (FETCH 13.8 vs 12.8 GB at 1 M x
+// 50 kb), but this walk measured slower (1 M x 50 kb step 3.10 -> 3.16 ms, same
+// box): the halo re-reads hit the caches, the edge loads and DPP do not pay.
+// Off (kept for the record and further tries).
+template <class TP, class Pats, class Tvrs>
+struct TWalkerH {
+  static constexpr int kL = TP::kL, kLam = TP::kLam, kT = TP::kT;
+  static constexpr int U = 16, D = 8;
+  static constexpr int C = (kL - kLam) / U;           // loop runs: P in [kLam + U c, + U), all < kL
+  static constexpr int P1 = kLam + U * C, P2 = kL + kLam;  // epilogue positions [P1, P2)
+  static constexpr int NP0 = 2 * kLam, NE = P2 - P1;
+  static constexpr int kNH = kLam / 2;                // head slots 0 .. kNH - 1
+  static constexpr int kT0 = (kL - kLam) / 2;         // tail slots kT0 .. kT - 1
+  static constexpr int kNT = kT - kT0;
+  static constexpr int NS0 = cmax(8 * C, kT0 - kNH);  // ring stream: block slots kNH + f, f < NS0
+
+  __amdgpu_buffer_rsrc_t rs;
+  int vb;          // byte offset of this lane's block in the stripe (< 0: zeros)
+  int vl, vr;      // uniform: the previous stripe's last block, the next stripe's first block
+  uint4 S[D];      // the ring: stream slot f sits in S[f % D]
+  uint4 Hs[kNH > 0 ? kNH : 1], Ts[kNT];  // own head / tail slots
+  uint4 XL[kNT], XR[kNH > 0 ? kNH : 1];  // lane 0's left / lane 63's right neighbour slots
+  TPipe<TP, Pats, Tvrs> pp;
+
+  __device__ __forceinline__ uint4 ld(int voff, int soff) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, NT_TS_LOAD_AUX);
+#if NT_TS_PIN
+    __builtin_amdgcn_sched_barrier(0);  // keep the load where it is issued
+#endif
+    return make_uint4(v[0], v[1], v[2], v[3]);
+  }
+  __device__ __forceinline__ void set_stripe(int st, int lane, bool active, int nst) {
+    vb = active ? (st * kT * kWave + lane) * 16 : -1;
+    vl = st > 0 ? ((st - 1) * kT * kWave + (kWave - 1)) * 16 : -1;
+    vr = st + 1 < nst ? (st + 1) * kT * kWave * 16 : -1;
+  }
+  // the stripe's first loads: edges, neighbours' edges, the ring's first D
+  __device__ __forceinline__ void prime() {
+#pragma unroll
+    for (int j = 0; j < kNT; ++j) Ts[j] = ld(vb, (kT0 + j) * 1024);
+#pragma unroll
+    for (int j = 0; j < kNH; ++j) Hs[j] = ld(vb, j * 1024);
+#pragma unroll
+    for (int j = 0; j < kNT; ++j) XL[j] = ld(vl, (kT0 + j) * 1024);
+#pragma unroll
+    for (int j = 0; j < kNH; ++j) XR[j] = ld(vr, j * 1024);
+#pragma unroll
+    for (int f = 0; f < D; ++f) S[f] = f < NS0 ? ld(vb, (kNH + f) * 1024) : make_uint4(0u, 0u, 0u, 0u);
+  }
+  // the neighbour's slot: DPP by one lane, the edge lane's from the uniform load
+  template <int kCtrl>
+  __device__ __forceinline__ static uint4 nb(const uint4& own, const uint4& edge) {
+    return make_uint4((uint32_t)__builtin_amdgcn_update_dpp((int)edge.x, (int)own.x, kCtrl, 0xf, 0xf, false),
+                      (uint32_t)__builtin_amdgcn_update_dpp((int)edge.y, (int)own.y, kCtrl, 0xf, 0xf, false),
+                      (uint32_t)__builtin_amdgcn_update_dpp((int)edge.z, (int)own.z, kCtrl, 0xf, 0xf, false),
+                      (uint32_t)__builtin_amdgcn_update_dpp((int)edge.w, (int)own.w, kCtrl, 0xf, 0xf, false));
+  }
+
+  __device__ __forceinline__ void walk(bool first, uint32_t (&acc)[3][8]) {
+    pp.init();
+    {  // prologue: the left neighbour's tail (wave_shr:1), then the own head
+      auto get = [&](auto ii) {
+        constexpr int i = decltype(ii)::value, P = -kLam + i;
+        uint4 v;
+        if constexpr (P < 0) v = nb<0x138>(Ts[(kL + P) / 2 - kT0], XL[(kL + P) / 2 - kT0]);
+        else v = Hs[P / 2];
+        constexpr bool odd = ((P < 0 ? kL + P : P) & 1) != 0;
+        const uint32_t vm = (P < 0 && first) ? 0u : 0xFFFFFFFFu;
+        return odd ? make_uint3(v.z, v.w, vm) : make_uint3(v.x, v.y, vm);
+      };
+      pp.template run<NP0, false, true>(get, [&](auto) {});
+    }
+#pragma nounroll
+    for (int c = 0; c < C; ++c) {  // loop runs: stream slots 8 c + i
+      auto get = [&](auto ui) {
+        constexpr int u = decltype(ui)::value;
+        const uint4 v = S[(u >> 1) % D];
+        return (u & 1) ? make_uint3(v.z, v.w, 0u) : make_uint3(v.x, v.y, 0u);
+      };
+      pp.template run<U, true, false>(get, [&](auto ui) {
+        constexpr int u = decltype(ui)::value;
+        if constexpr (u & 1) {  // stream slot 8 c + i consumed: refill with 8 (c + 1) + i
+          constexpr int i = u >> 1;
+          const int f = 8 * (c + 1) + i;
+          S[i] = ld(f < NS0 ? vb : -1, (kNH + f) * 1024);
+        }
+      });
+    }
+    {  // epilogue: the own slots (ring, then the tail), then the right neighbour's head (wave_shl:1)
+      auto get = [&](auto ii) {
+        constexpr int i = decltype(ii)::value, P = P1 + i;
+        uint4 v;
+        if constexpr (P >= kL) v = nb<0x130>(Hs[(P - kL) / 2], XR[(P - kL) / 2]);
+        else if constexpr (P / 2 >= kT0) v = Ts[P / 2 - kT0];
+        else v = S[(P / 2 - kNH) % D];
+        constexpr bool odd = ((P >= kL ? P - kL : P) & 1) != 0;
+        return odd ? make_uint3(v.z, v.w, 0u) : make_uint3(v.x, v.y, 0u);
+      };
+      pp.template run<NE, true, false>(get, [&](auto ui) {
+        constexpr int i = decltype(ui)::value, P = P1 + i;
+        // a ring slot consumed in the epilogue: refill when the stream goes on
+        if constexpr (P < kL && P / 2 < kT0 && (P & 1) && P / 2 - kNH + D < NS0)
+          S[(P / 2 - kNH) % D] = ld(vb, (P / 2 + D) * 1024);
+      });
+    }
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+#pragma unroll
+      for (int b = 0; b < 8; ++b) acc[p][b] = pp.bc[p].acc[b];
+  }
+};
+
 // 8x8 bit transpose inside every byte of 8 words: afterwards byte g of word j
 // holds bit b (of word b before) = bit b of the count of slot 8 g + j.
 __device__ __forceinline__ void transpose8(uint32_t (&a)[8]) {
@@ -695,13 +817,19 @@ __device__ __forceinline__ void tscan_bundles(const NtBatch& B, const NtOut& O, 
         const_cast<uint32_t*>(B.tplanes) + g0 * (uint64_t)kT * kWave * 4, (short)0,
         (int)((g1 - g0) * (uint64_t)kT * kWave * 16), 0x00020000);
     wave_sync();
+#if NT_TS_HALO
+    TWalkerH<TP, Pats, Tvrs> wk;
+    wk.rs = rs;
+    wk.set_stripe(0, lane, lane < nblk, nst);
+#else
     TWalker<TP, Pats, Tvrs> wk;
     wk.rs = rs;
     wk.set_stripe(0, lane, lane < nblk);
     if (NT_TS_XPRIME) wk.prime();
+#endif
     for (int st = 0; st < nst; ++st) {
       const int k = st * kWave + lane;  // this lane's block = window
-      if (!NT_TS_XPRIME) wk.prime();
+      if (!NT_TS_XPRIME || NT_TS_HALO) wk.prime();
       uint32_t acc[3][8];
 #if NT_TS_DBG_NOWALK  // timing experiments only: results are wrong
 #pragma unroll
@@ -711,7 +839,11 @@ __device__ __forceinline__ void tscan_bundles(const NtBatch& B, const NtOut& O, 
 #else
       wk.walk(k == 0, acc);
 #endif
+#if NT_TS_HALO
+      wk.set_stripe(st + 1, lane, k + kWave < nblk, nst);  // lanes past the bundle's last block load nothing
+#else
       wk.set_stripe(st + 1, lane, k + kWave < nblk);  // lanes past the bundle's last block load nothing
+#endif
 #if NT_TS_DBG_NOOUT  // timing experiments only: results are wrong
       {
         uint32_t x = 0;
