@@ -20,7 +20,7 @@ nt_tscan_jit(NtBatch B, NtOut O, uint64_t* __restrict__ tmask,
 EOT
 cd "$out"
 /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off ${ISA_DEFS:-} -I"$here/telomere-analyzer_amd/csrc" \
-  -c --save-temps -Rpass-analysis=kernel-resource-usage t.hip -o t.o 2>&1 | grep -E "error|VGPRs:|SGPRs:|Spill|Occupancy|ScratchSize" | sed 's/.*remark: //'
+  -c --save-temps -Rpass-analysis=kernel-resource-usage t.hip -o t.o 2>&1 | grep -E "error|VGPRs:|AGPRs:|SGPRs:|Spill|Occupancy|ScratchSize" | sed 's/.*remark: //'
 python3 - <<'EOT'
 import collections
 s=open('t-hip-amdgcn-amd-amdhsa-gfx950.s').read()
