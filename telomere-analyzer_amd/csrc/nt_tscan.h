@@ -407,6 +407,9 @@ struct TPipe {
 #ifndef NT_TS_XPRIME
 #define NT_TS_XPRIME 0
 #endif
+#ifndef NT_TS_RING  // slots in the walk's prefetch ring (8: one 16-position run ahead; 16: 32)
+#define NT_TS_RING 8
+#endif
 #ifndef NT_TS_HALO  // 1: block halos from the neighbour lanes (TWalkerH), 0: loaded (TWalker)
 #define NT_TS_HALO 0
 #endif
@@ -424,7 +427,7 @@ struct TPipe {
 template <class TP, class Pats, class Tvrs>
 struct TWalker {
   static constexpr int kL = TP::kL, kLam = TP::kLam, kT = TP::kT;
-  static constexpr int U = 16, D = 8;
+  static constexpr int D = NT_TS_RING, U = 2 * D;  // ring slots; positions per loop run
   static constexpr int PA = -kLam, PB = kLam;         // prologue positions [PA, PB)
   static constexpr int C = (kL - kLam) / U;           // loop runs: P in [kLam + U c, + U), all < kL
   static constexpr int P1 = kLam + U * C, P2 = kL + kLam;  // epilogue positions [P1, P2)
@@ -440,7 +443,7 @@ struct TWalker {
   }
   static constexpr int NA = sidx(PA, PB - 1) + 1;      // prologue slots
   static constexpr int NEs = sidx(P1, P2 - 1) + 1;     // epilogue slots
-  static constexpr int NS0 = NA + 8 * C + NEs;
+  static constexpr int NS0 = NA + D * C + NEs;
   static constexpr int NS = (NS0 + D - 1) / D * D;    // stream slots per stripe (padded)
   // first position of segment slot j of the segment starting at a
   static constexpr int spos(int a, int b, int j) {
@@ -450,10 +453,10 @@ struct TWalker {
   }
   // static stream slot f (not a loop slot): kind 0 = slot (rel, t), 1 = pad (no load)
   static constexpr int srel(int f) {
-    return f < NA ? rel(spos(PA, PB, f)) : (f >= NA + 8 * C && f < NS0 ? rel(spos(P1, P2, f - NA - 8 * C)) : 2);
+    return f < NA ? rel(spos(PA, PB, f)) : (f >= NA + D * C && f < NS0 ? rel(spos(P1, P2, f - NA - D * C)) : 2);
   }
   static constexpr int st_(int f) {
-    return f < NA ? off(spos(PA, PB, f)) / 2 : (f >= NA + 8 * C && f < NS0 ? off(spos(P1, P2, f - NA - 8 * C)) / 2 : 0);
+    return f < NA ? off(spos(PA, PB, f)) / 2 : (f >= NA + D * C && f < NS0 ? off(spos(P1, P2, f - NA - D * C)) / 2 : 0);
   }
 
   __amdgpu_buffer_rsrc_t rs;
@@ -474,7 +477,7 @@ struct TWalker {
   __device__ __forceinline__ void load_static() {
     constexpr bool nxt = F >= NS;
     constexpr int f = nxt ? F - NS : F;
-    if constexpr (f >= NA && f < NA + 8 * C) {  // a loop slot (only run 0's, from the prime)
+    if constexpr (f >= NA && f < NA + D * C) {  // a loop slot (only run 0's, from the prime)
       constexpr int so = (kLam / 2 + (f - NA)) * 1024;
       S[F % D] = ld(nxt ? vbn[1] : vb[1], so);
     } else if constexpr (srel(f) == 2) {
@@ -515,7 +518,7 @@ struct TWalker {
       });
     }
 #pragma nounroll
-    for (int c = 0; c < C; ++c) {  // loop runs: stream slots NA + 8c + i
+    for (int c = 0; c < C; ++c) {  // loop runs: stream slots NA + D c + i
       auto get = [&](auto ui) {
         constexpr int u = decltype(ui)::value;
         const uint4 v = S[(NA + (u >> 1)) % D];
@@ -524,11 +527,11 @@ struct TWalker {
       const bool last = c == C - 1;
       pp.template run<U, true, false>(get, [&](auto ui) {
         constexpr int u = decltype(ui)::value;
-        if constexpr (u & 1) {  // slot i = u / 2 consumed: refill with stream slot NA + 8 (c + 1) + i
-          constexpr int i = u >> 1, fe = NA + 8 * C + i;  // the target when c is the last run
+        if constexpr (u & 1) {  // slot i = u / 2 consumed: refill with stream slot NA + D (c + 1) + i
+          constexpr int i = u >> 1, fe = NA + D * C + i;  // the target when c is the last run
           constexpr int re = fe < NS0 ? srel(fe) : 2;
           constexpr int soe = fe < NS0 ? st_(fe) * 1024 : 0;
-          const int vo_loop = vb[1], so_loop = (kLam / 2 + 8 * (c + 1) + i) * 1024;
+          const int vo_loop = vb[1], so_loop = (kLam / 2 + D * (c + 1) + i) * 1024;
           int vo, so;
           if constexpr (fe < NS && re != 2) {
             vo = last ? vb[re + 1] : vo_loop;
@@ -543,14 +546,14 @@ struct TWalker {
     }
     {  // epilogue: static slots; the refills reach into the next stripe
       auto get = [&](auto ii) {
-        constexpr int i = decltype(ii)::value, P = P1 + i, f = NA + 8 * C + sidx(P1, P);
+        constexpr int i = decltype(ii)::value, P = P1 + i, f = NA + D * C + sidx(P1, P);
         const uint4 v = S[f % D];
         return (off(P) & 1) ? make_uint3(v.z, v.w, 0u) : make_uint3(v.x, v.y, 0u);
       };
       pp.template run<NE, true, false>(get, [&](auto ui) {
         constexpr int i = decltype(ui)::value, P = P1 + i;
         if constexpr (i == NE - 1 || key(P + 1) != key(P)) {
-          constexpr int f = NA + 8 * C + sidx(P1, P);
+          constexpr int f = NA + D * C + sidx(P1, P);
           if constexpr (NT_TS_XPRIME || f + D < NS) load_static<f + D>();
           if constexpr (NT_TS_XPRIME && i == NE - 1) {  // the pad slots of the stream: their refills too
             static_for<f + 1, NS>([&](auto gi) { load_static<decltype(gi)::value + D>(); });
