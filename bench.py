@@ -135,8 +135,8 @@ def cpu_baseline(cfg, budget_s=12.0):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="c50k", choices=sorted(CONFIGS))
     ap.add_argument("--reads", type=int, default=0, help="override reads per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
