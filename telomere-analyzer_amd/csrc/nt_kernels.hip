@@ -955,38 +955,43 @@ nt_bundle_kernel(NtBatch B, uint32_t* __restrict__ tp, int L, uint32_t div_m, ui
       *reinterpret_cast<uint4*>(meta + 4 * s) = make_uint4((uint32_t)len, (uint32_t)bo, (uint32_t)(bo >> 32), 0u);
     }
     __syncthreads();
-    for (uint64_t u = 0; u < 2 * (g1 - g0); ++u) {  // half stripes of the bundle
+    // 1. a half stripe's words [w0, w0 + L) of the 32 reads, coalesced (8
+    // bytes a thread), into registers -- the next half stripe's while this
+    // one is transposed -- then into LDS
+    constexpr int kMaxE = (NT_BUNDLE * 170 + 255) / 256;  // L <= 170 (nt_tscan_eligible)
+    uint2 v[kMaxE];
+    auto fetch = [&](uint64_t uu) {
+      const uint64_t wu = (uint64_t)L * uu;
+#pragma unroll
+      for (int k = 0; k < kMaxE; ++k) {
+        const uint32_t e = threadIdx.x + 256u * k;
+        v[k] = make_uint2(0u, 0u);
+        if (e < (uint32_t)(NT_BUNDLE * L)) {
+          const uint32_t rs = __umulhi(e, div_m) >> div_s, wd = e - rs * (uint32_t)L;
+          const uint4 m = *reinterpret_cast<const uint4*>(meta + 4 * rs);
+          if (32 * (int64_t)(wu + wd) < (int64_t)m.x)  // (empty slots have len 0)
+            v[k] = reinterpret_cast<const uint2*>(B.planes)[(((uint64_t)m.z << 32) | m.y) + wu + wd];
+        }
+      }
+    };
+    const uint64_t nu = 2 * (g1 - g0);  // half stripes of the bundle
+    fetch(0);
+    for (uint64_t u = 0; u < nu; ++u) {
       const uint64_t G = g0 + (u >> 1);
       const int h = (int)(u & 1);
       const uint64_t w0 = (uint64_t)L * u;  // first plane word of the half stripe
-      // 1. the 32 reads' words [w0, w0 + L) into LDS, coalesced (8 bytes a
-      // thread), every load of the thread issued before the first is used
-      {
-        constexpr int kMaxE = (NT_BUNDLE * 170 + 255) / 256;  // L <= 170 (nt_tscan_eligible)
-        uint2 v[kMaxE];
 #pragma unroll
-        for (int k = 0; k < kMaxE; ++k) {
-          const uint32_t e = threadIdx.x + 256u * k;
-          v[k] = make_uint2(0u, 0u);
-          if (e < (uint32_t)(NT_BUNDLE * L)) {
-            const uint32_t rs = __umulhi(e, div_m) >> div_s, wd = e - rs * (uint32_t)L;
-            const uint4 m = *reinterpret_cast<const uint4*>(meta + 4 * rs);
-            if (32 * (int64_t)(w0 + wd) < (int64_t)m.x)  // (empty slots have len 0)
-              v[k] = reinterpret_cast<const uint2*>(B.planes)[(((uint64_t)m.z << 32) | m.y) + w0 + wd];
-          }
-        }
-#pragma unroll
-        for (int k = 0; k < kMaxE; ++k) {
-          const uint32_t e = threadIdx.x + 256u * k;
-          if (e < (uint32_t)(NT_BUNDLE * L)) {
-            const uint32_t rs = __umulhi(e, div_m) >> div_s, wd = e - rs * (uint32_t)L;
-            *reinterpret_cast<uint2*>(in + rs * R + 2 * wd) = v[k];
-          }
+      for (int k = 0; k < kMaxE; ++k) {
+        const uint32_t e = threadIdx.x + 256u * k;
+        if (e < (uint32_t)(NT_BUNDLE * L)) {
+          const uint32_t rs = __umulhi(e, div_m) >> div_s, wd = e - rs * (uint32_t)L;
+          *reinterpret_cast<uint2*>(in + rs * R + 2 * wd) = v[k];
         }
       }
       if ((L & 1) && threadIdx.x < 32)  // odd L: the last row's second half holds no position
         *reinterpret_cast<uint2*>(rows + (T - 1) * kBndRowWords + 4 * s + 2) = make_uint2(0u, 0u);
       __syncthreads();
+      if (u + 1 < nu) fetch(u + 1);  // in flight during the transposes and the stores
       // 2. wave wv takes the steps wv, wv + 4, ... (step = 2 words: lanes 0-31
       // the first, 32-63 the second): lane 32 hh + i gets the 32-read columns
       // of position 32 wl + i
