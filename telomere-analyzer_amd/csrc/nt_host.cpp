@@ -679,6 +679,9 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
   const uint64_t tmw = nt_dev_tmask_words(batch->n_windows, batch->n_reads, np);
   if ((e = ctx->tmask.ensure(tmw * 8)) != hipSuccess) return hip_fail(ctx, e, "hipMalloc(tmask)");
   uint64_t* tmask = (uint64_t*)ctx->tmask.p;
+  // debugging: NT_DBG_POISON_AUX=<byte> fills the aux buffer first (every word read must be written)
+  if (const char* v = std::getenv("NT_DBG_POISON_AUX"))
+    (void)hipMemsetAsync(tmask, std::atoi(v) & 255, tmw * 8, ctx->stream);
   // per-wave window counters live in LDS up to the cap, in global scratch beyond
   const uint32_t max_nw = (uint32_t)window_count((int64_t)max_len, L);
   const int noslots = (single || ctx->jit) ? 1 : 0;  // register hit counters

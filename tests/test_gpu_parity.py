@@ -17,6 +17,19 @@ pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
+@pytest.fixture(autouse=True)
+def _torch_stream():
+    """The tests' torch work on a stream of their own (not the null stream,
+    which a context stream created non-blocking does not wait for); _nt()
+    puts each context on it, so fills, copies and clears are ordered with
+    the kernels."""
+    import torch
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        yield
+    s.synchronize()
+
+
 def _nt(jit=True, **kw):
     """NanoTel context; jit=False forces the ahead-of-time scan kernels."""
     from nanotel_amd import NanoTel
@@ -30,6 +43,14 @@ def _nt(jit=True, **kw):
         else:
             os.environ["NT_JIT"] = old
     assert nt.jit == jit, "hiprtc specialisation unavailable"
+    # the context works on the tests' torch stream (_torch_stream): torch
+    # fills, copies and clears of device buffers are ordered with its kernels
+    # (on a stream of its own, a zeros() still in flight could land on the
+    # scan's counts)
+    import torch
+    h = torch.cuda.current_stream().cuda_stream
+    assert h, "the null stream: the context would keep its own"
+    nt.set_stream(h)
     return nt
 
 
@@ -217,7 +238,7 @@ def test_device_synth_matches_host_generator():
     import torch
     from nanotel_amd import NanoTel, read_blocks, synth_params, synth_read_ascii
     sp = synth_params(read_len=5000, first_read=123)
-    nt = NanoTel(patterns="TTAGGG")
+    nt = _nt(patterns="TTAGGG")
     n = 16
     nblk = read_blocks(5000)
     assert nblk == 2 * 79
@@ -363,6 +384,42 @@ def test_bundle_ranges_with_mixed_lengths_and_exceptions(tvr):
     assert nt.tscan
     _check_both(nt, seqs, oracle_rows(seqs, pats, tvr=tvr))
     nt.close()
+
+
+@pytest.mark.parametrize("cfg", [("TTAGGG", None, 1_000_000, 50_000, 0.0),
+                                 ("TTAGGG TCAGGG", "TGAGGG TTGGGG", 400_000, 50_000, 0.05)],
+                         ids=["c50k_full", "c4_shape"])
+def test_full_size_bundle_scan_equals_per_read_scan(cfg):
+    # BASELINE's headline batch (1 M x 50 kb, 50 Gbases) and the c4 program:
+    # the bundle scan (as bench.py runs it) and the per-read scan agree on every
+    # output of every read -- a size-independent check of the path at full size
+    # (the oracle covers the same code on samples above)
+    import torch
+    from nanotel_amd import synth_params
+    pats, tvr, n, read_len, var = cfg
+    nt = _nt(patterns=pats, tvr_patterns=tvr)
+    assert nt.tscan
+    sp = synth_params(read_len=read_len, first_read=31, variant_rate=var)
+    t = _device_batch(nt, sp, n, read_len)
+    nt.scan_call_device(t["planes"].data_ptr(), t["blk_off"].data_ptr(), t["lens"].data_ptr(),
+                        t["win_off"].data_ptr(), n, n * t["rows"], read_len, t["start"].data_ptr(),
+                        t["end"].data_ptr(), t["dens"].data_ptr(), t["flags"].data_ptr(), t["wc"].data_ptr())
+    nt.synchronize()
+    ref = {k: t[k].clone() for k in ("start", "end", "dens", "flags", "wc")}
+    for k in ref:
+        t[k].zero_()
+    b, keep = _device_bundles(nt, t, n, read_len)
+    nt.scan_call_device(t["planes"].data_ptr(), t["blk_off"].data_ptr(), t["lens"].data_ptr(),
+                        t["win_off"].data_ptr(), n, n * t["rows"], read_len, t["start"].data_ptr(),
+                        t["end"].data_ptr(), t["dens"].data_ptr(), t["flags"].data_ptr(), t["wc"].data_ptr(),
+                        bundles=b)
+    nt.synchronize()
+    for k in ("start", "end", "dens", "flags"):
+        assert torch.equal(t[k], ref[k]), k
+    assert torch.equal(_valid_counts(t, n, nt.n_pass), _valid_counts(t, n, nt.n_pass, ref["wc"]))
+    assert int(((t["flags"] & 1) != 0).sum()) > n // 4  # telomeric reads present
+    del t, ref, keep
+    torch.cuda.empty_cache()
 
 
 def test_odd_block_offset_is_reported():
