@@ -288,7 +288,8 @@ def main():
                          "kernel_avg_ms": round(scan_s * 1e3, 4),
                          "kernel_launches_per_step": launches // n_calls,
                          "algorithmic_bytes_per_launch": scan_bytes,
-                         "call_kernel": "nt::nt_call_kernel",
+                         "call_kernel": ("nt_call_jit (calling kernel specialised for the patterns, hiprtc)"
+                                         if nt.call_jit() else "nt_call_kernel (ahead-of-time calling kernel)"),
                          "call_kernel_avg_ms": round(call_ms / n_calls, 4),
                          "call_bytes_per_launch": n * call_bytes_per_read(npass, nw, nt.count_bytes),
                          "step_event_avg_ms": round(sum(step_ms) / len(step_ms), 4)},

@@ -187,6 +187,10 @@ int64_t nt_kernel_times(nt_ctx* ctx, double* scan_ms, double* call_ms);
 /* Scan-kernel launches (bundle-scan ranges count one each) behind the last
  * nt_kernel_times: scan_ms / this = the scan kernel's average launch. */
 int64_t nt_kernel_launches(const nt_ctx* ctx);
+/* 1 if the last nt_scan_call ran the calling kernel specialised for the
+ * program's patterns (hiprtc, built on the first batch of >= 65,536 reads, or
+ * every batch with NT_CALL_JIT=1), 0 for the ahead-of-time one (same results). */
+int nt_call_jit_state(const nt_ctx* ctx);
 
 /* Host-buffer convenience: pack (+rc), upload, scan+call, download, sync.
  * win_counts/hits optional.  Returns the first per-read error, if any. */

@@ -48,6 +48,10 @@ bool nt_jit_get(int device, const NtProgram& P, void* fn[4], void** tfn, std::st
 bool nt_tscan_eligible(const NtProgram& P);
 hipError_t nt_tjit_launch(void* fn, int grid, hipStream_t stream, const NtBatch* B, const NtOut* O,
                           uint64_t* tmask, unsigned long long* queue, uint32_t thr_full);
+void* nt_cjit_get(int device, const NtProgram& P, std::string& err);
+hipError_t nt_cjit_launch(void* fn, int grid, hipStream_t stream, const NtProgram* prog, const NtBatch* B,
+                          const NtOut* O, const uint64_t* tmask, const uint32_t* thr, uint32_t thr_size,
+                          int fix_last);
 hipError_t nt_jit_launch(void* fn, int grid, size_t lds_bytes, hipStream_t stream,
                          const NtProgram* prog, const uint32_t* thr, const NtBatch* B,
                          const NtOut* O, uint64_t* tmask, unsigned long long* queue,
@@ -291,6 +295,12 @@ struct nt_ctx {
   std::vector<uint32_t> thr_h;  // telomeric threshold per window width (nt_compile)
   int tscan_bpc = 0;        // its resident 256-thread blocks per CU
   std::string jit_err;
+  // the calling kernel specialised for the program (nt_call.h via hiprtc),
+  // built on the first batch that uses it; null: the ahead-of-time kernel
+  void* cjit_fn = nullptr;
+  bool cjit_tried = false;
+  int cjit_last = 0;  // the last nt_scan_call launched it
+  std::string cjit_err;
   NtProgram prog{};
   nt_params params{};
   NtProgram* prog_dev = nullptr;
@@ -304,6 +314,33 @@ struct nt_ctx {
 static int fail(nt_ctx* ctx, int code, const std::string& msg) {
   if (ctx) ctx->err = msg;
   return code;
+}
+
+// The calling kernel for a batch of n_reads: the hiprtc-specialised one
+// (letter tests as constant truth tables; 117 VGPRs and no spills against the
+// ahead-of-time kernel's 168 + 15 spilled) for batches of at least
+// kCallJitMinReads reads -- its build takes ~20 s once per pattern set, which
+// only a large batch repays -- else the ahead-of-time kernel (same results).
+// NT_CALL_JIT=1 uses it for every batch, NT_CALL_JIT=0 never.
+constexpr uint64_t kCallJitMinReads = 1u << 16;
+
+static void* call_jit_fn(nt_ctx* ctx, uint64_t n_reads) {
+  const char* v = std::getenv("NT_CALL_JIT");
+  const int mode = v ? std::atoi(v) : -1;
+  if (mode == 0 || !ctx->jit || (mode < 0 && n_reads < kCallJitMinReads)) return nullptr;
+  if (!ctx->cjit_tried) {
+    ctx->cjit_fn = nt_cjit_get(ctx->device, ctx->prog, ctx->cjit_err);
+    ctx->cjit_tried = true;
+  }
+  return ctx->cjit_fn;
+}
+
+static hipError_t launch_call(nt_ctx* ctx, void* cfn, const NtBatch* B, const NtOut* O, const uint64_t* tm,
+                              int fix_last, int grid, hipStream_t s) {
+  const uint32_t* thr = (const uint32_t*)ctx->thr.p;
+  const uint32_t ts = (uint32_t)ctx->thr_h.size();
+  return cfn ? nt_cjit_launch(cfn, grid, s, ctx->prog_dev, B, O, tm, thr, ts, fix_last)
+             : nt_dev_launch_call(ctx->prog_dev, B, O, tm, thr, ts, fix_last, grid, s);
 }
 
 static int hip_fail(nt_ctx* ctx, hipError_t e, const char* what) {
@@ -473,6 +510,8 @@ int nt_compile(nt_ctx* ctx, const nt_params* prm, nt_program_info* info) {
   ctx->params = *prm;
   ctx->compiled = true;
   ctx->jit = nt_jit_get(ctx->device, P, ctx->jit_fn, &ctx->tjit_fn, ctx->jit_err);
+  ctx->cjit_fn = nullptr;
+  ctx->cjit_tried = false;
   ctx->tscan_bpc = 0;
   if (ctx->tjit_fn && std::getenv("NT_TSCAN") && std::getenv("NT_TSCAN")[0] == '0') ctx->tjit_fn = nullptr;
   if (ctx->tjit_fn) {
@@ -741,6 +780,8 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
   const uint64_t nqueue = 2 * nsub + tsub;
   if ((e = ctx->queue.ensure(nqueue * NT_QUEUE_WORDS * 8)) != hipSuccess) return hip_fail(ctx, e, "hipMalloc(queue)");
   unsigned long long* queue = (unsigned long long*)ctx->queue.p;
+  void* cfn = call_jit_fn(ctx, batch->n_reads);  // (built here on first use, before any timing event)
+  ctx->cjit_last = cfn ? 1 : 0;
   hipEvent_t* ev = nullptr;
   if (ctx->profile) {
     if (ctx->n_ev == ctx->ev.size()) {
@@ -813,8 +854,7 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
         cs = ctx->call_stream;
       }
       if (!dbg_skip_call &&
-          (e = nt_dev_launch_call(ctx->prog_dev, &Bc, &O, tmask, (const uint32_t*)ctx->thr.p,
-                                  (uint32_t)ctx->thr_h.size(), 1, cgrid, cs)) != hipSuccess)
+          (e = launch_call(ctx, cfn, &Bc, &O, tmask, 1, cgrid, cs)) != hipSuccess)
         return hip_fail(ctx, e, "launch nt_call_kernel");
     }
   }
@@ -900,21 +940,18 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
       if (n_scan > 0 && !dbg_skip_call) {
         const uint64_t lanes = n_scan * (np <= 2 ? 2u : 4u);
         const int cgrid = (int)std::max<uint64_t>(1, std::min<uint64_t>((lanes + 255) / 256, (uint64_t)ctx->cu_count * 64));
-        e = nt_dev_launch_call(ctx->prog_dev, &Bk, &Ok, tmk, (const uint32_t*)ctx->thr.p, (uint32_t)ctx->thr_h.size(),
-                               0, cgrid, ctx->stream);
+        e = launch_call(ctx, cfn, &Bk, &Ok, tmk, 0, cgrid, ctx->stream);
       }
     } else if (nsub == 1) {
       if (ev) (void)hipEventRecord(ev[1], ctx->stream);
       e = dbg_skip_call ? hipSuccess
-                        : nt_dev_launch_call(ctx->prog_dev, &Bk, &Ok, tmk, (const uint32_t*)ctx->thr.p,
-                                             (uint32_t)ctx->thr_h.size(), 0, (int)call_grid, ctx->stream);
+                        : launch_call(ctx, cfn, &Bk, &Ok, tmk, 0, (int)call_grid, ctx->stream);
     } else {
       // calling kernel of this sub-batch on the call stream, after its scan
       if ((e = hipEventRecord(ctx->ev_scan, ctx->stream)) != hipSuccess ||
           (e = hipStreamWaitEvent(ctx->call_stream, ctx->ev_scan, 0)) != hipSuccess)
         return hip_fail(ctx, e, "stream dependency");
-      e = nt_dev_launch_call(ctx->prog_dev, &Bk, &Ok, tmk, (const uint32_t*)ctx->thr.p, (uint32_t)ctx->thr_h.size(),
-                             0, (int)call_grid, ctx->call_stream);
+      e = launch_call(ctx, cfn, &Bk, &Ok, tmk, 0, (int)call_grid, ctx->call_stream);
     }
     if (e != hipSuccess) return hip_fail(ctx, e, "launch nt_call_kernel");
   }
@@ -985,6 +1022,8 @@ int nt_bundle_layout(nt_ctx* ctx, const nt_batch* batch, uint32_t* tplanes, uint
                                       ctx->prog.div32_s, ctx->stream, ctx->cu_count);
   return e == hipSuccess ? NT_OK : hip_fail(ctx, e, "launch nt_bundle_kernel");
 }
+
+int nt_call_jit_state(const nt_ctx* ctx) { return ctx ? ctx->cjit_last : 0; }
 
 int64_t nt_kernel_launches(const nt_ctx* ctx) { return ctx ? ctx->last_launches : NT_E_ARG; }
 

@@ -36,11 +36,29 @@ struct JitEntry {
 std::mutex g_mu;
 std::map<std::string, JitEntry> g_cache;
 
-std::string pat_type(const NtPat& P) {
+// the calling kernel's modules (a separate hiprtc program: ~20 s to build, so
+// it is built only for batches that pay for it, see nt_host.cpp)
+struct CallEntry {
+  hipModule_t mod = nullptr;
+  hipFunction_t fn = nullptr;
+  std::string err;
+};
+std::map<std::string, CallEntry> g_ccache;
+
+// eq: the code-equality truth tables (fixed=TRUE, the edge steps) instead of the scan's
+std::string pat_type(const NtPat& P, bool eq = false) {
   std::string s = "nt::CtPat<" + std::to_string(P.m);
-  for (int j = 0; j < P.m; ++j) s += ", " + std::to_string((int)P.tt_scan[j]);
+  for (int j = 0; j < P.m; ++j) s += ", " + std::to_string((int)(eq ? P.tt_eq[j] : P.tt_scan[j]));
   return s + ">";
 }
+
+const char* const kTypedefs =
+    "typedef __hip_internal::uint8_t uint8_t;\n"
+    "typedef __hip_internal::uint16_t uint16_t;\n"
+    "typedef __hip_internal::uint32_t uint32_t;\n"
+    "typedef __hip_internal::uint64_t uint64_t;\n"
+    "typedef __hip_internal::int32_t int32_t;\n"
+    "typedef __hip_internal::int64_t int64_t;\n";
 
 }  // namespace
 
@@ -66,13 +84,7 @@ std::string jit_source(const NtProgram& P) {
   std::string pats, tvrs;
   for (int i = 0; i < P.n_pat; ++i) pats += (i ? ", " : "") + pat_type(P.pat[i]);
   for (int i = 0; i < P.n_tvr; ++i) tvrs += (i ? ", " : "") + pat_type(P.tvr[i]);
-  std::string s;
-  s += "typedef __hip_internal::uint8_t uint8_t;\n";
-  s += "typedef __hip_internal::uint16_t uint16_t;\n";
-  s += "typedef __hip_internal::uint32_t uint32_t;\n";
-  s += "typedef __hip_internal::uint64_t uint64_t;\n";
-  s += "typedef __hip_internal::int32_t int32_t;\n";
-  s += "typedef __hip_internal::int64_t int64_t;\n";
+  std::string s = kTypedefs;
   s += "#include \"nt_tscan.h\"\n";
   s += "using JitSet = nt::CtSet<nt::CtList<" + pats + ">, nt::CtList<" + tvrs + ">>;\n";
   if (nt_tscan_eligible(P)) {
@@ -123,12 +135,32 @@ NT_JIT_KERNELS(nt_scan_jit_nh, false)
   return s;
 }
 
-bool compile(int device, const std::string& src, JitEntry& e) {
+// The program's source of the calling kernel (nt_call.h) with its patterns as types.
+std::string call_source(const NtProgram& P) {
+  std::string pats, tvrs, pats_eq, tvrs_eq;
+  for (int i = 0; i < P.n_pat; ++i) {
+    pats += (i ? ", " : "") + pat_type(P.pat[i]);
+    pats_eq += (i ? ", " : "") + pat_type(P.pat[i], true);
+  }
+  for (int i = 0; i < P.n_tvr; ++i) {
+    tvrs += (i ? ", " : "") + pat_type(P.tvr[i]);
+    tvrs_eq += (i ? ", " : "") + pat_type(P.tvr[i], true);
+  }
+  std::string s = kTypedefs;
+  s += "#include \"nt_call.h\"\n";
+  s += "using JitCall = nt::CtCall<nt::CtList<" + pats + ">, nt::CtList<" + tvrs + ">, nt::CtList<" + pats_eq +
+       ">, nt::CtList<" + tvrs_eq + ">>;\n";
+  s += "NT_CALL_KERNEL(nt_call_jit, JitCall)\n";
+  return s;
+}
+
+// hiprtc-compiles src into a loaded module
+bool compile_module(int device, const std::string& src, hipModule_t& mod, std::string& err) {
   hiprtcProgram prog;
-  const char* hdrs[] = {kJitCommon, kJitDevice, kJitScan, kJitTScan};
-  const char* names[] = {"nt_common.h", "nt_device.h", "nt_scan.h", "nt_tscan.h"};
-  if (hiprtcCreateProgram(&prog, src.c_str(), "nt_scan_jit.hip", 4, hdrs, names) != HIPRTC_SUCCESS) {
-    e.err = "hiprtcCreateProgram failed";
+  const char* hdrs[] = {kJitCommon, kJitDevice, kJitScan, kJitTScan, kJitCall};
+  const char* names[] = {"nt_common.h", "nt_device.h", "nt_scan.h", "nt_tscan.h", "nt_call.h"};
+  if (hiprtcCreateProgram(&prog, src.c_str(), "nt_jit.hip", 5, hdrs, names) != HIPRTC_SUCCESS) {
+    err = "hiprtcCreateProgram failed";
     return false;
   }
   hipDeviceProp_t prop;
@@ -162,7 +194,7 @@ bool compile(int device, const std::string& src, JitEntry& e) {
     hiprtcGetProgramLogSize(prog, &n);
     std::string log(n + 1, '\0');
     hiprtcGetProgramLog(prog, &log[0]);
-    e.err = std::string("hiprtc: ") + hiprtcGetErrorString(rc) + "\n" + log.c_str();
+    err = std::string("hiprtc: ") + hiprtcGetErrorString(rc) + "\n" + log.c_str();
     hiprtcDestroyProgram(&prog);
     return false;
   }
@@ -171,11 +203,21 @@ bool compile(int device, const std::string& src, JitEntry& e) {
   std::vector<char> code(n);
   hiprtcGetCode(prog, code.data());
   hiprtcDestroyProgram(&prog);
-  hipError_t he = hipModuleLoadData(&e.mod, code.data());
+  const hipError_t he = hipModuleLoadData(&mod, code.data());
+  if (he != hipSuccess) {
+    err = std::string("hipModuleLoadData: ") + hipGetErrorString(he);
+    return false;
+  }
+  return true;
+}
+
+bool compile(int device, const std::string& src, JitEntry& e) {
+  if (!compile_module(device, src, e.mod, e.err)) return false;
+  hipError_t he = hipSuccess;
   const char* names4[4] = {"nt_scan_jit_lds", "nt_scan_jit_gmem", "nt_scan_jit_nh_lds", "nt_scan_jit_nh_gmem"};
   for (int i = 0; i < 4 && he == hipSuccess; ++i) he = hipModuleGetFunction(&e.fn[i], e.mod, names4[i]);
   if (he != hipSuccess) {
-    e.err = std::string("hipModuleLoadData: ") + hipGetErrorString(he);
+    e.err = std::string("hipModuleGetFunction: ") + hipGetErrorString(he);
     return false;
   }
   if (src.find("nt_tscan_jit(") != std::string::npos &&
@@ -240,4 +282,40 @@ int nt_jit_blocks_per_cu(void* fn, size_t lds_bytes) {
       hipSuccess)
     return 0;
   return nb;
+}
+
+// The calling kernel specialised for the program's patterns (nt_call.h,
+// CtCall), or null (and a message) when specialisation is off or failed --
+// the caller then launches the ahead-of-time kernel (same results).
+void* nt_cjit_get(int device, const NtProgram& P, std::string& err) {
+  const char* env = std::getenv("NT_JIT");
+  if (env && env[0] == '0') {
+    err = "NT_JIT=0";
+    return nullptr;
+  }
+  const std::string src = call_source(P);
+  const char* xo = std::getenv("NT_JIT_OPTS");
+  const std::string key = std::to_string(device) + "\n" + (xo ? xo : "") + "\n" + src;
+  std::lock_guard<std::mutex> lk(g_mu);
+  auto it = g_ccache.find(key);
+  if (it == g_ccache.end()) {
+    CallEntry e;
+    if (compile_module(device, src, e.mod, e.err) &&
+        hipModuleGetFunction(&e.fn, e.mod, "nt_call_jit") != hipSuccess) {
+      e.fn = nullptr;
+      e.err = "hipModuleGetFunction(nt_call_jit)";
+    }
+    it = g_ccache.emplace(key, e).first;
+  }
+  if (!it->second.fn) err = it->second.err;
+  return (void*)it->second.fn;
+}
+
+hipError_t nt_cjit_launch(void* fn, int grid, hipStream_t stream, const NtProgram* prog, const NtBatch* B,
+                          const NtOut* O, const uint64_t* tmask, const uint32_t* thr, uint32_t thr_size,
+                          int fix_last) {
+  NtBatch b = *B;
+  NtOut o = *O;
+  void* args[] = {&prog, &b, &o, &tmask, &thr, &thr_size, &fix_last};
+  return hipModuleLaunchKernel((hipFunction_t)fn, (unsigned)grid, 1, 1, 256, 1, 1, 0, stream, args, nullptr);
 }

@@ -101,6 +101,7 @@ SIGNATURES = {
     "nt_kernel_times": (ctypes.c_int64, [_P, ctypes.POINTER(ctypes.c_double),
                                          ctypes.POINTER(ctypes.c_double)]),
     "nt_kernel_launches": (ctypes.c_int64, [_P]),
+    "nt_call_jit_state": (ctypes.c_int, [_P]),
     "nt_analyze_host": (ctypes.c_int, [_P, _P, _P, ctypes.c_uint64, _P, _P, _P, _P, _P, _P]),
     "nt_filter_call": (ctypes.c_int, [_P, _P, _P]),
     "nt_filter_host": (ctypes.c_int, [_P, _P, _P, ctypes.c_uint64, _P]),

@@ -111,6 +111,11 @@ class NanoTel:
         ranges launches once per range): scan_ms / this = one launch."""
         return int(_check(lib().nt_kernel_launches(self._h), self._h))
 
+    def call_jit(self):
+        """True if the last scan_call() ran the calling kernel specialised for
+        the patterns (hiprtc), False for the ahead-of-time one."""
+        return bool(lib().nt_call_jit_state(self._h))
+
     def synchronize(self):
         _check(lib().nt_synchronize(self._h), self._h)
 

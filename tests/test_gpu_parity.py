@@ -160,6 +160,30 @@ def test_baseline_config_reads(cfg):
 ])
 @pytest.mark.parametrize("jit", [True, False], ids=["jit", "aot"])
 def test_random_reads(cfg, jit):
+    _random_reads(cfg, jit)
+
+
+# the calling kernel specialised for the patterns (nt_call.h through hiprtc,
+# ~8-25 s to build per pattern set, so a representative subset): forced with
+# NT_CALL_JIT=1 for these small batches (by default it serves batches of
+# >= 65,536 reads, where the full-size tests and the bench exercise it)
+@pytest.mark.parametrize("cfg", [
+    dict(patterns="TTAGGG"),
+    dict(patterns="YYAGGG"),
+    dict(patterns="CCCTAA", check_right_edge=True),
+    dict(patterns="TTAGGG TCAGGG", tvr_patterns="TGAGGG TTGGGG"),
+    dict(patterns="TTAGGG", subseq_length=37, min_density=0.3),
+    dict(patterns="TTAGGN"),
+    dict(patterns="TTRGGG CCCTAA", tvr_patterns="TYAGGG"),
+    dict(patterns="TAGGGTTAGGGTTAGGGT"),
+])
+def test_random_reads_specialised_call(cfg, monkeypatch):
+    monkeypatch.setenv("NT_CALL_JIT", "1")
+    nt = _random_reads(cfg, True)
+    assert nt.call_jit(), "the specialised calling kernel did not run"
+
+
+def _random_reads(cfg, jit):
     rng = np.random.default_rng(zlib.crc32(str(sorted(cfg.items())).encode()))
     seqs = []
     right = cfg.get("check_right_edge", False)
@@ -175,6 +199,7 @@ def test_random_reads(cfg, jit):
     orow = oracle_rows(seqs, cfg["patterns"], tvr=cfg.get("tvr_patterns"), L=cfg.get("subseq_length", 100),
                        min_density=cfg.get("min_density", 0.6), right_edge=right, rc=cfg.get("rc", False))
     _check_both(nt, seqs, orow)
+    return nt
 
 
 @pytest.mark.parametrize("jit", [True, False], ids=["jit", "aot"])

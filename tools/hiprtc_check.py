@@ -6,6 +6,8 @@ same headers and options nt_jit.cpp uses, for a pattern type list such as
 headers) before a GPU run.
 
 usage: tools/hiprtc_check.py "nt::CtPat<6,8,8,1,4,4,4>" [tvr list] [L] [extra options...]
+       tools/hiprtc_check.py --call "<patterns>" "<tvrs>" "<patterns, eq tables>" "<tvrs, eq tables>"
+         (the calling kernel, nt_call.h)
 """
 import ctypes
 import os
@@ -16,6 +18,8 @@ CSRC = os.path.join(HERE, "..", "telomere-analyzer_amd", "csrc")
 
 
 def main():
+    if sys.argv[1] == "--call":
+        return call_main()
     pats = sys.argv[1]
     tvrs = sys.argv[2] if len(sys.argv) > 2 else ""
     L = sys.argv[3] if len(sys.argv) > 3 else "100"
@@ -33,12 +37,28 @@ nt_tscan_jit(NtBatch B, NtOut O, uint64_t* __restrict__ tmask, unsigned long lon
   nt::tscan_bundles<TJit, TPats, TTvrs>(B, O, tmask, queue, thr_full, tsl + (threadIdx.x >> 6) * nt::kTsLdsWords);
 }
 """
-    names = ["nt_common.h", "nt_device.h", "nt_scan.h", "nt_tscan.h"]
+    sys.exit(compile_src(src, extra))
+
+
+def call_main():
+    pats, tvrs, pats_eq, tvrs_eq = (sys.argv[2:6] + ["", "", "", ""])[:4]
+    src = "".join(f"typedef __hip_internal::{t} {t};\n" for t in
+                  ("uint8_t", "uint16_t", "uint32_t", "uint64_t", "int32_t", "int64_t"))
+    src += '#include "nt_call.h"\n'
+    src += (f"using JitCall = nt::CtCall<nt::CtList<{pats}>, nt::CtList<{tvrs}>, nt::CtList<{pats_eq}>, "
+            f"nt::CtList<{tvrs_eq}>>;\nNT_CALL_KERNEL(nt_call_jit, JitCall)\n")
+    sys.exit(compile_src(src, sys.argv[6:]))
+
+
+def compile_src(src, extra):
+    import time
+    names = ["nt_common.h", "nt_device.h", "nt_scan.h", "nt_tscan.h", "nt_call.h"]
     hdrs = [open(os.path.join(CSRC, n), "rb").read() for n in names]
     lib = ctypes.CDLL("/opt/rocm/lib/libhiprtc.so")
     prog = ctypes.c_void_p()
-    arr = ctypes.c_char_p * 4
-    rc = lib.hiprtcCreateProgram(ctypes.byref(prog), src.encode(), b"nt_scan_jit.hip", 4,
+    arr = ctypes.c_char_p * len(names)
+    t0 = time.time()
+    rc = lib.hiprtcCreateProgram(ctypes.byref(prog), src.encode(), b"nt_jit.hip", len(names),
                                  arr(*hdrs), arr(*[n.encode() for n in names]))
     assert rc == 0, rc
     opts = [b"--offload-arch=gfx950", b"-O3", b"-std=c++17", b"-ffp-contract=off", b"-mllvm",
@@ -49,8 +69,8 @@ nt_tscan_jit(NtBatch B, NtOut O, uint64_t* __restrict__ tmask, unsigned long lon
     log = ctypes.create_string_buffer(n.value + 1)
     lib.hiprtcGetProgramLog(prog, log)
     print(log.value.decode(errors="replace")[-4000:])
-    print("hiprtc rc", rc)
-    sys.exit(0 if rc == 0 else 1)
+    print("hiprtc rc", rc, f"({time.time() - t0:.1f} s)")
+    return 0 if rc == 0 else 1
 
 
 if __name__ == "__main__":
