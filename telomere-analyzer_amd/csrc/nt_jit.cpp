@@ -15,6 +15,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <map>
 #include <mutex>
 #include <string>
@@ -300,10 +301,35 @@ void* nt_cjit_get(int device, const NtProgram& P, std::string& err) {
   auto it = g_ccache.find(key);
   if (it == g_ccache.end()) {
     CallEntry e;
-    if (compile_module(device, src, e.mod, e.err) &&
-        hipModuleGetFunction(&e.fn, e.mod, "nt_call_jit") != hipSuccess) {
-      e.fn = nullptr;
-      e.err = "hipModuleGetFunction(nt_call_jit)";
+    auto build = [&](const std::string& s) {
+      if (compile_module(device, s, e.mod, e.err) &&
+          hipModuleGetFunction(&e.fn, e.mod, "nt_call_jit") != hipSuccess) {
+        e.fn = nullptr;
+        e.err = "hipModuleGetFunction(nt_call_jit)";
+      }
+    };
+    build(src);
+    // Several patterns and TVRs raise the register demand of the unrolled
+    // neighbourhood code: at 3 waves/SIMD (168 VGPRs) the c4 set spilled 107
+    // VGPRs to scratch and called in 3.6 ms per 2M x 50 kb; at 2 (253 VGPRs, no
+    // spill) 2.0 ms.  A build that spills more than kCallScratchMax bytes a
+    // lane is redone at 2 waves/SIMD (a few spilled registers cost less than
+    // the occupancy: the 1-pattern kernels run at 3-4).
+    constexpr int kCallScratchMax = 64;
+    int scratch = 0;
+    const bool forced = xo && std::strstr(xo, "NT_CALL_WAVES_PER_EU");  // a tuning run sets it
+    if (e.fn && !forced &&
+        hipFuncGetAttribute(&scratch, HIP_FUNC_ATTRIBUTE_LOCAL_SIZE_BYTES, e.fn) == hipSuccess &&
+        scratch > kCallScratchMax) {
+      const hipModule_t m1 = e.mod;
+      const hipFunction_t f1 = e.fn;
+      build("#define NT_CALL_WAVES_PER_EU 2\n" + src);
+      if (e.fn) {
+        (void)hipModuleUnload(m1);
+      } else {
+        e.mod = m1;
+        e.fn = f1;
+      }
     }
     it = g_ccache.emplace(key, e).first;
   }
