@@ -434,9 +434,28 @@ static __device__ __forceinline__ int cov_count(const Lane& c, int x, int y) { r
 // windows, recomputed coverage for the partial windows at the two ends.
 // Covered bases of windows [0, k) (0 <= k <= nw): the scan's checkpoint at
 // window 16*(k/16) plus at most 15 window counts (independent loads).
+// 8-bit counts: the 16 counts of a checkpoint group are one aligned 16-byte
+// load (rows start on 64-window boundaries), summed under a byte mask with
+// v_dot4_u32_u8 -- one load instead of up to 15 (c10k: the two densities of
+// a call 0.20 -> see DESIGN §4.2).
 static __device__ __forceinline__ int cnt_before(const Lane& c, int k) {
   const int r = k & 15, k0 = k - r;
   int t = (int)c.ck[k >> 4];
+  if (c.c8) {
+    if (r > 0) {  // (r == 0: the group may lie past the row's allocation)
+      const uint4 v = reinterpret_cast<const uint4*>(c.cnt)[k >> 4];
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+      uint32_t acc = 0u;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int nb = min(max(r - 4 * i, 0), 4);  // bytes of word i before window k
+        const uint32_t m = nb >= 4 ? 0xFFFFFFFFu : ((1u << (8 * nb)) - 1u);
+        acc = __builtin_amdgcn_udot4(w[i] & m, 0x01010101u, acc, false);
+      }
+      t += (int)acc;
+    }
+    return t;
+  }
 #pragma unroll
   for (int i = 0; i < 15; ++i)
     if (i < r) t += wcount(c, k0 + i);
@@ -924,7 +943,9 @@ static __device__ __forceinline__ void run(const NtProgram* __restrict__ prog, N
         c.k = p == 0 ? 0 : 1;
         c.use_tvr = p == 2;
         c.raw = p == 0 && prog->raw_p1;
+#ifndef NT_DBG_NO_FIXLAST  // timing experiments only (wrong results for bundled reads)
         if (fix_last) call_fix_last(c, thr, thr_size);
+#endif
         call_pass(c, s, e, d, flags);
         if (s == -1) flags |= 1u << (NT_FLAG_NA_SHIFT + p);
         w = e - s + 1;
