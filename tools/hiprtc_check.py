@@ -17,40 +17,47 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "..", "telomere-analyzer_amd", "csrc")
 
 
-def main():
-    if sys.argv[1] == "--call":
-        return call_main()
-    pats = sys.argv[1]
-    tvrs = sys.argv[2] if len(sys.argv) > 2 else ""
-    L = sys.argv[3] if len(sys.argv) > 3 else "100"
-    extra = sys.argv[4:]
-    src = "".join(f"typedef __hip_internal::{t} {t};\n" for t in
-                  ("uint8_t", "uint16_t", "uint32_t", "uint64_t", "int32_t", "int64_t"))
-    src += '#include "nt_tscan.h"\n'
+TYPEDEFS = "".join(f"typedef __hip_internal::{t} {t};\n" for t in
+                   ("uint8_t", "uint16_t", "uint32_t", "uint64_t", "int32_t", "int64_t"))
+
+
+def tscan_source(pats, tvrs="", L="100"):
+    """The bundle scan's hiprtc source (as nt_jit.cpp jit_source builds it)."""
+    src = TYPEDEFS + '#include "nt_tscan.h"\n'
     src += f"using TPats = nt::CtList<{pats}>;\nusing TTvrs = nt::CtList<{tvrs}>;\n"
     src += f"using TJit = nt::TProg<TPats, TTvrs, {L}>;\n"
     src += """
-extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3)))
+extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
 nt_tscan_jit(NtBatch B, NtOut O, uint64_t* __restrict__ tmask, unsigned long long* __restrict__ queue,
              uint32_t thr_full) {
   __shared__ uint32_t tsl[4 * nt::kTsLdsWords];
   nt::tscan_bundles<TJit, TPats, TTvrs>(B, O, tmask, queue, thr_full, tsl + (threadIdx.x >> 6) * nt::kTsLdsWords);
 }
 """
-    sys.exit(compile_src(src, extra))
+    return src
 
 
-def call_main():
-    pats, tvrs, pats_eq, tvrs_eq = (sys.argv[2:6] + ["", "", "", ""])[:4]
-    src = "".join(f"typedef __hip_internal::{t} {t};\n" for t in
-                  ("uint8_t", "uint16_t", "uint32_t", "uint64_t", "int32_t", "int64_t"))
-    src += '#include "nt_call.h"\n'
-    src += (f"using JitCall = nt::CtCall<nt::CtList<{pats}>, nt::CtList<{tvrs}>, nt::CtList<{pats_eq}>, "
+def call_source(pats, tvrs="", pats_eq=None, tvrs_eq=None):
+    """The calling kernel's hiprtc source (as nt_jit.cpp call_source builds it)."""
+    pats_eq = pats if pats_eq is None else pats_eq
+    tvrs_eq = tvrs if tvrs_eq is None else tvrs_eq
+    return (TYPEDEFS + '#include "nt_call.h"\n'
+            f"using JitCall = nt::CtCall<nt::CtList<{pats}>, nt::CtList<{tvrs}>, nt::CtList<{pats_eq}>, "
             f"nt::CtList<{tvrs_eq}>>;\nNT_CALL_KERNEL(nt_call_jit, JitCall)\n")
-    sys.exit(compile_src(src, sys.argv[6:]))
 
 
-def compile_src(src, extra):
+def main():
+    if sys.argv[1] == "--call":
+        pats, tvrs, pats_eq, tvrs_eq = (sys.argv[2:6] + ["", "", "", ""])[:4]
+        sys.exit(compile_src(call_source(pats, tvrs, pats_eq, tvrs_eq), sys.argv[6:]))
+    pats = sys.argv[1]
+    tvrs = sys.argv[2] if len(sys.argv) > 2 else ""
+    L = sys.argv[3] if len(sys.argv) > 3 else "100"
+    sys.exit(compile_src(tscan_source(pats, tvrs, L), sys.argv[4:]))
+
+
+def compile_src(src, extra=(), quiet=False):
+    """hiprtc-compiles src for gfx950 with nt_jit.cpp's options; 0 = built."""
     import time
     names = ["nt_common.h", "nt_device.h", "nt_scan.h", "nt_tscan.h", "nt_call.h"]
     hdrs = [open(os.path.join(CSRC, n), "rb").read() for n in names]
@@ -68,7 +75,8 @@ def compile_src(src, extra):
     lib.hiprtcGetProgramLogSize(prog, ctypes.byref(n))
     log = ctypes.create_string_buffer(n.value + 1)
     lib.hiprtcGetProgramLog(prog, log)
-    print(log.value.decode(errors="replace")[-4000:])
+    if not quiet or rc != 0:
+        print(log.value.decode(errors="replace")[-4000:])
     print("hiprtc rc", rc, f"({time.time() - t0:.1f} s)")
     return 0 if rc == 0 else 1
 
