@@ -22,7 +22,7 @@ def main():
     out, config, reads, jit = sys.argv[1], sys.argv[2], int(sys.argv[3]), bool(int(sys.argv[4]))
     dest = sys.argv[5] if len(sys.argv) > 5 else "profiles/pmc_traffic.json"
     is_scan = lambda k: "nt_scan" in k or "nt_tscan" in k  # noqa: E731 (per-read or bundle scan)
-    is_call = lambda k: "nt_call_kernel" in k  # noqa: E731
+    is_call = lambda k: "nt_call_kernel" in k or "nt_call_jit" in k  # noqa: E731 (AOT or specialised)
     res = {"config": config, "reads": reads, "jit": jit,
            "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), per dispatch mean; "
                      "read bytes = FETCH_SIZE*1024*2 (gfx950 halves wide streaming reads), "
