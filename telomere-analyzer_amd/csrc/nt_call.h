@@ -58,6 +58,7 @@ struct RtTableEq {
 // known at compile time (-1: read the program).
 struct RtCall {
   static constexpr int kNTvr = -1;
+  static constexpr bool kMayRaw = true;  // P1 raw views possible (program's raw_p1)
   template <class F>
   __device__ __forceinline__ static void for_pat(const NtProgram* prog, F&& f) {
     for (int p = 0; p < prog->n_pat; ++p) f(p, RtTable<0>{&prog->pat[p]});
@@ -78,9 +79,12 @@ struct RtCall {
 
 // Compile-time lists (hiprtc): CtList<CtPat<m, tt...>...> of the scan truth
 // tables and of the code-equality ones, for the patterns and the TVRs.
-template <class Pats, class Tvrs, class PatsEq, class TvrsEq>
+template <class Pats, class Tvrs, class PatsEq, class TvrsEq, bool kRaw>
 struct CtCall {
   static constexpr int kNTvr = Tvrs::kN;
+  // raw_p1 (single fixed pattern) known: without it the raw-view marks and
+  // their registers are compiled out
+  static constexpr bool kMayRaw = kRaw;
   template <class F>
   __device__ __forceinline__ static void for_pat(const NtProgram* prog, F&& f) {
     CtVisit<Pats>::run(prog->pat, f);
@@ -137,6 +141,22 @@ __device__ __forceinline__ void words_hits(const D& d, const uint32_t* Lw, const
 #pragma unroll
       for (int h = 0; h < NH; ++h) x1[h] &= Vw[h];
     }
+  }
+}
+
+// A copy of the n words the compiler cannot prove equal to the originals
+// (an empty asm per word): letter tests made from it are not common
+// subexpressions of another pattern's, so they are recomputed (one op each)
+// instead of held live across all the patterns (NT_CALL_LAUNDER).
+#ifndef NT_CALL_LAUNDER
+#define NT_CALL_LAUNDER 1
+#endif
+template <int N>
+__device__ __forceinline__ void launder_words(const uint32_t* in, uint32_t* out) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    out[i] = in[i];
+    if (NT_CALL_LAUNDER) asm volatile("" : "+v"(out[i]));
   }
 }
 
@@ -313,7 +333,11 @@ static __device__ __forceinline__ void nb_compute(const Lane& c, int q0, const N
     constexpr int kM = decltype(d)::kM;
     const int m = d.m();
     uint32_t x0[NH], x1[NH];
-    words_hits<NH>(d, Lw, Hw, Vw, x0, x1);
+    uint32_t Lp[NP], Hp[NP], Vp[NP];
+    launder_words<NP>(Lw, Lp);
+    launder_words<NP>(Hw, Hp);
+    launder_words<NP>(Vw, Vp);
+    words_hits<NH>(d, Lp, Hp, Vp, x0, x1);
     if (c.rc.n_exc) {
 #pragma unroll
       for (int h = 0; h < NH; ++h)
@@ -324,7 +348,7 @@ static __device__ __forceinline__ void nb_compute(const Lane& c, int q0, const N
     for (int ci = 0; ci < NC; ++ci)
       nb.cov[ci + 1 - E] |= spread<kM>(c.k ? x1[ci + 1] : x0[ci + 1], c.k ? x1[ci] : x0[ci], m);
     if constexpr (kMarks) {
-      if (c.raw && pi == 0) {
+      if (CS::kMayRaw && c.raw && pi == 0) {
 #pragma unroll
         for (int ci = 0; ci < NC; ++ci) {
           nb.rs[ci] = x0[ci + 1];
@@ -337,7 +361,11 @@ static __device__ __forceinline__ void nb_compute(const Lane& c, int q0, const N
     CS::for_tvr(prog, [&](int, auto d) {
       constexpr int kM = decltype(d)::kM;
       uint32_t x0[NH], x1[NH];
-      words_hits<NH>(d, Lw, Hw, Vw, x0, x1);
+      uint32_t Lp[NP], Hp[NP], Vp[NP];
+      launder_words<NP>(Lw, Lp);
+      launder_words<NP>(Hw, Hp);
+      launder_words<NP>(Vw, Vp);
+      words_hits<NH>(d, Lp, Hp, Vp, x0, x1);
       if (c.rc.n_exc) {
 #pragma unroll
         for (int h = 0; h < NH; ++h)
@@ -372,7 +400,7 @@ static __device__ __forceinline__ int nb_min_start(const Lane& c, const Nb<K>& n
 #pragma unroll
   for (int i = 0; i < K; ++i) {
     const uint32_t cur = nb.cov[i + 1];
-    const uint32_t mk = c.raw ? nb.rs[i + 1] : (cur & ~((cur << 1) | (nb.cov[i] >> 31)));
+    const uint32_t mk = (CS::kMayRaw && c.raw) ? nb.rs[i + 1] : (cur & ~((cur << 1) | (nb.cov[i] >> 31)));
     const uint32_t m = mk & range_mask((int64_t)nb.q0 + 32 * i, a, b);
     if (!found && m) {
       res = nb.q0 + 32 * i + __builtin_ctz(m) + 1;
@@ -391,7 +419,7 @@ static __device__ __forceinline__ int nb_max_end(const Lane& c, const Nb<K>& nb,
 #pragma unroll
   for (int i = K - 1; i >= 0; --i) {
     const uint32_t cur = nb.cov[i + 1];
-    const uint32_t mk = c.raw ? nb.re[i + 1] : (cur & ~((cur >> 1) | (nb.cov[i + 2] << 31)));
+    const uint32_t mk = (CS::kMayRaw && c.raw) ? nb.re[i + 1] : (cur & ~((cur >> 1) | (nb.cov[i + 2] << 31)));
     const uint32_t m = mk & range_mask((int64_t)nb.q0 + 32 * i, a, b);
     if (!found && m) {
       res = nb.q0 + 32 * i + (31 - __builtin_clz(m)) + 1;

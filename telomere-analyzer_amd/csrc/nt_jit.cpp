@@ -150,7 +150,7 @@ std::string call_source(const NtProgram& P) {
   std::string s = kTypedefs;
   s += "#include \"nt_call.h\"\n";
   s += "using JitCall = nt::CtCall<nt::CtList<" + pats + ">, nt::CtList<" + tvrs + ">, nt::CtList<" + pats_eq +
-       ">, nt::CtList<" + tvrs_eq + ">>;\n";
+       ">, nt::CtList<" + tvrs_eq + ">, " + (P.raw_p1 ? "true" : "false") + ">;\n";
   s += "NT_CALL_KERNEL(nt_call_jit, JitCall)\n";
   return s;
 }

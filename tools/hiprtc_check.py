@@ -37,13 +37,17 @@ nt_tscan_jit(NtBatch B, NtOut O, uint64_t* __restrict__ tmask, unsigned long lon
     return src
 
 
-def call_source(pats, tvrs="", pats_eq=None, tvrs_eq=None):
-    """The calling kernel's hiprtc source (as nt_jit.cpp call_source builds it)."""
+def call_source(pats, tvrs="", pats_eq=None, tvrs_eq=None, raw=None):
+    """The calling kernel's hiprtc source (as nt_jit.cpp call_source builds it).
+    raw: the program keeps P1's raw views (one fixed pattern); default: one
+    pattern in the list."""
+    if raw is None:
+        raw = pats.count("CtPat") == 1
     pats_eq = pats if pats_eq is None else pats_eq
     tvrs_eq = tvrs if tvrs_eq is None else tvrs_eq
     return (TYPEDEFS + '#include "nt_call.h"\n'
             f"using JitCall = nt::CtCall<nt::CtList<{pats}>, nt::CtList<{tvrs}>, nt::CtList<{pats_eq}>, "
-            f"nt::CtList<{tvrs_eq}>>;\nNT_CALL_KERNEL(nt_call_jit, JitCall)\n")
+            f"nt::CtList<{tvrs_eq}>, {'true' if raw else 'false'}>;\nNT_CALL_KERNEL(nt_call_jit, JitCall)\n")
 
 
 def main():
