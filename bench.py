@@ -154,9 +154,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # NT_BENCH_BACKEND=gloo: a rehearsal of the N-rank path on fewer GPUs (ranks
+    # share GPUs round-robin, host collectives); the measurement runs RCCL, one
+    # rank per GPU
+    backend = os.environ.get("NT_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(1, torch.cuda.device_count())
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -241,7 +250,7 @@ def main():
     assert n_calls == args.steps
     launches = nt.kernel_launches()  # the bundle scan runs in ranges: per-LAUNCH figures below
     if world > 1:
-        t = torch.tensor([wall], dtype=torch.float64, device=dev)
+        t = torch.tensor([wall], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wall = float(t.item())
 
@@ -291,7 +300,9 @@ def main():
                          "call_kernel": ("nt_call_jit (calling kernel specialised for the patterns, hiprtc)"
                                          if nt.call_jit() else "nt_call_kernel (ahead-of-time calling kernel)"),
                          "call_kernel_avg_ms": round(call_ms / n_calls, 4),
-                         "call_bytes_per_launch": n * call_bytes_per_read(npass, nw, nt.count_bytes),
+                         # the calling kernel runs once per scan launch (bundle range)
+                         "call_bytes_per_launch": n * call_bytes_per_read(npass, nw, nt.count_bytes) * n_calls
+                         // launches,
                          "step_event_avg_ms": round(sum(step_ms) / len(step_ms), 4)},
         }
         if world == 1 and not args.no_cpu_baseline:
