@@ -132,6 +132,29 @@ def cpu_baseline(cfg, budget_s=12.0):
     return out
 
 
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _launch_ranks(n):
+    """`bench.py --gpus N` run without a launcher: start N ranks, one process
+    per GPU (torch.distributed.run on 127.0.0.1), as child processes of this
+    one -- which has not touched the GPU -- and return their exit status.
+    Rank 0 prints the JSON line.  (The reference's parallelism is the 8-way
+    fork of NanoTel.R:2207, 2245-2254; here one process per GPU.)"""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -143,6 +166,14 @@ def main():
     ap.add_argument("--per-read", action="store_true", help="per-read scan only (no bundle layout)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(_launch_ranks(args.gpus))
+    if int(os.environ.get("WORLD_SIZE", "1")) != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={os.environ.get('WORLD_SIZE')} ranks were launched",
+              file=sys.stderr)
+        sys.exit(2)
 
     import torch
     import torch.distributed as dist
@@ -160,6 +191,10 @@ def main():
     backend = os.environ.get("NT_BENCH_BACKEND", "nccl")
     if backend != "nccl":
         local = local % max(1, torch.cuda.device_count())
+    elif world > torch.cuda.device_count():
+        print(f"bench.py: {world} ranks over RCCL need {world} GPUs, {torch.cuda.device_count()} visible "
+              f"(NT_BENCH_BACKEND=gloo rehearses N ranks on fewer GPUs)", file=sys.stderr)
+        sys.exit(2)
     if world > 1:
         torch.cuda.set_device(local)
         if backend == "nccl":
@@ -207,16 +242,20 @@ def main():
         if plan.tplane_bytes + (4 << 30) > free:
             plan = None
             scan_path = "per-read (bundle layout does not fit beside the planes)"
+    if plan is not None and plan.n_bundles == 0:
+        plan = None
     if plan is not None:
         from nanotel_amd.api import DeviceBundles
         import numpy as np
-        scan_path = "bundle"
+        scan_path = "bundle" if len(plan.list) == 0 else f"bundle + per-read ({len(plan.list)} reads)"
         bread = torch.from_numpy(plan.bnd_read.view(np.int32)).to(dev)
         bstripe = torch.from_numpy(plan.bnd_stripe.view(np.int64)).to(dev)
         tpl = torch.empty(max(1, plan.tplane_bytes // 4), dtype=torch.int32, device=dev)
-        keep = [bread, bstripe, tpl]
-        bundles = DeviceBundles(tpl.data_ptr(), bread.data_ptr(), bstripe.data_ptr(), plan.n_bundles, 0, 0,
-                                plan.tplane_bytes)
+        # reads the plan leaves outside the bundles go to the per-read scan
+        blist = torch.from_numpy(plan.list.view(np.int32)).to(dev) if len(plan.list) else None
+        keep = [bread, bstripe, tpl, blist]
+        bundles = DeviceBundles(tpl.data_ptr(), bread.data_ptr(), bstripe.data_ptr(), plan.n_bundles,
+                                blist.data_ptr() if blist is not None else 0, len(plan.list), plan.tplane_bytes)
         nt.bundle_layout_device(planes.data_ptr(), blk_off.data_ptr(), lens.data_ptr(), win_off.data_ptr(),
                                 n, n * rows, bundles)
     torch.cuda.synchronize(dev)

@@ -218,6 +218,31 @@ int nt_filter_host(nt_ctx* ctx, const char* const* seqs, const uint64_t* lens, u
 int64_t nt_assign_serials(const uint8_t* is_telo, uint64_t n, double* serial_start_io,
                           double* max_serial_io, double* serial_out, int64_t* order_out);
 
+/* --- analyze_read's rows as the columns of the summary data.frame --------- */
+/* R's NA values, written where a pass found no telomere: NA_integer_ and the
+ * NA_real_ NaN (payload 1954), so a .Call shim passes INTEGER() / REAL() of
+ * its column vectors straight through. */
+#define NT_NA_INT32 ((int32_t)0x80000000)
+#define NT_NA_REAL_BITS 0x7FF00000000007A2ull
+/* The rows of one chunk, row i = read order[i] (order/rows from
+ * nt_assign_serials: the reference's group-major row order, NanoTel.R:2254),
+ * as analyze_read's columns (NanoTel.R:1820-1837, 1926-1974):
+ *   col_serial[i]  = serial[order[i]]                        Serial (double)
+ *   col_length[i]  = lens[order[i]]                          sequence_length
+ *   and per pass p < n_pass, at [p*rows + i]:
+ *   col_density / col_start / col_end / col_width (= end - start + 1)
+ *     -> telo_density, Telomere_start, Telomere_end, Telomere_length
+ *        (suffixes "", "_mismatch", "_mismatch_tvr"); all four NA when the
+ *        pass's start is -1 (NanoTel.R:1926-1940, 1956-1961).
+ * sequence_ID is the caller's names[order[i]].  start/end/density: the
+ * [n_reads*3] outputs of nt_scan_call / nt_analyze_host.  Returns rows or < 0
+ * (NT_E_ARG: an order entry >= n_reads; NT_E_LIMIT: a read >= 2^31 bases). */
+int64_t nt_rows_columns(const int32_t* start, const int32_t* end, const double* density,
+                        const uint64_t* lens, uint64_t n_reads, int32_t n_pass,
+                        const double* serial, const int64_t* order, int64_t rows,
+                        double* col_serial, int32_t* col_length, double* col_density,
+                        int32_t* col_start, int32_t* col_end, int32_t* col_width);
+
 /* --- host ingest: FASTA/FASTQ(.gz) in nrec-record chunks ------------------ */
 /* readDNAStringSet(open_input_files(path), nrec, format) (NanoTel.R:2171-2216):
  * path = a file or a directory (files listed recursively, sorted, read as one

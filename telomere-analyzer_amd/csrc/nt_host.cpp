@@ -1327,6 +1327,42 @@ int64_t nt_assign_serials(const uint8_t* is_telo, uint64_t n, double* serial_sta
   return rows;
 }
 
+int64_t nt_rows_columns(const int32_t* start, const int32_t* end, const double* density,
+                        const uint64_t* lens, uint64_t n_reads, int32_t n_pass,
+                        const double* serial, const int64_t* order, int64_t rows,
+                        double* col_serial, int32_t* col_length, double* col_density,
+                        int32_t* col_start, int32_t* col_end, int32_t* col_width) {
+  if (rows < 0 || n_pass < 1 || n_pass > NT_MAX_PASS) return NT_E_ARG;
+  if (rows == 0) return 0;
+  if (!start || !end || !density || !lens || !serial || !order || !col_serial || !col_length ||
+      !col_density || !col_start || !col_end || !col_width)
+    return NT_E_ARG;
+  double na_real;
+  const uint64_t na_bits = NT_NA_REAL_BITS;
+  std::memcpy(&na_real, &na_bits, sizeof na_real);
+  for (int64_t i = 0; i < rows; ++i) {
+    const int64_t j = order[i];
+    if (j < 0 || (uint64_t)j >= n_reads) return NT_E_ARG;
+    if (lens[j] > 0x7FFFFFFFull) return NT_E_LIMIT;
+    col_serial[i] = serial[j];
+    col_length[i] = (int32_t)lens[j];  // length(current_seq_unlist), integer
+    for (int p = 0; p < n_pass; ++p) {
+      const int64_t o = (int64_t)p * rows + i;
+      const int32_t s = start[3 * j + p], e = end[3 * j + p];
+      if (s == -1) {  // start(telo_position) == -1: NA columns (NanoTel.R:1926-1940)
+        col_density[o] = na_real;
+        col_start[o] = col_end[o] = col_width[o] = NT_NA_INT32;
+      } else {
+        col_density[o] = density[3 * j + p];
+        col_start[o] = s;
+        col_end[o] = e;
+        col_width[o] = (int32_t)((int64_t)e - s + 1);  // width(IRanges(s, e))
+      }
+    }
+  }
+  return rows;
+}
+
 static NtSynth to_synth(const nt_synth_params* sp) {
   NtSynth S;
   S.seed = sp->seed;

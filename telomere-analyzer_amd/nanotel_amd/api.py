@@ -295,3 +295,37 @@ def assign_serials(is_telo, serial_start=1.0, max_serial=float("-inf")):
                                    ser.ctypes.data, order.ctypes.data)
     _check(rows)
     return ser[:n], order[:rows], ss.value, mx.value
+
+
+NA_INT32 = -(1 << 31)  # R's NA_integer_ (NT_NA_INT32)
+NA_REAL_BITS = 0x7FF00000000007A2  # R's NA_real_ (NT_NA_REAL_BITS)
+
+
+def rows_columns(res, lengths, serials, order, n_pass):
+    """nt_rows_columns: the chunk's rows (row i = read order[i]) as the columns
+    of analyze_read's data.frame (NanoTel.R:1820-1837, 1926-1974), with R's NA
+    values where a pass found no telomere.  Returns a dict: serial (rows,)
+    float64, length (rows,) int32, density / start / end / width (n_pass, rows)
+    and na (n_pass, rows) bool."""
+    n = int(res["start"].shape[0])
+    order = np.ascontiguousarray(order, np.int64)
+    rows = int(order.size)
+    start = np.ascontiguousarray(res["start"], np.int32)
+    end = np.ascontiguousarray(res["end"], np.int32)
+    dens = np.ascontiguousarray(res["density"], np.float64)
+    lens = np.ascontiguousarray(lengths, np.uint64)
+    ser = np.ascontiguousarray(serials, np.float64)
+    assert start.shape == (n, 3) and end.shape == (n, 3) and dens.shape == (n, 3) and lens.size == n
+    out = {"serial": np.zeros(max(1, rows), np.float64), "length": np.zeros(max(1, rows), np.int32),
+           "density": np.zeros((n_pass, max(1, rows)), np.float64)}
+    for k in ("start", "end", "width"):
+        out[k] = np.zeros((n_pass, max(1, rows)), np.int32)
+    got = lib().nt_rows_columns(start.ctypes.data, end.ctypes.data, dens.ctypes.data, lens.ctypes.data, n,
+                                int(n_pass), ser.ctypes.data, order.ctypes.data, rows,
+                                out["serial"].ctypes.data, out["length"].ctypes.data, out["density"].ctypes.data,
+                                out["start"].ctypes.data, out["end"].ctypes.data, out["width"].ctypes.data)
+    _check(got)
+    for k in out:
+        out[k] = out[k][..., :rows]
+    out["na"] = out["start"] == NA_INT32
+    return out

@@ -24,7 +24,7 @@ import numpy as np
 
 from . import plots, shard
 from .analysis import write_analysis
-from .api import NanoTel
+from .api import NanoTel, rows_columns
 from .io import Reader, csv_field, format_double, format_int, r_as_character, write_fasta_gz
 
 VERSION = "Telomere Analyzer  version v1.1.9-beta 2026-02-19"
@@ -50,18 +50,19 @@ def columns(tvr):
 
 def chunk_rows(res, names, lengths, serials, order, n_pass):
     """Summary rows of one chunk in the reference's row order (analyze_read's
-    row, NanoTel.R:1920-1974): per pass start/end/length/density, NA when the
+    row, NanoTel.R:1920-1974) from the C-ABI's column builder
+    (nt_rows_columns): per pass density/start/end/length, None (NA) when the
     pass found no telomere (start == -1)."""
+    c = rows_columns(res, lengths, serials, order, n_pass)
     rows = []
-    for j in order:
-        j = int(j)
-        row = [float(serials[j]), names[j], int(lengths[j])]
+    for i, j in enumerate(order):
+        row = [float(c["serial"][i]), names[int(j)], int(c["length"][i])]
         for p in range(n_pass):
-            s, e = int(res["start"][j, p]), int(res["end"][j, p])
-            if s == -1:
+            if c["na"][p, i]:
                 row += [None, None, None, None]
             else:
-                row += [float(res["density"][j, p]), s, e, e - s + 1]
+                row += [float(c["density"][p, i]), int(c["start"][p, i]), int(c["end"][p, i]),
+                        int(c["width"][p, i])]
         rows.append(row)
     return rows
 
@@ -214,10 +215,9 @@ def run(input_path, save_path, patterns, fmt="fastq", nrec=10000, rc=False, min_
     dist_on = dist.is_available() and dist.is_initialized()
     rank = dist.get_rank() if dist_on else 0
     world = dist.get_world_size() if dist_on else 1
-    coll_dev = None  # RCCL (backend "nccl") reduces device tensors; gloo CPU ones
-    if dist_on and world > 1 and dist.get_backend() == "nccl":
-        import torch
-        coll_dev = torch.device("cuda", torch.cuda.current_device())
+    # RCCL (backend "nccl") reduces device tensors, gloo host ones: every
+    # collective below runs on coll_dev
+    coll_dev = shard.collective_device() if dist_on and world > 1 else None
     os.makedirs(save_path, exist_ok=True)
     reads_dir = os.path.join(save_path, "reads")
     os.makedirs(reads_dir, exist_ok=True)
@@ -303,7 +303,7 @@ def run(input_path, save_path, patterns, fmt="fastq", nrec=10000, rc=False, min_
         for f in pending:
             f.result()
         # the last -Inf row of the whole stream: written by the rank that holds it
-        last = shard.max_over_ranks(held[0] if held else -1)
+        last = shard.max_over_ranks(held[0] if held else -1, device=coll_dev)
         if held is not None and held[0] == last:
             name, seq, rcf = held[1]
             if write_reads:
@@ -318,7 +318,7 @@ def run(input_path, save_path, patterns, fmt="fastq", nrec=10000, rc=False, min_
     if plotters is not None:
         plotters.shutdown()
     src.close()
-    if shard.any_rank(failure is not None):
+    if shard.any_rank(failure is not None, device=coll_dev):
         rdr.close()
         nt.close()
         if failure is not None:

@@ -92,20 +92,31 @@ def exchange_rel_max(local, n_chunks, group=None, device=None, failed=False):
     return a[:n_chunks], bool(a[n_chunks] > 0.0)
 
 
-def max_over_ranks(x, group=None):
-    """max over the ranks of an integer (one all_reduce on the host)."""
+def collective_device(group=None):
+    """Where this process group's collectives reduce: a device tensor for RCCL
+    (backend "nccl" -- it refuses host tensors), None (host) for gloo."""
+    import torch
+    import torch.distributed as dist
+    if dist.is_initialized() and dist.get_backend(group) == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return None
+
+
+def max_over_ranks(x, group=None, device=None):
+    """max over the ranks of an integer (one all_reduce; on `device` for
+    RCCL, see collective_device)."""
     import torch
     import torch.distributed as dist
     if not (dist.is_initialized() and dist.get_world_size(group) > 1):
         return int(x)
-    t = torch.tensor([int(x)], dtype=torch.int64)
+    t = torch.tensor([int(x)], dtype=torch.int64, device=device if device is not None else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
     return int(t.item())
 
 
-def any_rank(flag, group=None):
+def any_rank(flag, group=None, device=None):
     """True on every rank if `flag` is true on any."""
-    return max_over_ranks(1 if flag else 0, group) > 0
+    return max_over_ranks(1 if flag else 0, group, device) > 0
 
 
 def assign_chunk_serials(rel, start):
