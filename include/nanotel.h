@@ -166,8 +166,16 @@ int nt_pack_reads(const char* const* seqs, const uint64_t* lens, uint64_t n_read
 int nt_bundle_plan(nt_ctx* ctx, const uint32_t* len, const uint8_t* has_exc, uint64_t n_reads,
                    uint32_t* bnd_read, uint64_t* bnd_stripe, uint64_t* n_bundles, uint32_t* list,
                    uint64_t* n_list, uint64_t* tplane_bytes);
-/* Device: write the T-layout (batch->tplanes, tplane_bytes from the plan) from
- * the batch's per-read planes.  Asynchronous on the context stream. */
+/* Host (ingest): write the T-layout of the planned bundles into the host
+ * buffer tplanes (tplane_bytes from the plan; every byte written) from host
+ * planes packed by nt_pack_reads -- a 32 x 32 bit transpose per 32-base block
+ * (AVX2), all host threads.  nt_analyze_host builds its batches' T-layout this
+ * way and uploads it beside the planes (no device transposer per batch). */
+int nt_bundle_layout_host(const uint32_t* planes, const uint64_t* blk_off, const uint32_t* len,
+                          const uint32_t* bnd_read, const uint64_t* bnd_stripe, uint64_t n_bundles,
+                          int32_t subseq_length, uint32_t* tplanes, uint64_t tplane_bytes);
+/* Device: the same T-layout (bit for bit) from the batch's device planes, for
+ * callers whose reads are already resident.  Asynchronous on the context stream. */
 int nt_bundle_layout(nt_ctx* ctx, const nt_batch* batch, uint32_t* tplanes, uint64_t tplane_bytes);
 
 /* --- the hot path --------------------------------------------------------- */

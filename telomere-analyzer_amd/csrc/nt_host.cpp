@@ -174,6 +174,45 @@ inline bool pack32(const unsigned char* p, uint32_t& lo, uint32_t& hi) {
   return g_avx2 ? pack32_avx2(p, lo, hi) : pack32_scalar(p, lo, hi);
 }
 
+// 32 x 32 bit transpose: y[i] bit s = x[s] bit i (32 reads' plane words of
+// one 32-base block -> the T-layout words of its 32 positions, bit s = slot s).
+// AVX2: a byte transpose of the 32 rows into 4 registers (register b, byte s
+// = byte b of x[s]: in-lane byte shuffle, dword permute, 64-bit 4x4 transpose),
+// then bit k of every byte by one shift + movemask per output word.
+__attribute__((target("avx2"))) static void transpose32_avx2(const uint32_t* x, uint32_t* y) {
+  const __m256i bsh = _mm256_setr_epi8(0, 4, 8, 12, 1, 5, 9, 13, 2, 6, 10, 14, 3, 7, 11, 15,
+                                       0, 4, 8, 12, 1, 5, 9, 13, 2, 6, 10, 14, 3, 7, 11, 15);
+  const __m256i dperm = _mm256_setr_epi32(0, 4, 1, 5, 2, 6, 3, 7);
+  __m256i B[4];
+  for (int g = 0; g < 4; ++g) {
+    // lane h, dword b = byte b of rows 8g+4h .. 8g+4h+3; then qword b = byte b of rows 8g .. 8g+7
+    const __m256i a = _mm256_shuffle_epi8(_mm256_loadu_si256((const __m256i*)(x + 8 * g)), bsh);
+    B[g] = _mm256_permutevar8x32_epi32(a, dperm);
+  }
+  const __m256i t0 = _mm256_unpacklo_epi64(B[0], B[1]), t1 = _mm256_unpackhi_epi64(B[0], B[1]);
+  const __m256i t2 = _mm256_unpacklo_epi64(B[2], B[3]), t3 = _mm256_unpackhi_epi64(B[2], B[3]);
+  const __m256i Y[4] = {_mm256_permute2x128_si256(t0, t2, 0x20), _mm256_permute2x128_si256(t1, t3, 0x20),
+                        _mm256_permute2x128_si256(t0, t2, 0x31), _mm256_permute2x128_si256(t1, t3, 0x31)};
+  for (int b = 0; b < 4; ++b) {
+    y[8 * b + 7] = (uint32_t)_mm256_movemask_epi8(Y[b]);
+    y[8 * b + 6] = (uint32_t)_mm256_movemask_epi8(_mm256_slli_epi16(Y[b], 1));
+    y[8 * b + 5] = (uint32_t)_mm256_movemask_epi8(_mm256_slli_epi16(Y[b], 2));
+    y[8 * b + 4] = (uint32_t)_mm256_movemask_epi8(_mm256_slli_epi16(Y[b], 3));
+    y[8 * b + 3] = (uint32_t)_mm256_movemask_epi8(_mm256_slli_epi16(Y[b], 4));
+    y[8 * b + 2] = (uint32_t)_mm256_movemask_epi8(_mm256_slli_epi16(Y[b], 5));
+    y[8 * b + 1] = (uint32_t)_mm256_movemask_epi8(_mm256_slli_epi16(Y[b], 6));
+    y[8 * b + 0] = (uint32_t)_mm256_movemask_epi8(_mm256_slli_epi16(Y[b], 7));
+  }
+}
+
+static void transpose32_scalar(const uint32_t* x, uint32_t* y) {
+  for (int i = 0; i < 32; ++i) {
+    uint32_t w = 0;
+    for (int s = 0; s < 32; ++s) w |= ((x[s] >> i) & 1u) << s;
+    y[i] = w;
+  }
+}
+
 // number of non-A/C/G/T bytes in s[0, n)
 static uint64_t count_non_acgt(const unsigned char* s, uint64_t n) {
   uint64_t e = 0, i = 0;
@@ -285,7 +324,7 @@ struct nt_ctx {
   // per recorded call: [0] start, [1] end of the scans (serial calling), [2]
   // end, [3 + 2k], [4 + 2k] around bundle-scan range k (overlapped calling)
   static constexpr int kMaxTsub = 16;
-  std::vector<std::array<hipEvent_t, 3 + 2 * kMaxTsub>> ev;
+  std::vector<std::array<hipEvent_t, 3 + 2 * (kMaxTsub + 1)>> ev;  // + the per-read scan of list reads
   std::vector<int> ev_nt;  // bundle-scan ranges of each recorded call
   int64_t last_launches = 0;  // scan-kernel launches of the last nt_kernel_times window
   size_t n_ev = 0;  // calls recorded since the last nt_kernel_times
@@ -308,7 +347,7 @@ struct nt_ctx {
   DevBuf planes, blk_off, len, win_off, exc_off, exc_pos, exc_code;
   DevBuf wc, start, end, dens, flags, hits, scratch, tmask, thr, queue;
   DevBuf tplanes, bnd_read, bnd_stripe, list;  // upload_reads' bundle layout
-  HostBuf h_planes, h_meta;  // upload_reads staging
+  HostBuf h_planes, h_meta, h_tplanes;  // upload_reads staging
 };
 
 static int fail(nt_ctx* ctx, int code, const std::string& msg) {
@@ -691,6 +730,10 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
   if (!out->win_counts || !out->start || !out->end || !out->density || !out->flags)
     return fail(ctx, NT_E_ARG, "win_counts/start/end/density/flags outputs are required");
   if (max_len > (1ull << 30)) return fail(ctx, NT_E_LIMIT, "read longer than 2^30 bases");
+  // win_off / n_windows count PADDED rows (multiples of 64, nt_window_rows):
+  // the aux scratch is sized from n_windows and indexed by the padded win_off
+  if (batch->n_windows % 64)
+    return fail(ctx, NT_E_ARG, "n_windows must be the sum of the padded window rows (a multiple of 64)");
   (void)hipSetDevice(ctx->device);
   const NtProgram& P = ctx->prog;
   const int np = P.n_pass, L = P.L, nh = P.n_hits;
@@ -785,7 +828,7 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
   hipEvent_t* ev = nullptr;
   if (ctx->profile) {
     if (ctx->n_ev == ctx->ev.size()) {
-      std::array<hipEvent_t, 3 + 2 * nt_ctx::kMaxTsub> a{};
+      std::array<hipEvent_t, 3 + 2 * (nt_ctx::kMaxTsub + 1)> a{};
       for (hipEvent_t& x : a)
         if ((e = hipEventCreate(&x)) != hipSuccess) return hip_fail(ctx, e, "hipEventCreate");
       ctx->ev.push_back(a);
@@ -903,6 +946,10 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
         (void)hipMemcpy(dbg, h, sizeof h, hipMemcpyHostToDevice);
       }
     }
+    // the per-read scan beside the bundle scan (its list reads): one more
+    // timed launch of the scan kernels (nt_kernel_times)
+    const int pe = (ev && tscan && n_scan > 0) ? ctx->ev_nt[ctx->n_ev - 1] : -1;
+    if (pe >= 0) (void)hipEventRecord(ev[3 + 2 * pe], ctx->stream);
     if (dbg_skip_scan || n_scan == 0)
       e = hipSuccess;
     else if (ctx->jit)
@@ -931,6 +978,10 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
                           0xFFFFFFFFu, 1u, 0u, single, 0, 0, 0, ww_g, (uint32_t*)ctx->scratch.p, (int)grid_g, 0,
                           ctx->stream);
       if (e != hipSuccess) return hip_fail(ctx, e, "launch nt_scan_kernel<global>");
+    }
+    if (pe >= 0) {
+      (void)hipEventRecord(ev[4 + 2 * pe], ctx->stream);
+      ctx->ev_nt[ctx->n_ev - 1] = pe + 1;
     }
     // one lane per (read, pass): 2 lanes per read, 4 with TVRs
     const uint64_t call_lanes = nr * (np <= 2 ? 2u : 4u);
@@ -1004,6 +1055,78 @@ int nt_bundle_plan(nt_ctx* ctx, const uint32_t* len, const uint8_t* has_exc, uin
   *n_bundles = nb;
   *n_list = nl;
   *tplane_bytes = g * stripe_bytes;
+  return NT_OK;
+}
+
+// The T-layout of one bundle on the host (nt_common.h): stripes [g0, g0 +
+// nst) of tp, every word written (zeros past a read's end and in the unused
+// half of the last row when L is odd).  Block w of the 32 slots' plane words
+// -> 32 positions; position p = block k = p / L (stripe k / 64, lane k % 64),
+// offset o = p % L (row o / 2, half o % 2).
+static void tlayout_bundle(const uint32_t* planes, const uint64_t* blk_off, const uint32_t* len,
+                           const uint32_t* slots, uint64_t g0, uint64_t nst, uint32_t L, uint32_t* tp) {
+  const uint64_t T = (L + 1) / 2;
+  uint32_t* base = tp + g0 * T * 64 * 4;
+  std::memset(base, 0, nst * T * 64 * 16);
+  uint64_t n_max = 0;
+  const uint32_t* pl[NT_BUNDLE];
+  uint64_t ln[NT_BUNDLE];
+  for (int s = 0; s < NT_BUNDLE; ++s) {
+    const uint32_t r = slots[s];
+    ln[s] = r != 0xFFFFFFFFu ? len[r] : 0;
+    pl[s] = r != 0xFFFFFFFFu ? planes + 2 * blk_off[r] : nullptr;
+    n_max = std::max(n_max, ln[s]);
+  }
+  n_max = std::min<uint64_t>(n_max, nst * 64 * L);
+  alignas(32) uint32_t xl[32], xh[32], yl[32], yh[32];
+  uint64_t k = 0, o = 0;  // block and offset of position 32 w
+  for (uint64_t w = 0; 32 * w < n_max; ++w) {
+    for (int s = 0; s < NT_BUNDLE; ++s) {
+      const int64_t nb = (int64_t)ln[s] - 32 * (int64_t)w;  // valid bases of the word
+      const uint32_t m = nb >= 32 ? ~0u : nb <= 0 ? 0u : ((1u << nb) - 1u);
+      xl[s] = m ? pl[s][2 * w] & m : 0u;
+      xh[s] = m ? pl[s][2 * w + 1] & m : 0u;
+    }
+    if (g_avx2) {
+      transpose32_avx2(xl, yl);
+      transpose32_avx2(xh, yh);
+    } else {
+      transpose32_scalar(xl, yl);
+      transpose32_scalar(xh, yh);
+    }
+    const int np = (int)std::min<uint64_t>(32, n_max - 32 * w);
+    uint64_t kk = k, oo = o;
+    for (int i = 0; i < np; ++i) {
+      uint32_t* q = base + (((kk >> 6) * T + (oo >> 1)) * 64 + (kk & 63)) * 4 + 2 * (oo & 1);
+      q[0] = yl[i];
+      q[1] = yh[i];
+      if (++oo == L) {
+        oo = 0;
+        ++kk;
+      }
+    }
+    o += 32;
+    while (o >= L) {
+      o -= L;
+      ++k;
+    }
+  }
+}
+
+int nt_bundle_layout_host(const uint32_t* planes, const uint64_t* blk_off, const uint32_t* len,
+                          const uint32_t* bnd_read, const uint64_t* bnd_stripe, uint64_t n_bundles,
+                          int32_t subseq_length, uint32_t* tplanes, uint64_t tplane_bytes) {
+  if (n_bundles == 0) return NT_OK;
+  if (!planes || !blk_off || !len || !bnd_read || !bnd_stripe || !tplanes) return NT_E_ARG;
+  if (subseq_length < 1 || subseq_length > 170) return NT_E_ARG;
+  const uint64_t L = (uint64_t)subseq_length, T = (L + 1) / 2;
+  if (bnd_stripe[n_bundles] * T * 64 * 16 > tplane_bytes) return NT_E_ARG;
+  for (uint64_t b = 0; b < n_bundles; ++b)
+    if (bnd_stripe[b + 1] < bnd_stripe[b]) return NT_E_ARG;
+  parallel_for(n_bundles, [&](uint64_t b) {
+    tlayout_bundle(planes, blk_off, len, bnd_read + NT_BUNDLE * b, bnd_stripe[b], bnd_stripe[b + 1] - bnd_stripe[b],
+                   (uint32_t)L, tplanes);
+  });
   return NT_OK;
 }
 
@@ -1151,7 +1274,8 @@ static int upload_reads(nt_ctx* ctx, const char* const* seqs, const uint64_t* le
     // the exception lists are pageable vectors: finish their copies before they go
     if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess) return hip_fail(ctx, e, "hipStreamSynchronize");
   }
-  // the bundle layout of the batch (bundle scan), built on the device
+  // the bundle layout of the batch (bundle scan): built on the host from the
+  // packed planes (ingest) and uploaded beside them
   uint64_t nb = 0, nl = 0, tpb = 0;
   std::vector<uint32_t> h_bread, h_list;
   std::vector<uint64_t> h_bstripe;
@@ -1169,10 +1293,14 @@ static int upload_reads(nt_ctx* ctx, const char* const* seqs, const uint64_t* le
     h_list.resize(nl);
   }
   if (nb) {
+    if ((e = ctx->h_tplanes.ensure(tpb)) != hipSuccess) return hip_fail(ctx, e, "hipHostMalloc(tplanes)");
+    int rc = nt_bundle_layout_host(hp, h_blk, h_len, h_bread.data(), h_bstripe.data(), nb, L,
+                                   (uint32_t*)ctx->h_tplanes.p, tpb);
+    if (rc) return fail(ctx, rc, "nt_bundle_layout_host");
+    NT_UP_PTR(tplanes, ctx->h_tplanes.p, tpb);
     NT_UP(bnd_read, h_bread);
     NT_UP(bnd_stripe, h_bstripe);
     if (nl) { NT_UP(list, h_list); }
-    if ((e = ctx->tplanes.ensure(tpb)) != hipSuccess) return hip_fail(ctx, e, "hipMalloc(tplanes)");
     // the vectors are pageable: finish their copies before they go
     if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess) return hip_fail(ctx, e, "hipStreamSynchronize");
   }
@@ -1187,10 +1315,6 @@ static int upload_reads(nt_ctx* ctx, const char* const* seqs, const uint64_t* le
                 nb ? (const uint32_t*)ctx->bnd_read.p : nullptr,
                 nb ? (const uint64_t*)ctx->bnd_stripe.p : nullptr, nb,
                 nl && nb ? (const uint32_t*)ctx->list.p : nullptr, nb ? nl : 0};
-  if (nb) {
-    const int rc = nt_bundle_layout(ctx, B, (uint32_t*)ctx->tplanes.p, tpb);
-    if (rc) return rc;
-  }
   *max_len = ml;
   return NT_OK;
 }

@@ -20,10 +20,14 @@
 //    inflates one stream on one core; the parts are independent), and parsed
 //    in order from there.  A single file is streamed.
 #include <dirent.h>
+#include <fcntl.h>
+#include <unistd.h>
 #include <sys/stat.h>
 #include <zlib.h>
 
 #include <algorithm>
+#include <atomic>
+#include <cstdio>
 #include <condition_variable>
 #include <cstdlib>
 #include <cstring>
@@ -47,7 +51,7 @@ static bool gz_failed(gzFile g) {
 // being parsed; the parser waits for its file's buffer.
 struct Prefetcher {
   struct Slot {
-    bool done = false;
+    bool done = false, plain = false;  // plain: not gzip, the parser reads it itself (parallel pread)
     std::string err;
     std::vector<char> data;
   };
@@ -75,8 +79,14 @@ struct Prefetcher {
         i = next++;
       }
       Slot sl;
-      gzFile g = gzopen((*files)[i].c_str(), "rb");
-      if (!g) {
+      unsigned char mg[2] = {0, 0};
+      if (FILE* f = std::fopen((*files)[i].c_str(), "rb")) {
+        sl.plain = std::fread(mg, 1, 2, f) != 2 || mg[0] != 0x1f || mg[1] != 0x8b;
+        std::fclose(f);
+      }
+      gzFile g = sl.plain ? nullptr : gzopen((*files)[i].c_str(), "rb");
+      if (sl.plain) {
+      } else if (!g) {
         sl.err = "cannot open " + (*files)[i];
       } else {
         gzbuffer(g, 1 << 20);
@@ -103,7 +113,7 @@ struct Prefetcher {
     }
   }
   // the inflated file i (waits for it); releases the window for one more file
-  bool take(size_t i, std::vector<char>& out, std::string& err) {
+  bool take(size_t i, std::vector<char>& out, bool& plain, std::string& err) {
     std::unique_lock<std::mutex> lk(mu);
     consumed = i + 1;
     cv.notify_all();
@@ -112,6 +122,8 @@ struct Prefetcher {
       err = slots[i].err;
       return false;
     }
+    plain = slots[i].plain;
+    if (plain) return true;
     out.swap(slots[i].data);
     std::vector<char>().swap(slots[i].data);
     return true;
@@ -128,17 +140,23 @@ struct Prefetcher {
 
 struct nt_reader {
   std::vector<std::string> files;
-  size_t file_idx = 0;
+  size_t file_idx = 0;  // next file to open
+  int format = 0;       // 0 fasta, 1 fastq
+  // the current file's bytes come from a plain descriptor (parallel pread), a
+  // gzip stream (serial inflate) or a whole file inflated ahead (Prefetcher)
+  int fd = -1;
+  uint64_t fsize = 0, foff = 0;
   gzFile gz = nullptr;
-  bool active = false;  // a file is open (streamed through gz, or inflated in buf)
+  bool active = false;   // a file is open
+  bool src_eof = true;   // no bytes of the current file beyond buf[end)
   std::unique_ptr<Prefetcher> pf;
-  int format = 0;  // 0 fasta, 1 fastq
+  // the window: bytes [pos, end) of buf not yet parsed; nl = offsets (into buf)
+  // of the '\n' in [scan, end), nl[nl_i] the first one at or after pos
   std::vector<char> buf;
-  size_t pos = 0, end = 0;
-  bool eof_file = true;
+  size_t pos = 0, end = 0, scan = 0;
+  std::vector<uint64_t> nl;
+  size_t nl_i = 0;
   std::string err;
-  std::string pending_header;  // FASTA: header already read for the next record
-  bool has_pending = false;
   // chunk storage, two slots used in turn: a chunk stays valid through the
   // next nt_reader_next call (so the caller can read chunk k+1 on another
   // thread while it still scans chunk k)
@@ -150,12 +168,38 @@ struct nt_reader {
   } store[2];
   int cur = 0;
   Store& c() { return store[cur]; }
-  bool seq_direct = false;  // FASTQ: next_record wrote the sequence into seqs_blob at seq_mark
-  size_t seq_mark = 0;
+  // records parsed from the window and not yet copied into the chunk store:
+  // name range, sequence pieces [piece0, piece1) of `pieces` (offset, length in buf)
+  struct Pend {
+    uint64_t name_at, name_len, piece0, piece1, seq_len;
+  };
+  std::vector<Pend> pend;
+  std::vector<std::pair<uint64_t, uint64_t>> pieces;
   uint64_t records_total = 0;
 };
 
 namespace {
+
+constexpr size_t kWindow0 = 64u << 20;  // window bytes (grows for a record that does not fit)
+
+unsigned host_threads() {
+  unsigned nt = std::thread::hardware_concurrency();
+  nt = std::max(1u, std::min(nt == 0 ? 1u : nt, 16u));
+  if (const char* v = std::getenv("NT_READER_PARSE_THREADS")) nt = (unsigned)std::max(1, atoi(v));
+  return nt;
+}
+
+template <class F>
+void par(unsigned n, F&& f) {
+  if (n <= 1) {
+    if (n) f(0u);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (unsigned t = 1; t < n; ++t) th.emplace_back([&f, t] { f(t); });
+  f(0u);
+  for (auto& x : th) x.join();
+}
 
 void list_files(const std::string& path, std::vector<std::string>& out) {
   DIR* d = opendir(path.c_str());
@@ -174,242 +218,342 @@ void list_files(const std::string& path, std::vector<std::string>& out) {
   closedir(d);
 }
 
-bool open_next(nt_reader* r) {
-  if (r->gz) {
-    gzclose(r->gz);
-    r->gz = nullptr;
-  }
+bool is_gzip(const std::string& path) {
+  unsigned char m[2] = {0, 0};
+  FILE* f = std::fopen(path.c_str(), "rb");
+  if (!f) return false;
+  const size_t k = std::fread(m, 1, 2, f);
+  std::fclose(f);
+  return k == 2 && m[0] == 0x1f && m[1] == 0x8b;
+}
+
+void close_source(nt_reader* r) {
+  if (r->gz) gzclose(r->gz);
+  r->gz = nullptr;
+  if (r->fd >= 0) ::close(r->fd);
+  r->fd = -1;
   r->active = false;
-  if (!r->err.empty() || r->file_idx >= r->files.size()) return false;
-  if (r->pf) {  // inflated ahead by the workers: parse straight from memory
-    if (!r->pf->take(r->file_idx++, r->buf, r->err)) return false;
+}
+
+// the '\n' offsets of buf[scan, end): parallel memchr over large ranges
+void index_lines(nt_reader* r) {
+  const size_t a = r->scan, b = r->end;
+  if (b <= a) return;
+  const char* base = r->buf.data();
+  auto scan_range = [base](size_t x, size_t y, std::vector<uint64_t>& out) {
+    const char* p = base + x;
+    const char* e = base + y;
+    while (p < e) {
+      const char* q = (const char*)memchr(p, '\n', (size_t)(e - p));
+      if (!q) break;
+      out.push_back((uint64_t)(q - base));
+      p = q + 1;
+    }
+  };
+  const unsigned nt = (b - a) >= (8u << 20) ? host_threads() : 1u;
+  if (nt == 1) {
+    scan_range(a, b, r->nl);
+  } else {
+    std::vector<std::vector<uint64_t>> part(nt);
+    par(nt, [&](unsigned t) { scan_range(a + (b - a) * t / nt, a + (b - a) * (t + 1) / nt, part[t]); });
+    for (auto& v : part) r->nl.insert(r->nl.end(), v.begin(), v.end());
+  }
+  r->scan = b;
+}
+
+// Make room and read more of the current file after buf[end): the unparsed
+// bytes [pos, end) move to the front first.  Returns false when nothing more
+// can come (end of the file, or an error).
+bool fill(nt_reader* r) {
+  if (r->src_eof || !r->active) return false;
+  // move the unparsed tail (and its line index) to the front
+  if (r->pos > 0) {
+    const size_t keep = r->end - r->pos;
+    std::memmove(r->buf.data(), r->buf.data() + r->pos, keep);
+    size_t j = 0;
+    for (size_t i = r->nl_i; i < r->nl.size(); ++i) r->nl[j++] = r->nl[i] - r->pos;
+    r->nl.resize(j);
+    r->nl_i = 0;
+    r->scan -= r->pos;
+    r->end = keep;
     r->pos = 0;
-    r->end = r->buf.size();
-    r->eof_file = true;
-    r->active = true;
-    return true;
   }
-  r->gz = gzopen(r->files[r->file_idx++].c_str(), "rb");
-  if (!r->gz) {
-    r->err = "cannot open " + r->files[r->file_idx - 1];
-    return false;
+  if (r->buf.size() < kWindow0) r->buf.resize(kWindow0);
+  if (r->end * 2 > r->buf.size()) r->buf.resize(r->buf.size() * 2);  // a record larger than half the window
+  const size_t room = r->buf.size() - r->end;
+  if (r->fd >= 0) {  // plain file: parallel pread of the next `want` bytes
+    const uint64_t want = std::min<uint64_t>(room, r->fsize - r->foff);
+    const unsigned nt = want >= (8u << 20) ? host_threads() : 1u;
+    std::atomic<bool> bad{false};
+    char* dst = r->buf.data() + r->end;
+    const uint64_t off0 = r->foff;
+    par(nt, [&](unsigned t) {
+      uint64_t x = want * t / nt;
+      const uint64_t y = want * (t + 1) / nt;
+      while (x < y) {
+        const ssize_t k = ::pread(r->fd, dst + x, (size_t)(y - x), (off_t)(off0 + x));
+        if (k <= 0) {
+          bad = true;
+          return;
+        }
+        x += (uint64_t)k;
+      }
+    });
+    if (bad) {
+      r->err = "read error in " + r->files[r->file_idx - 1];
+      r->src_eof = true;
+      return false;
+    }
+    r->foff += want;
+    r->end += want;
+    r->src_eof = r->foff >= r->fsize;
+    index_lines(r);
+    return want > 0;
   }
-  gzbuffer(r->gz, 1 << 20);
-  if (r->buf.size() != (1u << 20)) std::vector<char>(1 << 20).swap(r->buf);
-  r->pos = r->end = 0;
-  r->eof_file = false;
+  // gzip stream: serial inflate into the room
+  size_t got = 0;
+  while (got < room) {
+    const int n = gzread(r->gz, r->buf.data() + r->end + got, (unsigned)std::min<size_t>(room - got, 1u << 30));
+    if (n < 0 || (n == 0 && gz_failed(r->gz))) {  // corrupt or truncated gzip stream
+      r->err = "read error in " + r->files[r->file_idx - 1];
+      r->src_eof = true;
+      return false;
+    }
+    if (n == 0) {
+      r->src_eof = true;
+      break;
+    }
+    got += (size_t)n;
+  }
+  r->end += got;
+  index_lines(r);
+  return got > 0;
+}
+
+bool open_next(nt_reader* r) {
+  close_source(r);
+  r->pos = r->end = r->scan = 0;
+  r->nl.clear();
+  r->nl_i = 0;
+  if (!r->err.empty() || r->file_idx >= r->files.size()) return false;
+  const std::string& path = r->files[r->file_idx++];
+  if (r->pf) {  // a gzip part inflated ahead by the workers: parse straight from memory
+    bool plain = false;
+    if (!r->pf->take(r->file_idx - 1, r->buf, plain, r->err)) return false;
+    if (!plain) {
+      r->end = r->buf.size();
+      r->src_eof = true;
+      r->active = true;
+      index_lines(r);
+      return true;
+    }
+  }
+  if (!is_gzip(path)) {
+    r->fd = ::open(path.c_str(), O_RDONLY);
+    struct stat st;
+    if (r->fd < 0 || fstat(r->fd, &st) != 0) {
+      r->err = "cannot open " + path;
+      close_source(r);
+      return false;
+    }
+    r->fsize = (uint64_t)st.st_size;
+    r->foff = 0;
+  } else {
+    r->gz = gzopen(path.c_str(), "rb");
+    if (!r->gz) {
+      r->err = "cannot open " + path;
+      return false;
+    }
+    gzbuffer(r->gz, 1 << 20);
+  }
+  r->src_eof = false;
   r->active = true;
   return true;
 }
 
-// One line of the current file (without '\n' / '\r') appended to `out`
-// (nullptr: skipped, e.g. FASTQ qualities); false at end of file.  Returns the
-// line length through `len`.
-bool take_line(nt_reader* r, std::string* out, size_t* len = nullptr) {
-  if (!r->active) return false;
-  const size_t base = out ? out->size() : 0;
-  size_t n_line = 0;
-  bool any = false;
-  for (;;) {
-    if (r->pos == r->end) {
-      if (r->eof_file) break;
-      const int n = gzread(r->gz, r->buf.data(), (unsigned)r->buf.size());
-      if (n < 0 || (n == 0 && gz_failed(r->gz)))  // corrupt or truncated gzip stream
-        r->err = "read error in " + r->files[r->file_idx - 1];
-      if (n <= 0) {
-        r->eof_file = true;
+// Line cursor over the window: (p, i) = byte offset and index into nl of the
+// next '\n' at or after p.
+struct Cur {
+  size_t p, i;
+};
+
+// The next line at the cursor: [ls, le) without '\n' / '\r'.  false when the
+// window holds no complete line there: more bytes may come (need = true), or
+// the file is exhausted (need = false).  At the end of a file the last,
+// unterminated line counts when it is not empty.
+bool next_line(const nt_reader* r, Cur& c, size_t& ls, size_t& le, bool& need) {
+  need = false;
+  if (c.p >= r->end) {
+    need = !r->src_eof;
+    return false;
+  }
+  ls = c.p;
+  if (c.i < r->nl.size()) {
+    le = (size_t)r->nl[c.i];
+    c.p = le + 1;
+    ++c.i;
+  } else {
+    if (!r->src_eof) {
+      need = true;
+      return false;
+    }
+    le = r->end;
+    c.p = r->end;
+  }
+  if (le > ls && r->buf[le - 1] == '\r') --le;
+  return true;
+}
+
+// One record from the window at the committed cursor; appended to r->pend
+// (or, when lens_only, its sequence length to `len`).  Returns 1 = a record,
+// 0 = end of this file, -1 = error, 2 = incomplete (fill and retry).
+int parse_record(nt_reader* r, bool lens_only, uint64_t& len) {
+  Cur c{r->pos, r->nl_i};
+  size_t ls = 0, le = 0;
+  bool need = false;
+  const char* b = r->buf.data();
+  len = 0;
+  if (r->format == 0) {
+    uint64_t name_at = 0, name_len = 0;
+    for (;;) {  // the header (lines before the first one are skipped)
+      if (!next_line(r, c, ls, le, need)) return need ? 2 : 0;
+      if (le > ls && b[ls] == '>') break;
+    }
+    name_at = ls + 1;
+    name_len = le - ls - 1;
+    const size_t p0 = r->pieces.size();
+    for (;;) {  // sequence lines up to the next header or the end of the file
+      Cur save = c;
+      if (!next_line(r, c, ls, le, need)) {
+        if (need) {
+          r->pieces.resize(p0);
+          return 2;
+        }
         break;
       }
-      r->pos = 0;
-      r->end = (size_t)n;
+      if (le == ls || b[ls] == ';') continue;  // blank and ';' comment lines are dropped
+      if (b[ls] == '>') {
+        c = save;  // the next record's header
+        break;
+      }
+      len += le - ls;
+      if (!lens_only) r->pieces.emplace_back(ls, le - ls);
     }
-    any = true;
-    const char* b = r->buf.data() + r->pos;
-    const char* nl = (const char*)memchr(b, '\n', r->end - r->pos);
-    const size_t k = nl ? (size_t)(nl - b) : r->end - r->pos;
-    if (out) out->append(b, k);
-    n_line += k;
-    r->pos += k;
-    if (nl) {
-      ++r->pos;
-      if (out && out->size() > base && out->back() == '\r') out->pop_back(), --n_line;
-      else if (!out && k && b[k - 1] == '\r') --n_line;
-      if (len) *len = n_line;
-      return true;
-    }
+    r->pos = c.p;
+    r->nl_i = c.i;
+    if (!lens_only) r->pend.push_back({name_at, name_len, p0, r->pieces.size(), len});
+    return 1;
   }
-  if (len) *len = n_line;
-  return any && n_line > 0;
-}
-
-bool get_line(nt_reader* r, std::string& line) {
-  line.clear();
-  return take_line(r, &line);
-}
-
-void add_record(nt_reader* r, const std::string& name, const std::string& seq) {
-  r->c().name_off.push_back(r->c().names_blob.size());
-  r->c().name_len.push_back(name.size());
-  r->c().names_blob += name;
-  if (r->seq_direct) {  // FASTQ: already in the blob from seq_mark on
-    r->c().seq_len.push_back(r->c().seqs_blob.size() - r->seq_mark);
-  } else {
-    r->c().seq_off.push_back(r->c().seqs_blob.size());
-    r->c().seq_len.push_back(seq.size());
-    r->c().seqs_blob += seq;
-    return;
-  }
-  r->c().seq_off.push_back(r->seq_mark);
-}
-
-// Next record of the stream; false at the end of all files (or error).
-bool next_record(nt_reader* r, std::string& name, std::string& seq) {
-  std::string line;
-  seq.clear();
+  // FASTQ: '@' name, the sequence line, '+' line, quality lines up to the sequence's length
   for (;;) {
-    if (r->format == 0) {
-      if (!r->has_pending) {
-        // find the next header
-        bool got = false;
-        while (get_line(r, line)) {
-          if (!line.empty() && line[0] == '>') {
-            r->pending_header = line.substr(1);
-            r->has_pending = got = true;
-            break;
-          }
-        }
-        if (!got) {
-          if (!open_next(r)) return false;
-          continue;
-        }
-      }
-      name = r->pending_header;
-      r->has_pending = false;
-      while (get_line(r, line)) {
-        if (line.empty() || line[0] == ';') continue;
-        if (line[0] == '>') {
-          r->pending_header = line.substr(1);
-          r->has_pending = true;
-          break;
-        }
-        seq += line;
-      }
-      return true;
-    }
-    // FASTQ
-    bool got = false;
-    while (get_line(r, line)) {
-      if (line.empty()) continue;
-      if (line[0] != '@') {
-        r->err = "malformed FASTQ record (expected '@')";
-        return false;
-      }
-      got = true;
-      break;
-    }
-    if (!got) {
-      if (!open_next(r)) return false;
-      continue;
-    }
-    name = line.substr(1);
-    // the sequence line goes straight into the chunk's blob (seq_direct)
-    std::string plus;
-    const size_t s0 = r->c().seqs_blob.size();
-    size_t sl = 0, ql = 0, k = 0;
-    if (!take_line(r, &r->c().seqs_blob, &sl) || !get_line(r, plus) || plus.empty() || plus[0] != '+') {
-      r->c().seqs_blob.resize(s0);
-      r->err = "malformed FASTQ record '" + name + "'";
-      return false;
-    }
-    // quality may in principle wrap; skip lines until its length matches
-    while (ql < sl && take_line(r, nullptr, &k)) ql += k;
-    r->seq_mark = s0;
-    r->seq_direct = true;
-    return true;
-  }
-}
-
-// First byte of the current file's next line (refilling the buffer), -1 at
-// the end of the file.
-int peek_byte(nt_reader* r) {
-  if (!r->active) return -1;
-  if (r->pos == r->end) {
-    if (r->eof_file) return -1;
-    const int n = gzread(r->gz, r->buf.data(), (unsigned)r->buf.size());
-    if (n < 0 || (n == 0 && gz_failed(r->gz))) r->err = "read error in " + r->files[r->file_idx - 1];
-    if (n <= 0) {
-      r->eof_file = true;
+    if (!next_line(r, c, ls, le, need)) return need ? 2 : 0;
+    if (le == ls) continue;
+    if (b[ls] != '@') {
+      r->err = "malformed FASTQ record (expected '@')";
       return -1;
     }
-    r->pos = 0;
-    r->end = (size_t)n;
+    break;
   }
-  return (unsigned char)r->buf[r->pos];
-}
-
-// next_record without the copies: the record's sequence length only (the
-// same parse and the same errors; names are short and parsed into a scratch
-// string).  false at the end of all files (or error).
-bool skip_record(nt_reader* r, uint64_t& len) {
-  std::string line;
-  len = 0;
-  for (;;) {
-    if (r->format == 0) {
-      if (!r->has_pending) {
-        bool got = false;
-        while (get_line(r, line)) {
-          if (!line.empty() && line[0] == '>') {
-            r->pending_header = line.substr(1);
-            r->has_pending = got = true;
-            break;
-          }
-        }
-        if (!got) {
-          if (!open_next(r)) return false;
-          continue;
-        }
-      }
-      r->has_pending = false;
-      for (;;) {
-        const int c = peek_byte(r);
-        if (c < 0) break;
-        if (c == '>') {  // the next record's header (its name is needed if next_record reads it)
-          get_line(r, line);
-          r->pending_header = line.substr(1);
-          r->has_pending = true;
-          break;
-        }
-        size_t k = 0;
-        if (!take_line(r, nullptr, &k)) break;
-        if (c != ';') len += k;  // ';' comment lines are dropped, as next_record does
-      }
-      return true;
-    }
-    bool got = false;
-    while (get_line(r, line)) {
-      if (line.empty()) continue;
-      if (line[0] != '@') {
-        r->err = "malformed FASTQ record (expected '@')";
-        return false;
-      }
-      got = true;
+  const uint64_t name_at = ls + 1, name_len = le - ls - 1;
+  auto malformed = [&] {
+    r->err = "malformed FASTQ record '" + std::string(b + name_at, name_len) + "'";
+    return -1;
+  };
+  size_t ss = 0, se = 0;
+  if (!next_line(r, c, ss, se, need)) return need ? 2 : malformed();
+  if (!next_line(r, c, ls, le, need) || le == ls || b[ls] != '+') return need ? 2 : malformed();
+  uint64_t ql = 0;
+  const uint64_t sl = se - ss;
+  while (ql < sl) {  // quality may in principle wrap
+    if (!next_line(r, c, ls, le, need)) {
+      if (need) return 2;
       break;
     }
-    if (!got) {
-      if (!open_next(r)) return false;
+    ql += le - ls;
+  }
+  r->pos = c.p;
+  r->nl_i = c.i;
+  len = sl;
+  if (!lens_only) {
+    r->pieces.emplace_back(ss, sl);
+    r->pend.push_back({name_at, name_len, r->pieces.size() - 1, r->pieces.size(), sl});
+  }
+  return 1;
+}
+
+// Copy the pending records' names and sequences into the chunk store (all
+// host threads over the records), before the window moves.
+void flush_pending(nt_reader* r) {
+  if (r->pend.empty()) return;
+  auto& S = r->c();
+  const size_t n0 = S.name_len.size(), m = r->pend.size();
+  uint64_t nb = S.names_blob.size(), sb = S.seqs_blob.size();
+  S.name_off.resize(n0 + m);
+  S.name_len.resize(n0 + m);
+  S.seq_off.resize(n0 + m);
+  S.seq_len.resize(n0 + m);
+  for (size_t k = 0; k < m; ++k) {
+    const auto& q = r->pend[k];
+    S.name_off[n0 + k] = nb;
+    S.name_len[n0 + k] = q.name_len;
+    S.seq_off[n0 + k] = sb;
+    S.seq_len[n0 + k] = q.seq_len;
+    nb += q.name_len;
+    sb += q.seq_len;
+  }
+  S.names_blob.resize(nb);
+  S.seqs_blob.resize(sb);
+  const char* b = r->buf.data();
+  char* nd = &S.names_blob[0];
+  char* sd = &S.seqs_blob[0];
+  const uint64_t bytes = sb;
+  const unsigned nt = (bytes >= (4u << 20) && m > 1) ? std::min<unsigned>(host_threads(), (unsigned)m) : 1u;
+  par(nt, [&](unsigned t) {
+    for (size_t k = m * t / nt; k < m * (t + 1) / nt; ++k) {
+      const auto& q = r->pend[k];
+      std::memcpy(nd + S.name_off[n0 + k], b + q.name_at, q.name_len);
+      char* o = sd + S.seq_off[n0 + k];
+      for (uint64_t j = q.piece0; j < q.piece1; ++j) {
+        std::memcpy(o, b + r->pieces[j].first, r->pieces[j].second);
+        o += r->pieces[j].second;
+      }
+    }
+  });
+  r->pend.clear();
+  r->pieces.clear();
+}
+
+// Up to nrec records into the chunk store (or their lengths only); returns
+// the count, or -1 on error.
+int64_t read_records(nt_reader* r, uint64_t nrec, bool lens_only) {
+  auto& S = r->c();
+  uint64_t got = 0;
+  while (got < nrec) {
+    if (!r->active) {
+      flush_pending(r);
+      if (!open_next(r)) break;
       continue;
     }
-    const std::string name = line.substr(1);
-    std::string plus;
-    size_t sl = 0, ql = 0, k = 0;
-    if (!take_line(r, nullptr, &sl) || !get_line(r, plus) || plus.empty() || plus[0] != '+') {
-      r->err = "malformed FASTQ record '" + name + "'";
-      return false;
+    uint64_t len = 0;
+    const int k = parse_record(r, lens_only, len);
+    if (k == 1) {
+      ++got;
+      if (lens_only) S.seq_len.push_back(len);
+      continue;
     }
-    while (ql < sl && take_line(r, nullptr, &k)) ql += k;
-    len = sl;
-    return true;
+    if (k < 0) return -1;
+    if (k == 2) {  // incomplete: copy what is parsed, then read more of the file
+      flush_pending(r);
+      if (!fill(r) && !r->err.empty()) return -1;
+      continue;
+    }
+    flush_pending(r);  // k == 0: this file is done
+    if (!r->err.empty()) return -1;
+    close_source(r);
   }
+  flush_pending(r);
+  if (!r->err.empty()) return -1;
+  return (int64_t)got;
 }
 
 }  // namespace
@@ -435,8 +579,7 @@ int nt_reader_open(const char* path, int format, nt_reader** out) {
     r->files.push_back(path);
   }
   r->format = format;
-  r->buf.resize(1 << 20);
-  if (r->files.size() > 1) {  // a run directory: inflate parts ahead on worker threads
+  if (r->files.size() > 1) {  // a run directory: inflate gzip parts ahead on worker threads
     unsigned nt = std::thread::hardware_concurrency();
     nt = std::max(1u, std::min(nt == 0 ? 1u : nt, 16u));
     if (const char* v = std::getenv("NT_READER_THREADS")) nt = (unsigned)std::max(0, atoi(v));
@@ -451,7 +594,7 @@ int nt_reader_open(const char* path, int format, nt_reader** out) {
 
 void nt_reader_close(nt_reader* r) {
   if (!r) return;
-  if (r->gz) gzclose(r->gz);
+  close_source(r);
   delete r;
 }
 
@@ -463,66 +606,49 @@ const char* nt_reader_file(const nt_reader* r, uint64_t i) {
 
 const char* nt_reader_error(const nt_reader* r) { return r ? r->err.c_str() : "null reader"; }
 
+static void clear_store(nt_reader* r) {
+  r->cur ^= 1;
+  auto& S = r->c();
+  S.names_blob.clear();
+  S.seqs_blob.clear();
+  S.name_off.clear();
+  S.seq_off.clear();
+  S.name_len.clear();
+  S.seq_len.clear();
+  S.name_ptr.clear();
+  S.seq_ptr.clear();
+}
+
 int64_t nt_reader_next(nt_reader* r, uint64_t nrec, const char* const** names,
                        const uint64_t** name_lens, const char* const** seqs,
                        const uint64_t** seq_lens) {
   if (!r || !names || !name_lens || !seqs || !seq_lens || nrec == 0) return NT_E_ARG;
-  r->cur ^= 1;
-  r->c().names_blob.clear();
-  r->c().seqs_blob.clear();
-  r->c().name_off.clear();
-  r->c().seq_off.clear();
-  r->c().name_len.clear();
-  r->c().seq_len.clear();
-  if (!r->active && r->file_idx == 0 && !open_next(r)) return r->err.empty() ? 0 : NT_E_ARG;
-  std::string name, seq;
-  while (r->c().name_len.size() < nrec) {
-    r->seq_direct = false;
-    if (!next_record(r, name, seq)) {
-      if (!r->err.empty()) return NT_E_ARG;
-      break;
-    }
-    add_record(r, name, seq);
+  clear_store(r);
+  const int64_t n = read_records(r, nrec, false);
+  if (n < 0) return NT_E_ARG;
+  auto& S = r->c();
+  S.name_ptr.resize((size_t)n);
+  S.seq_ptr.resize((size_t)n);
+  for (int64_t i = 0; i < n; ++i) {
+    S.name_ptr[i] = S.names_blob.data() + S.name_off[i];
+    S.seq_ptr[i] = S.seqs_blob.data() + S.seq_off[i];
   }
-  const size_t n = r->c().name_len.size();
-  r->c().name_ptr.resize(n);
-  r->c().seq_ptr.resize(n);
-  for (size_t i = 0; i < n; ++i) {
-    r->c().name_ptr[i] = r->c().names_blob.data() + r->c().name_off[i];
-    r->c().seq_ptr[i] = r->c().seqs_blob.data() + r->c().seq_off[i];
-  }
-  *names = r->c().name_ptr.data();
-  *name_lens = r->c().name_len.data();
-  *seqs = r->c().seq_ptr.data();
-  *seq_lens = r->c().seq_len.data();
-  r->records_total += n;
-  return (int64_t)n;
+  *names = S.name_ptr.data();
+  *name_lens = S.name_len.data();
+  *seqs = S.seq_ptr.data();
+  *seq_lens = S.seq_len.data();
+  r->records_total += (uint64_t)n;
+  return n;
 }
 
 int64_t nt_reader_skip(nt_reader* r, uint64_t nrec, const uint64_t** seq_lens) {
   if (!r || !seq_lens || nrec == 0) return NT_E_ARG;
-  r->cur ^= 1;
-  r->c().names_blob.clear();
-  r->c().seqs_blob.clear();
-  r->c().name_off.clear();
-  r->c().seq_off.clear();
-  r->c().name_len.clear();
-  r->c().seq_len.clear();
-  r->c().name_ptr.clear();
-  r->c().seq_ptr.clear();
-  if (!r->active && r->file_idx == 0 && !open_next(r)) return r->err.empty() ? 0 : NT_E_ARG;
-  uint64_t len = 0;
-  while (r->c().seq_len.size() < nrec) {
-    if (!skip_record(r, len)) {
-      if (!r->err.empty()) return NT_E_ARG;
-      break;
-    }
-    r->c().seq_len.push_back(len);
-  }
-  const size_t n = r->c().seq_len.size();
+  clear_store(r);
+  const int64_t n = read_records(r, nrec, true);
+  if (n < 0) return NT_E_ARG;
   *seq_lens = r->c().seq_len.data();
-  r->records_total += n;
-  return (int64_t)n;
+  r->records_total += (uint64_t)n;
+  return n;
 }
 
 }  // extern "C"

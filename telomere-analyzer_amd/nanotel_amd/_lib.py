@@ -95,6 +95,8 @@ SIGNATURES = {
     "nt_pack_reads": (ctypes.c_int, [_P, _P, ctypes.c_uint64, ctypes.c_int32, ctypes.c_int32, _P, _P,
                                      _P, _P, _P, _P, _P]),
     "nt_bundle_plan": (ctypes.c_int, [_P, _P, _P, ctypes.c_uint64, _P, _P, _U64P, _P, _U64P, _U64P]),
+    "nt_bundle_layout_host": (ctypes.c_int, [_P, _P, _P, _P, _P, ctypes.c_uint64, ctypes.c_int32, _P,
+                                             ctypes.c_uint64]),
     "nt_bundle_layout": (ctypes.c_int, [_P, ctypes.POINTER(NtBatch), _P, ctypes.c_uint64]),
     "nt_scan_call": (ctypes.c_int, [_P, ctypes.POINTER(NtBatch), ctypes.POINTER(NtOut), ctypes.c_uint64]),
     "nt_set_profiling": (ctypes.c_int, [_P, ctypes.c_int]),

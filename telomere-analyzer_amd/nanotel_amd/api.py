@@ -239,6 +239,11 @@ class NanoTel:
                                     ctypes.byref(nl), ctypes.byref(tpb)), self._h)
         return BundlePlan(bread[:nb.value * 32], bstripe[:nb.value + 1], lst[:nl.value], tpb.value)
 
+    def bundle_layout_host(self, planes, blk_off, lengths, plan):
+        """nt_bundle_layout_host: the T-layout of a BundlePlan (host numpy
+        planes / blk_off / lengths as from nt_pack_reads) -> uint32 array."""
+        return bundle_layout_host(planes, blk_off, lengths, plan, self.subseq_length)
+
     def bundle_layout_device(self, planes, blk_off, lengths, win_off, n_reads, n_windows, bundles):
         """nt_bundle_layout: write bundles.tplanes (device) from the per-read planes."""
         B = self._batch(planes, blk_off, lengths, win_off, n_reads, n_windows, bundles=bundles)
@@ -268,6 +273,20 @@ class DeviceBundles:
     def __init__(self, tplanes, bnd_read, bnd_stripe, n_bundles, lst, n_list, tplane_bytes):
         self.tplanes, self.bnd_read, self.bnd_stripe, self.n_bundles = tplanes, bnd_read, bnd_stripe, n_bundles
         self.list, self.n_list, self.tplane_bytes = lst, n_list, tplane_bytes
+
+
+def bundle_layout_host(planes, blk_off, lengths, plan, subseq_length):
+    """nt_bundle_layout_host (no device): host T-layout of `plan`'s bundles."""
+    pl = np.ascontiguousarray(planes, np.uint32)
+    bo = np.ascontiguousarray(blk_off, np.uint64)
+    ln = np.ascontiguousarray(lengths, np.uint32)
+    br = np.ascontiguousarray(plan.bnd_read, np.uint32)
+    bs = np.ascontiguousarray(plan.bnd_stripe, np.uint64)
+    out = np.empty(max(1, plan.tplane_bytes // 4), np.uint32)
+    _check(lib().nt_bundle_layout_host(pl.ctypes.data, bo.ctypes.data, ln.ctypes.data, br.ctypes.data,
+                                       bs.ctypes.data, plan.n_bundles, int(subseq_length), out.ctypes.data,
+                                       int(plan.tplane_bytes)))
+    return out[:plan.tplane_bytes // 4]
 
 
 def synth_params(seed=20260501, first_read=0, read_len=50000, p_tract=0.5, sub_rate=0.02,

@@ -123,28 +123,36 @@ def test_cli_two_ranks_match_one(tmp_path):
     assert a == b and len(a["in_summary.csv"].splitlines()) > 5
 
 
-def test_bench_two_ranks():
-    """bench.py under torch.distributed.run with 2 ranks (weak scaling: each
-    rank scans its own reads, max-over-ranks time, whole-job value): the
-    driver's N-GPU measurement path, rehearsed on one GPU (both ranks on GPU 0,
-    host collectives, NT_BENCH_BACKEND=gloo)."""
+@pytest.mark.parametrize("launcher", ["self", "torchrun"])
+def test_bench_two_ranks(launcher):
+    """bench.py --gpus 2 (weak scaling: each rank scans its own reads,
+    max-over-ranks time, whole-job value): the driver's N-GPU measurement path,
+    rehearsed on one GPU (both ranks on GPU 0, host collectives,
+    NT_BENCH_BACKEND=gloo).  "self": run with no launcher, bench.py starts its
+    own 2 ranks; "torchrun": under torch.distributed.run, as the driver does."""
     import json
     import socket
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ, NT_BENCH_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0")
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    args = ["--steps", "3", "--warmup", "1", "--config", "c10k", "--reads", "20000", "--no-cpu-baseline"]
-    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-                        "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(root, "bench.py"),
-                        "--gpus", "2"] + args, env=env, check=True, timeout=240, capture_output=True, text=True)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    args = ["--gpus", "2", "--steps", "3", "--warmup", "1", "--config", "c10k", "--reads", "20000",
+            "--no-cpu-baseline"]
+    cmd = [sys.executable, os.path.join(root, "bench.py")] + args
+    if launcher == "torchrun":
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+        s.close()
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+               "--master-addr", "127.0.0.1", "--master-port", str(port)] + cmd[1:]
+    r = subprocess.run(cmd, env=env, check=True, timeout=240, capture_output=True, text=True)
     lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
     assert len(lines) == 1, r.stdout  # rank 0 prints the one JSON line
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["scaling"] == "weak" and d["value"] > 0
     # value = bases of both ranks / the slower rank's time
     assert abs(d["value"] - 2 * 20000 * 10000 * 3 / (d["ms_per_step"] * 3 / 1e3) / 1e9) < 0.01 * d["value"]
+

@@ -447,6 +447,63 @@ def test_full_size_bundle_scan_equals_per_read_scan(cfg):
     torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("read_len", [50000, 10000, 6450, 3001])
+def test_host_tlayout_matches_device(read_len):
+    # the T-layout the host path uploads (nt_bundle_layout_host, built at
+    # ingest) and the one the bench builds on the device (nt_bundle_layout)
+    # are the same bits, so the bench's timed step is the product's device work
+    from nanotel_amd import synth_params
+    n = 160  # 5 bundles
+    nt = _nt(patterns="TTAGGG")
+    t = _device_batch(nt, synth_params(read_len=read_len, first_read=read_len), n, read_len)
+    b, d = _device_bundles(nt, t, n, read_len)
+    plan = nt.bundle_plan(np.full(n, read_len, np.uint32))
+    host = nt.bundle_layout_host(t["planes"].cpu().numpy().view(np.uint32),
+                                 t["blk_off"].cpu().numpy().view(np.uint64),
+                                 t["lens"].cpu().numpy().view(np.uint32), plan)
+    dev = d["tplanes"].cpu().numpy().view(np.uint32)[:plan.tplane_bytes // 4]
+    assert host.shape == dev.shape
+    assert np.array_equal(host, dev), np.flatnonzero(host != dev)[:8]
+
+
+def test_host_tlayout_matches_device_mixed_lengths():
+    # ragged bundles (lengths sorted within a bundle, ends inside words),
+    # L = 37 (odd: the last row's second half holds no position)
+    import ctypes
+    import torch
+    from nanotel_amd import _lib
+    from nanotel_amd.api import DeviceBundles
+    rng = np.random.default_rng(5)
+    seqs = [bytes(rng.choice(list(b"ACGT"), int(rng.integers(1, 12000))).tolist()) for _ in range(150)]
+    L = 37
+    lib = _lib.lib()
+    n = len(seqs)
+    ptrs = (ctypes.c_char_p * n)(*seqs)
+    lens = np.array([len(x) for x in seqs], np.uint64)
+    tb, tw, te, ml, bad = (ctypes.c_uint64() for _ in range(5))
+    assert lib.nt_pack_count(ctypes.cast(ptrs, ctypes.c_void_p), lens.ctypes.data, n, L, ctypes.byref(tb),
+                             ctypes.byref(tw), ctypes.byref(te), ctypes.byref(ml), ctypes.byref(bad)) == 0
+    planes = np.zeros(2 * tb.value + 2, np.uint32)
+    blk, ln, wo = np.zeros(n, np.uint64), np.zeros(n, np.uint32), np.zeros(n, np.uint64)
+    assert lib.nt_pack_reads(ctypes.cast(ptrs, ctypes.c_void_p), lens.ctypes.data, n, 0, L, planes.ctypes.data,
+                             blk.ctypes.data, ln.ctypes.data, wo.ctypes.data, None, None, None) == 0
+    nt = _nt(patterns="TTAGGG", subseq_length=L)
+    plan = nt.bundle_plan(ln)
+    host = nt.bundle_layout_host(planes, blk, ln, plan)
+    dp = torch.from_numpy(planes.view(np.int32)).cuda()
+    dblk = torch.from_numpy(blk.view(np.int64)).cuda()
+    dln = torch.from_numpy(ln.view(np.int32)).cuda()
+    dwo = torch.from_numpy(wo.view(np.int64)).cuda()
+    br = torch.from_numpy(plan.bnd_read.view(np.int32)).cuda()
+    bs = torch.from_numpy(plan.bnd_stripe.view(np.int64)).cuda()
+    tp = torch.full((plan.tplane_bytes // 4,), -1, dtype=torch.int32, device="cuda")
+    bb = DeviceBundles(tp.data_ptr(), br.data_ptr(), bs.data_ptr(), plan.n_bundles, 0, 0, plan.tplane_bytes)
+    nt.bundle_layout_device(dp.data_ptr(), dblk.data_ptr(), dln.data_ptr(), dwo.data_ptr(), n, int(tw.value), bb)
+    nt.synchronize()
+    dev = tp.cpu().numpy().view(np.uint32)
+    assert np.array_equal(host, dev), np.flatnonzero(host != dev)[:8]
+
+
 def test_odd_block_offset_is_reported():
     from nanotel_amd import synth_params
     from nanotel_amd._lib import ROW_DONE, ROW_ERR_ALIGN
@@ -460,16 +517,20 @@ def test_odd_block_offset_is_reported():
     assert all((f[i] & ROW_ERR_ALIGN) == 0 for i in range(n) if i != 3)
 
 
-@pytest.mark.parametrize("jit", [True, False], ids=["jit", "aot"])
-def test_offsets_beyond_32_bits(jit):
+@pytest.mark.parametrize("path", ["jit", "aot", "bundle"])
+def test_offsets_beyond_32_bits(path):
     # Batches of 10M x 50 kb reads have block offsets >= 2^31 and window
-    # offsets >= 2^32 (a sign-extended 32-bit block offset once faulted there).
-    # Reproduced without allocating them: the planes / window-count base
-    # pointers are shifted down by exactly the offsets added to blk_off / win_off.
+    # offsets >= 2^32 (a sign-extended 32-bit block offset once faulted there),
+    # and their T-layout word offsets pass 2^32.  Reproduced without
+    # allocating them: the planes / window-count / T-layout base pointers are
+    # shifted down by exactly the offsets added to blk_off / win_off /
+    # bnd_stripe.  Bundle path: the bundle scan reads the shifted T-layout, the
+    # calling kernel the shifted planes.
     import torch
     from nanotel_amd import synth_params
-    n, read_len = 64, 50000
-    nt = _nt(jit=jit, patterns="TTAGGG")
+    from nanotel_amd.api import DeviceBundles
+    n, read_len = 64 if path != "bundle" else 96, 50000
+    nt = _nt(jit=path != "aot", patterns="TTAGGG")
     t = _device_batch(nt, synth_params(read_len=read_len, first_read=77), n, read_len)
     _run_device(nt, t, n, read_len)
     keys = ("start", "end", "dens", "flags", "wc")
@@ -478,12 +539,26 @@ def test_offsets_beyond_32_bits(jit):
         t[k].zero_()
     boff, woff = 1 << 31, 1 << 32  # blocks of 8 bytes, windows
     blk, win = t["blk_off"] + boff, t["win_off"] + woff
+    bundles, keep = None, None
+    if path == "bundle":
+        b, keep = _device_bundles(nt, t, n, read_len)
+        stripe_bytes = 50 * 64 * 16
+        soff = (1 << 35) // stripe_bytes + 1  # stripes: T-layout offsets past 2^35 bytes (2^33 words)
+        bs = keep["bnd_stripe"] + soff
+        bundles = DeviceBundles(b.tplanes - soff * stripe_bytes, b.bnd_read, bs.data_ptr(), b.n_bundles, 0, 0,
+                                b.tplane_bytes)
+        keep["bs_shift"] = bs
     nt.scan_call_device(t["planes"].data_ptr() - boff * 8, blk.data_ptr(), t["lens"].data_ptr(), win.data_ptr(),
                         n, woff + n * t["rows"], read_len, t["start"].data_ptr(), t["end"].data_ptr(),
-                        t["dens"].data_ptr(), t["flags"].data_ptr(), t["wc"].data_ptr() - woff * nt.n_pass * nt.count_bytes)
+                        t["dens"].data_ptr(), t["flags"].data_ptr(), t["wc"].data_ptr() - woff * nt.n_pass * nt.count_bytes,
+                        bundles=bundles)
     nt.synchronize()
     for k in keys:
-        assert torch.equal(t[k], ref[k]), k
+        if k == "wc":
+            assert torch.equal(_valid_counts(t, n, nt.n_pass), _valid_counts(t, n, nt.n_pass, ref[k])), k
+        else:
+            assert torch.equal(t[k], ref[k]), k
+    del keep
 
 
 @pytest.mark.parametrize("jit", [True, False], ids=["jit", "aot"])
