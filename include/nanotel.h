@@ -196,9 +196,19 @@ int64_t nt_kernel_times(nt_ctx* ctx, double* scan_ms, double* call_ms);
  * nt_kernel_times: scan_ms / this = the scan kernel's average launch. */
 int64_t nt_kernel_launches(const nt_ctx* ctx);
 /* 1 if the last nt_scan_call ran the calling kernel specialised for the
- * program's patterns (hiprtc, built on the first batch of >= 65,536 reads, or
+ * program's patterns (hiprtc; batches of >= 65,536 reads once it is built,
  * every batch with NT_CALL_JIT=1), 0 for the ahead-of-time one (same results). */
 int nt_call_jit_state(const nt_ctx* ctx);
+/* The first batch of >= 65,536 reads starts the hiprtc build of that
+ * specialised calling kernel on a background thread (seconds; code objects are
+ * kept in an on-disk cache, NT_JIT_CACHE); until it is done large batches run
+ * the ahead-of-time kernel.  This starts it if need be and waits for it:
+ * 1 = built, 0 = unavailable (the ahead-of-time kernel serves). */
+int nt_call_jit_wait(nt_ctx* ctx);
+/* Host only (no device): compile the kernels specialised for a parameter set
+ * into the on-disk code-object cache (arch: "gfx950"), so that a later
+ * nt_compile / first large batch loads them instead of running hiprtc. */
+int nt_jit_prebuild(const nt_params* params, const char* arch);
 
 /* Host-buffer convenience: pack (+rc), upload, scan+call, download, sync.
  * win_counts/hits optional.  Returns the first per-read error, if any. */
@@ -255,9 +265,10 @@ int64_t nt_rows_columns(const int32_t* start, const int32_t* end, const double* 
 /* readDNAStringSet(open_input_files(path), nrec, format) (NanoTel.R:2171-2216):
  * path = a file or a directory (files listed recursively, sorted, read as one
  * record stream); format 0 = fasta, 1 = fastq; gzip transparent.  A chunk's
- * names/sequences stay valid through the next nt_reader_next call (two
- * buffers in turn: chunk k+1 may be read while chunk k is scanned) and until
- * the one after it, or close.
+ * names/sequences stay valid through the next nt_reader_next call (chunk k+1
+ * may be read while chunk k is scanned; nt_reader_keep for more), or close.
+ * Plain files are mapped and records point into them (no copies); gzip input
+ * is inflated into shared windows; wrapped FASTA sequences are joined.
  * Returns the number of records (0 at the end) or < 0 (nt_reader_error). */
 typedef struct nt_reader nt_reader;
 int nt_reader_open(const char* path, int format, nt_reader** out);
@@ -270,8 +281,13 @@ int64_t nt_reader_next(nt_reader* r, uint64_t nrec, const char* const** names,
                        const uint64_t** seq_lens);
 /* The next nrec records without copying them (a multi-GPU rank passing over
  * the chunks other ranks scan): the same parse and errors as nt_reader_next,
- * only the sequence lengths are kept (valid as nt_reader_next's arrays). */
+ * only the sequence lengths are kept (valid through the next nt_reader_skip;
+ * a skip does not retire an nt_reader_next chunk). */
 int64_t nt_reader_skip(nt_reader* r, uint64_t nrec, const uint64_t** seq_lens);
+/* Keep the last `chunks` chunks valid (default 2, i.e. a chunk stays valid
+ * through the next call): a caller that scans several chunks in one device
+ * call holds them all.  Only grows. */
+int nt_reader_keep(nt_reader* r, uint32_t chunks);
 
 /* --- synthetic long reads (bench / tests) --------------------------------- */
 int nt_synth_device(nt_ctx* ctx, const nt_synth_params* sp, uint64_t n_reads, uint32_t* planes_dev);

@@ -7,10 +7,12 @@
 #include <algorithm>
 #include <array>
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <future>
 #include <string>
 #include <thread>
 #include <vector>
@@ -49,6 +51,7 @@ bool nt_tscan_eligible(const NtProgram& P);
 hipError_t nt_tjit_launch(void* fn, int grid, hipStream_t stream, const NtBatch* B, const NtOut* O,
                           uint64_t* tmask, unsigned long long* queue, uint32_t thr_full);
 void* nt_cjit_get(int device, const NtProgram& P, std::string& err);
+int nt_jit_prebuild_program(const NtProgram& P, const std::string& arch);
 hipError_t nt_cjit_launch(void* fn, int grid, hipStream_t stream, const NtProgram* prog, const NtBatch* B,
                           const NtOut* O, const uint64_t* tmask, const uint32_t* thr, uint32_t thr_size,
                           int fix_last);
@@ -338,6 +341,8 @@ struct nt_ctx {
   // built on the first batch that uses it; null: the ahead-of-time kernel
   void* cjit_fn = nullptr;
   bool cjit_tried = false;
+  // its build, started in the background by nt_compile (hiprtc, or the disk cache)
+  std::future<std::pair<void*, std::string>> cjit_build;
   int cjit_last = 0;  // the last nt_scan_call launched it
   std::string cjit_err;
   NtProgram prog{};
@@ -363,14 +368,43 @@ static int fail(nt_ctx* ctx, int code, const std::string& msg) {
 // NT_CALL_JIT=1 uses it for every batch, NT_CALL_JIT=0 never.
 constexpr uint64_t kCallJitMinReads = 1u << 16;
 
-static void* call_jit_fn(nt_ctx* ctx, uint64_t n_reads) {
+static int call_jit_mode() {
   const char* v = std::getenv("NT_CALL_JIT");
-  const int mode = v ? std::atoi(v) : -1;
-  if (mode == 0 || !ctx->jit || (mode < 0 && n_reads < kCallJitMinReads)) return nullptr;
-  if (!ctx->cjit_tried) {
-    ctx->cjit_fn = nt_cjit_get(ctx->device, ctx->prog, ctx->cjit_err);
-    ctx->cjit_tried = true;
+  return v ? std::atoi(v) : -1;
+}
+
+// The specialised calling kernel of the program: its build (hiprtc, or the
+// on-disk code-object cache) runs on a background thread, started by the first
+// batch that would use it; returns false while it runs (waits when `wait`).
+static bool cjit_collect(nt_ctx* ctx, bool wait) {
+  if (ctx->cjit_tried) return true;
+  if (!ctx->cjit_build.valid()) {
+    const int dev = ctx->device;
+    const NtProgram prog = ctx->prog;
+    ctx->cjit_build = std::async(std::launch::async, [dev, prog]() {
+      (void)hipSetDevice(dev);  // the module loads on this thread's device
+      std::string err;
+      void* fn = nt_cjit_get(dev, prog, err);
+      return std::make_pair(fn, err);
+    });
   }
+  if (!wait && ctx->cjit_build.wait_for(std::chrono::seconds(0)) != std::future_status::ready) return false;
+  auto r = ctx->cjit_build.get();
+  ctx->cjit_fn = r.first;
+  ctx->cjit_err = r.second;
+  ctx->cjit_tried = true;
+  return true;
+}
+
+// Default: batches of >= kCallJitMinReads reads take the specialised kernel
+// once its background build (started by the first of them) is done -- until then,
+// and for smaller batches, the ahead-of-time kernel (same results; no call
+// ever waits for hiprtc).  NT_CALL_JIT=1: every batch, waiting for the build;
+// NT_CALL_JIT=0: never.
+static void* call_jit_fn(nt_ctx* ctx, uint64_t n_reads) {
+  const int mode = call_jit_mode();
+  if (mode == 0 || !ctx->jit || (mode < 0 && n_reads < kCallJitMinReads)) return nullptr;
+  if (!cjit_collect(ctx, mode > 0)) return nullptr;
   return ctx->cjit_fn;
 }
 
@@ -422,6 +456,7 @@ int nt_create(int device, nt_ctx** out) {
 
 void nt_destroy(nt_ctx* ctx) {
   if (!ctx) return;
+  if (ctx->cjit_build.valid()) ctx->cjit_build.wait();
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->call_stream) (void)hipStreamSynchronize(ctx->call_stream);
@@ -454,31 +489,31 @@ uint64_t nt_window_rows(int64_t nw) { return nw <= 0 ? 0 : NT_WIN_ROWS((uint64_t
 
 uint64_t nt_read_blocks(uint64_t n) { return read_blocks(n); }
 
-int nt_compile(nt_ctx* ctx, const nt_params* prm, nt_program_info* info) {
-  if (!ctx || !prm) return NT_E_ARG;
-  if (!prm->patterns) return fail(ctx, NT_E_ARG, "Missing required parameter:  --patterns");
-  if (prm->subseq_length <= 0) return fail(ctx, NT_E_ARG, "--subseq_length must be >= 1");
+// The program of a parameter set (host only): patterns, passes, the divisor
+// magic and the telomeric threshold table.
+static int make_program(const nt_params* prm, NtProgram& P, std::vector<uint32_t>& thr, std::string& err) {
+  if (!prm) return NT_E_ARG;
+  if (!prm->patterns) { err = "Missing required parameter:  --patterns"; return NT_E_ARG; }
+  if (prm->subseq_length <= 0) { err = "--subseq_length must be >= 1"; return NT_E_ARG; }
   if (prm->subseq_length > 43690)
-    return fail(ctx, NT_E_LIMIT, "--subseq_length > 43690 overflows the uint16 window counts");
-  NtProgram P;
+    { err = "--subseq_length > 43690 overflows the uint16 window counts"; return NT_E_LIMIT; }
   std::memset(&P, 0, sizeof P);
   std::vector<std::string> pats, tvrs;
   bool pat_list = false, tvr_list = false;
-  std::string err;
   int rc = parse_tokens(prm->patterns, pats, pat_list, err);
-  if (rc) return fail(ctx, rc, err);
-  if (pats.size() > NT_MAX_PAT) return fail(ctx, NT_E_LIMIT, "more than 8 unique patterns");
+  if (rc) return rc;
+  if (pats.size() > NT_MAX_PAT) { err = "more than 8 unique patterns"; return NT_E_LIMIT; }
   for (size_t i = 0; i < pats.size(); ++i) {
     rc = build_pat(pats[i], NT_MAX_M, P.pat[i], err);
-    if (rc) return fail(ctx, rc, err);
+    if (rc) return rc;
   }
   if (prm->tvr_patterns) {
     rc = parse_tokens(prm->tvr_patterns, tvrs, tvr_list, err);
-    if (rc) return fail(ctx, rc, err);
-    if (tvrs.size() > NT_MAX_PAT) return fail(ctx, NT_E_LIMIT, "more than 8 unique TVR patterns");
+    if (rc) return rc;
+    if (tvrs.size() > NT_MAX_PAT) { err = "more than 8 unique TVR patterns"; return NT_E_LIMIT; }
     for (size_t i = 0; i < tvrs.size(); ++i) {
       rc = build_pat(tvrs[i], NT_MAX_TVR_M, P.tvr[i], err);
-      if (rc) return fail(ctx, rc, err);
+      if (rc) return rc;
     }
   }
   P.n_pat = (int32_t)pats.size();
@@ -500,7 +535,7 @@ int nt_compile(nt_ctx* ctx, const nt_params* prm, nt_program_info* info) {
     // 32-bit form for p < 2^31: M = floor(2^(31+l) / L) + 1 < 2^32, error < 2^-l <= 1/L
     if (P.L >= 2) {
       const uint64_t m32 = ((1ull << (31 + l)) / (uint64_t)P.L) + 1;
-      if (m32 > 0xFFFFFFFFull) return fail(ctx, NT_E_LIMIT, "divisor magic overflow");
+      if (m32 > 0xFFFFFFFFull) { err = "divisor magic overflow"; return NT_E_LIMIT; }
       P.div32_m = (uint32_t)m32;
       P.div32_s = l - 1;
     } else {
@@ -512,7 +547,7 @@ int nt_compile(nt_ctx* ctx, const nt_params* prm, nt_program_info* info) {
   // fl(c / w) is monotone in c, so the class is count >= thr[w] with thr[w]
   // the smallest such count -- found here with the very fp64 division R does.
   const uint32_t wmax = (uint32_t)P.L + (uint32_t)(P.L + 1) / 2 + 1;
-  std::vector<uint32_t> thr(wmax + 1, 0);
+  thr.assign(wmax + 1, 0);
   for (uint32_t w = 1; w <= wmax; ++w) {
     uint32_t c = 0;
     while (c <= w && ((double)c / (double)w < P.min_density)) ++c;
@@ -538,6 +573,16 @@ int nt_compile(nt_ctx* ctx, const nt_params* prm, nt_program_info* info) {
       X.xh[j] = (c & 2u) ? 0u : 0xFFFFFFFFu;
     }
   }
+  return NT_OK;
+}
+
+int nt_compile(nt_ctx* ctx, const nt_params* prm, nt_program_info* info) {
+  if (!ctx || !prm) return NT_E_ARG;
+  NtProgram P;
+  std::vector<uint32_t> thr;
+  std::string err;
+  const int rc = make_program(prm, P, thr, err);
+  if (rc) return fail(ctx, rc, err);
   (void)hipSetDevice(ctx->device);
   hipError_t e = hipMemcpy(ctx->prog_dev, &P, sizeof P, hipMemcpyHostToDevice);
   if (e != hipSuccess) return hip_fail(ctx, e, "hipMemcpy(program)");
@@ -549,6 +594,8 @@ int nt_compile(nt_ctx* ctx, const nt_params* prm, nt_program_info* info) {
   ctx->params = *prm;
   ctx->compiled = true;
   ctx->jit = nt_jit_get(ctx->device, P, ctx->jit_fn, &ctx->tjit_fn, ctx->jit_err);
+  if (ctx->cjit_build.valid()) ctx->cjit_build.wait();  // a previous program's build
+  ctx->cjit_build = {};
   ctx->cjit_fn = nullptr;
   ctx->cjit_tried = false;
   ctx->tscan_bpc = 0;
@@ -1147,6 +1194,23 @@ int nt_bundle_layout(nt_ctx* ctx, const nt_batch* batch, uint32_t* tplanes, uint
 }
 
 int nt_call_jit_state(const nt_ctx* ctx) { return ctx ? ctx->cjit_last : 0; }
+
+int nt_jit_prebuild(const nt_params* params, const char* arch) {
+  NtProgram P;
+  std::vector<uint32_t> thr;
+  std::string err;
+  const int rc = make_program(params, P, thr, err);
+  if (rc) return rc;
+  return nt_jit_prebuild_program(P, arch ? arch : "gfx950");
+}
+
+int nt_call_jit_wait(nt_ctx* ctx) {
+  if (!ctx) return NT_E_ARG;
+  if (!ctx->compiled) return fail(ctx, NT_E_STATE, "nt_compile() not called");
+  if (!ctx->jit || call_jit_mode() == 0) return 0;
+  cjit_collect(ctx, true);
+  return ctx->cjit_fn ? 1 : 0;
+}
 
 int64_t nt_kernel_launches(const nt_ctx* ctx) { return ctx ? ctx->last_launches : NT_E_ARG; }
 

@@ -21,6 +21,7 @@
 //    in order from there.  A single file is streamed.
 #include <dirent.h>
 #include <fcntl.h>
+#include <sys/mman.h>
 #include <unistd.h>
 #include <sys/stat.h>
 #include <zlib.h>
@@ -138,49 +139,67 @@ struct Prefetcher {
   }
 };
 
+// A buffer records point into: an inflated file or stream window (owned
+// bytes) or a read-only mapping of a plain file.  Shared: the chunk stores
+// that hold pointers into a buffer keep it alive (a chunk stays valid through
+// the next nt_reader_next call).
+struct RBuf {
+  std::vector<char> own;
+  void* map = nullptr;
+  size_t map_len = 0;
+  const char* data = nullptr;
+  size_t size = 0;
+  ~RBuf() {
+    if (map) munmap(map, map_len);
+  }
+};
+
 struct nt_reader {
   std::vector<std::string> files;
   size_t file_idx = 0;  // next file to open
   int format = 0;       // 0 fasta, 1 fastq
-  // the current file's bytes come from a plain descriptor (parallel pread), a
-  // gzip stream (serial inflate) or a whole file inflated ahead (Prefetcher)
-  int fd = -1;
-  uint64_t fsize = 0, foff = 0;
+  // the current file's bytes: a mapping of the whole plain file, a whole gzip
+  // part inflated ahead (Prefetcher), or windows of a gzip stream (serial inflate)
   gzFile gz = nullptr;
   bool active = false;   // a file is open
-  bool src_eof = true;   // no bytes of the current file beyond buf[end)
+  bool src_eof = true;   // no bytes of the current file beyond win[end)
   std::unique_ptr<Prefetcher> pf;
-  // the window: bytes [pos, end) of buf not yet parsed; nl = offsets (into buf)
-  // of the '\n' in [scan, end), nl[nl_i] the first one at or after pos
-  std::vector<char> buf;
+  // the window: bytes [pos, end) of win not yet parsed; nl = offsets of the
+  // '\n' in [pos, scan) (indexed lazily, in slices), nl[nl_i] the first one at
+  // or after pos
+  std::shared_ptr<RBuf> win;
   size_t pos = 0, end = 0, scan = 0;
   std::vector<uint64_t> nl;
   size_t nl_i = 0;
   std::string err;
   // chunk storage, two slots used in turn: a chunk stays valid through the
   // next nt_reader_next call (so the caller can read chunk k+1 on another
-  // thread while it still scans chunk k)
+  // thread while it still scans chunk k).  Names and single-line sequences
+  // point into the buffers (refs); multi-line FASTA sequences are joined in
+  // seqs_blob (seq_off = blob offset, marked by seq_blob).
   struct Store {
-    std::string names_blob, seqs_blob;
-    std::vector<uint64_t> name_off, seq_off;
+    std::string seqs_blob;
+    std::vector<uint64_t> seq_off;
+    std::vector<uint8_t> seq_blob;
     std::vector<const char*> name_ptr, seq_ptr;
     std::vector<uint64_t> name_len, seq_len;
-  } store[2];
-  int cur = 0;
-  Store& c() { return store[cur]; }
-  // records parsed from the window and not yet copied into the chunk store:
-  // name range, sequence pieces [piece0, piece1) of `pieces` (offset, length in buf)
-  struct Pend {
-    uint64_t name_at, name_len, piece0, piece1, seq_len;
+    std::vector<std::shared_ptr<RBuf>> refs;
   };
-  std::vector<Pend> pend;
+  std::vector<Store> store = std::vector<Store>(2);  // a ring: the last store.size() chunks stay valid
+  size_t cur = 0;
+  Store& c() { return store[cur]; }
+  // nt_reader_skip's lengths (two in turn: valid through the next skip call;
+  // skips do not take a chunk store)
+  std::vector<uint64_t> skip_len[2];
+  int skip_cur = 0;
+  // the current record's multi-line FASTA pieces (offset, length in win)
   std::vector<std::pair<uint64_t, uint64_t>> pieces;
   uint64_t records_total = 0;
 };
 
 namespace {
 
-constexpr size_t kWindow0 = 64u << 20;  // window bytes (grows for a record that does not fit)
+constexpr size_t kWindow = 64u << 20;  // gzip stream window / index slice (grows for a larger record)
 
 unsigned host_threads() {
   unsigned nt = std::thread::hardware_concurrency();
@@ -230,16 +249,20 @@ bool is_gzip(const std::string& path) {
 void close_source(nt_reader* r) {
   if (r->gz) gzclose(r->gz);
   r->gz = nullptr;
-  if (r->fd >= 0) ::close(r->fd);
-  r->fd = -1;
   r->active = false;
 }
 
-// the '\n' offsets of buf[scan, end): parallel memchr over large ranges
-void index_lines(nt_reader* r) {
-  const size_t a = r->scan, b = r->end;
-  if (b <= a) return;
-  const char* base = r->buf.data();
+// Index the '\n' of the next slice of the window, [scan, scan + kWindow) or
+// to its end: parallel memchr (which also faults a mapping's pages in on all
+// host threads).  Returns false when the window is indexed to its end.
+bool index_more(nt_reader* r) {
+  const size_t a = r->scan, b = std::min(r->end, r->scan + kWindow);
+  if (b <= a) return false;
+  if (r->nl_i > 0) {  // drop the consumed entries
+    r->nl.erase(r->nl.begin(), r->nl.begin() + (ptrdiff_t)r->nl_i);
+    r->nl_i = 0;
+  }
+  const char* base = r->win->data;
   auto scan_range = [base](size_t x, size_t y, std::vector<uint64_t>& out) {
     const char* p = base + x;
     const char* e = base + y;
@@ -250,7 +273,7 @@ void index_lines(nt_reader* r) {
       p = q + 1;
     }
   };
-  const unsigned nt = (b - a) >= (8u << 20) ? host_threads() : 1u;
+  const unsigned nt = (b - a) >= (4u << 20) ? host_threads() : 1u;
   if (nt == 1) {
     scan_range(a, b, r->nl);
   } else {
@@ -259,61 +282,24 @@ void index_lines(nt_reader* r) {
     for (auto& v : part) r->nl.insert(r->nl.end(), v.begin(), v.end());
   }
   r->scan = b;
+  return true;
 }
 
-// Make room and read more of the current file after buf[end): the unparsed
-// bytes [pos, end) move to the front first.  Returns false when nothing more
-// can come (end of the file, or an error).
-bool fill(nt_reader* r) {
+// More of the current file: index the window further, or (gzip stream)
+// inflate the next window -- a new buffer that starts with the unparsed
+// bytes [pos, end) (records of the current chunk may point into the old
+// one).  Returns false when nothing more can come (end of file, or error).
+bool more(nt_reader* r) {
+  if (r->scan < r->end) return index_more(r);
   if (r->src_eof || !r->active) return false;
-  // move the unparsed tail (and its line index) to the front
-  if (r->pos > 0) {
-    const size_t keep = r->end - r->pos;
-    std::memmove(r->buf.data(), r->buf.data() + r->pos, keep);
-    size_t j = 0;
-    for (size_t i = r->nl_i; i < r->nl.size(); ++i) r->nl[j++] = r->nl[i] - r->pos;
-    r->nl.resize(j);
-    r->nl_i = 0;
-    r->scan -= r->pos;
-    r->end = keep;
-    r->pos = 0;
-  }
-  if (r->buf.size() < kWindow0) r->buf.resize(kWindow0);
-  if (r->end * 2 > r->buf.size()) r->buf.resize(r->buf.size() * 2);  // a record larger than half the window
-  const size_t room = r->buf.size() - r->end;
-  if (r->fd >= 0) {  // plain file: parallel pread of the next `want` bytes
-    const uint64_t want = std::min<uint64_t>(room, r->fsize - r->foff);
-    const unsigned nt = want >= (8u << 20) ? host_threads() : 1u;
-    std::atomic<bool> bad{false};
-    char* dst = r->buf.data() + r->end;
-    const uint64_t off0 = r->foff;
-    par(nt, [&](unsigned t) {
-      uint64_t x = want * t / nt;
-      const uint64_t y = want * (t + 1) / nt;
-      while (x < y) {
-        const ssize_t k = ::pread(r->fd, dst + x, (size_t)(y - x), (off_t)(off0 + x));
-        if (k <= 0) {
-          bad = true;
-          return;
-        }
-        x += (uint64_t)k;
-      }
-    });
-    if (bad) {
-      r->err = "read error in " + r->files[r->file_idx - 1];
-      r->src_eof = true;
-      return false;
-    }
-    r->foff += want;
-    r->end += want;
-    r->src_eof = r->foff >= r->fsize;
-    index_lines(r);
-    return want > 0;
-  }
-  // gzip stream: serial inflate into the room
-  size_t got = 0;
-  while (got < room) {
-    const int n = gzread(r->gz, r->buf.data() + r->end + got, (unsigned)std::min<size_t>(room - got, 1u << 30));
+  const size_t keep = r->end - r->pos;
+  size_t cap = std::max(kWindow, 2 * keep);
+  auto nb = std::make_shared<RBuf>();
+  nb->own.resize(cap);
+  if (keep) std::memcpy(nb->own.data(), r->win->data + r->pos, keep);
+  size_t got = keep;
+  while (got < cap) {
+    const int n = gzread(r->gz, nb->own.data() + got, (unsigned)std::min<size_t>(cap - got, 1u << 30));
     if (n < 0 || (n == 0 && gz_failed(r->gz))) {  // corrupt or truncated gzip stream
       r->err = "read error in " + r->files[r->file_idx - 1];
       r->src_eof = true;
@@ -325,47 +311,73 @@ bool fill(nt_reader* r) {
     }
     got += (size_t)n;
   }
-  r->end += got;
-  index_lines(r);
-  return got > 0;
+  nb->data = nb->own.data();
+  nb->size = got;
+  for (size_t i = r->nl_i; i < r->nl.size(); ++i) r->nl[i] -= r->pos;
+  r->scan -= r->pos;
+  r->win = nb;
+  r->end = got;
+  r->pos = 0;
+  return got > keep;
 }
 
 bool open_next(nt_reader* r) {
   close_source(r);
+  r->win.reset();
   r->pos = r->end = r->scan = 0;
   r->nl.clear();
   r->nl_i = 0;
   if (!r->err.empty() || r->file_idx >= r->files.size()) return false;
   const std::string& path = r->files[r->file_idx++];
+  auto b = std::make_shared<RBuf>();
   if (r->pf) {  // a gzip part inflated ahead by the workers: parse straight from memory
     bool plain = false;
-    if (!r->pf->take(r->file_idx - 1, r->buf, plain, r->err)) return false;
+    if (!r->pf->take(r->file_idx - 1, b->own, plain, r->err)) return false;
     if (!plain) {
-      r->end = r->buf.size();
+      b->data = b->own.data();
+      b->size = b->own.size();
+      r->win = b;
+      r->end = b->size;
       r->src_eof = true;
       r->active = true;
-      index_lines(r);
       return true;
     }
   }
-  if (!is_gzip(path)) {
-    r->fd = ::open(path.c_str(), O_RDONLY);
+  if (!is_gzip(path)) {  // a plain file: mapped whole (no copy; pages fault in during the index)
+    const int fd = ::open(path.c_str(), O_RDONLY);
     struct stat st;
-    if (r->fd < 0 || fstat(r->fd, &st) != 0) {
-      r->err = "cannot open " + path;
-      close_source(r);
-      return false;
-    }
-    r->fsize = (uint64_t)st.st_size;
-    r->foff = 0;
-  } else {
-    r->gz = gzopen(path.c_str(), "rb");
-    if (!r->gz) {
+    if (fd < 0 || fstat(fd, &st) != 0) {
+      if (fd >= 0) ::close(fd);
       r->err = "cannot open " + path;
       return false;
     }
-    gzbuffer(r->gz, 1 << 20);
+    if (st.st_size > 0) {
+      void* m = mmap(nullptr, (size_t)st.st_size, PROT_READ, MAP_PRIVATE, fd, 0);
+      if (m == MAP_FAILED) {
+        ::close(fd);
+        r->err = "cannot map " + path;
+        return false;
+      }
+      (void)madvise(m, (size_t)st.st_size, MADV_SEQUENTIAL);
+      b->map = m;
+      b->map_len = (size_t)st.st_size;
+      b->data = (const char*)m;
+      b->size = (size_t)st.st_size;
+    }
+    ::close(fd);
+    r->win = b;
+    r->end = b->size;
+    r->src_eof = true;
+    r->active = true;
+    return true;
   }
+  r->gz = gzopen(path.c_str(), "rb");
+  if (!r->gz) {
+    r->err = "cannot open " + path;
+    return false;
+  }
+  gzbuffer(r->gz, 1 << 20);
+  r->win = b;  // empty: the first more() inflates
   r->src_eof = false;
   r->active = true;
   return true;
@@ -378,9 +390,9 @@ struct Cur {
 };
 
 // The next line at the cursor: [ls, le) without '\n' / '\r'.  false when the
-// window holds no complete line there: more bytes may come (need = true), or
-// the file is exhausted (need = false).  At the end of a file the last,
-// unterminated line counts when it is not empty.
+// window holds no complete line there: more bytes (or index) may come (need =
+// true), or the file is exhausted (need = false).  At the end of a file the
+// last, unterminated line counts.
 bool next_line(const nt_reader* r, Cur& c, size_t& ls, size_t& le, bool& need) {
   need = false;
   if (c.p >= r->end) {
@@ -393,42 +405,38 @@ bool next_line(const nt_reader* r, Cur& c, size_t& ls, size_t& le, bool& need) {
     c.p = le + 1;
     ++c.i;
   } else {
-    if (!r->src_eof) {
+    if (r->scan < r->end || !r->src_eof) {
       need = true;
       return false;
     }
     le = r->end;
     c.p = r->end;
   }
-  if (le > ls && r->buf[le - 1] == '\r') --le;
+  if (le > ls && r->win->data[le - 1] == '\r') --le;
   return true;
 }
 
-// One record from the window at the committed cursor; appended to r->pend
-// (or, when lens_only, its sequence length to `len`).  Returns 1 = a record,
-// 0 = end of this file, -1 = error, 2 = incomplete (fill and retry).
-int parse_record(nt_reader* r, bool lens_only, uint64_t& len) {
+// One record from the window at the committed cursor, appended to the chunk
+// store (or, when lens_only, its sequence length only).  Returns 1 = a
+// record, 0 = end of this file, -1 = error, 2 = incomplete (more() and retry).
+int parse_record(nt_reader* r, bool lens_only, std::vector<uint64_t>* skip_lens) {
   Cur c{r->pos, r->nl_i};
   size_t ls = 0, le = 0;
   bool need = false;
-  const char* b = r->buf.data();
-  len = 0;
+  const char* b = r->win->data;
+  auto& S = r->c();
   if (r->format == 0) {
-    uint64_t name_at = 0, name_len = 0;
     for (;;) {  // the header (lines before the first one are skipped)
       if (!next_line(r, c, ls, le, need)) return need ? 2 : 0;
       if (le > ls && b[ls] == '>') break;
     }
-    name_at = ls + 1;
-    name_len = le - ls - 1;
-    const size_t p0 = r->pieces.size();
+    const size_t name_at = ls + 1, name_len = le - ls - 1;
+    r->pieces.clear();
+    uint64_t len = 0;
     for (;;) {  // sequence lines up to the next header or the end of the file
       Cur save = c;
       if (!next_line(r, c, ls, le, need)) {
-        if (need) {
-          r->pieces.resize(p0);
-          return 2;
-        }
+        if (need) return 2;
         break;
       }
       if (le == ls || b[ls] == ';') continue;  // blank and ';' comment lines are dropped
@@ -437,11 +445,27 @@ int parse_record(nt_reader* r, bool lens_only, uint64_t& len) {
         break;
       }
       len += le - ls;
-      if (!lens_only) r->pieces.emplace_back(ls, le - ls);
+      r->pieces.emplace_back(ls, le - ls);
     }
     r->pos = c.p;
     r->nl_i = c.i;
-    if (!lens_only) r->pend.push_back({name_at, name_len, p0, r->pieces.size(), len});
+    if (lens_only) {
+      skip_lens->push_back(len);
+      return 1;
+    }
+    S.seq_len.push_back(len);
+    S.name_ptr.push_back(b + name_at);
+    S.name_len.push_back(name_len);
+    if (r->pieces.size() <= 1) {  // one line: points into the buffer
+      S.seq_ptr.push_back(r->pieces.empty() ? b + name_at : b + r->pieces[0].first);
+      S.seq_blob.push_back(0);
+      S.seq_off.push_back(0);
+    } else {  // wrapped: joined in the store's blob
+      S.seq_ptr.push_back(nullptr);
+      S.seq_blob.push_back(1);
+      S.seq_off.push_back(S.seqs_blob.size());
+      for (auto& pc : r->pieces) S.seqs_blob.append(b + pc.first, pc.second);
+    }
     return 1;
   }
   // FASTQ: '@' name, the sequence line, '+' line, quality lines up to the sequence's length
@@ -454,7 +478,7 @@ int parse_record(nt_reader* r, bool lens_only, uint64_t& len) {
     }
     break;
   }
-  const uint64_t name_at = ls + 1, name_len = le - ls - 1;
+  const size_t name_at = ls + 1, name_len = le - ls - 1;
   auto malformed = [&] {
     r->err = "malformed FASTQ record '" + std::string(b + name_at, name_len) + "'";
     return -1;
@@ -473,85 +497,50 @@ int parse_record(nt_reader* r, bool lens_only, uint64_t& len) {
   }
   r->pos = c.p;
   r->nl_i = c.i;
-  len = sl;
-  if (!lens_only) {
-    r->pieces.emplace_back(ss, sl);
-    r->pend.push_back({name_at, name_len, r->pieces.size() - 1, r->pieces.size(), sl});
+  if (lens_only) {
+    skip_lens->push_back(sl);
+    return 1;
   }
+  S.seq_len.push_back(sl);
+  S.name_ptr.push_back(b + name_at);
+  S.name_len.push_back(name_len);
+  S.seq_ptr.push_back(b + ss);
+  S.seq_blob.push_back(0);
+  S.seq_off.push_back(0);
   return 1;
-}
-
-// Copy the pending records' names and sequences into the chunk store (all
-// host threads over the records), before the window moves.
-void flush_pending(nt_reader* r) {
-  if (r->pend.empty()) return;
-  auto& S = r->c();
-  const size_t n0 = S.name_len.size(), m = r->pend.size();
-  uint64_t nb = S.names_blob.size(), sb = S.seqs_blob.size();
-  S.name_off.resize(n0 + m);
-  S.name_len.resize(n0 + m);
-  S.seq_off.resize(n0 + m);
-  S.seq_len.resize(n0 + m);
-  for (size_t k = 0; k < m; ++k) {
-    const auto& q = r->pend[k];
-    S.name_off[n0 + k] = nb;
-    S.name_len[n0 + k] = q.name_len;
-    S.seq_off[n0 + k] = sb;
-    S.seq_len[n0 + k] = q.seq_len;
-    nb += q.name_len;
-    sb += q.seq_len;
-  }
-  S.names_blob.resize(nb);
-  S.seqs_blob.resize(sb);
-  const char* b = r->buf.data();
-  char* nd = &S.names_blob[0];
-  char* sd = &S.seqs_blob[0];
-  const uint64_t bytes = sb;
-  const unsigned nt = (bytes >= (4u << 20) && m > 1) ? std::min<unsigned>(host_threads(), (unsigned)m) : 1u;
-  par(nt, [&](unsigned t) {
-    for (size_t k = m * t / nt; k < m * (t + 1) / nt; ++k) {
-      const auto& q = r->pend[k];
-      std::memcpy(nd + S.name_off[n0 + k], b + q.name_at, q.name_len);
-      char* o = sd + S.seq_off[n0 + k];
-      for (uint64_t j = q.piece0; j < q.piece1; ++j) {
-        std::memcpy(o, b + r->pieces[j].first, r->pieces[j].second);
-        o += r->pieces[j].second;
-      }
-    }
-  });
-  r->pend.clear();
-  r->pieces.clear();
 }
 
 // Up to nrec records into the chunk store (or their lengths only); returns
 // the count, or -1 on error.
-int64_t read_records(nt_reader* r, uint64_t nrec, bool lens_only) {
+int64_t read_records(nt_reader* r, uint64_t nrec, bool lens_only, std::vector<uint64_t>* skip_lens) {
   auto& S = r->c();
   uint64_t got = 0;
+  bool ref = false;  // the chunk holds a reference to the current window
   while (got < nrec) {
     if (!r->active) {
-      flush_pending(r);
       if (!open_next(r)) break;
+      ref = false;
       continue;
     }
-    uint64_t len = 0;
-    const int k = parse_record(r, lens_only, len);
+    const int k = parse_record(r, lens_only, skip_lens);
     if (k == 1) {
       ++got;
-      if (lens_only) S.seq_len.push_back(len);
+      if (!lens_only && !ref) {
+        S.refs.push_back(r->win);
+        ref = true;
+      }
       continue;
     }
     if (k < 0) return -1;
-    if (k == 2) {  // incomplete: copy what is parsed, then read more of the file
-      flush_pending(r);
-      if (!fill(r) && !r->err.empty()) return -1;
+    if (k == 2) {  // incomplete: index further, or inflate the next window
+      const RBuf* w = r->win.get();
+      if (!more(r) && !r->err.empty()) return -1;
+      if (r->win.get() != w) ref = false;
       continue;
     }
-    flush_pending(r);  // k == 0: this file is done
-    if (!r->err.empty()) return -1;
+    if (!r->err.empty()) return -1;  // k == 0: this file is done
     close_source(r);
   }
-  flush_pending(r);
   if (!r->err.empty()) return -1;
   return (int64_t)got;
 }
@@ -607,16 +596,24 @@ const char* nt_reader_file(const nt_reader* r, uint64_t i) {
 const char* nt_reader_error(const nt_reader* r) { return r ? r->err.c_str() : "null reader"; }
 
 static void clear_store(nt_reader* r) {
-  r->cur ^= 1;
+  r->cur = (r->cur + 1) % r->store.size();
   auto& S = r->c();
-  S.names_blob.clear();
   S.seqs_blob.clear();
-  S.name_off.clear();
   S.seq_off.clear();
-  S.name_len.clear();
-  S.seq_len.clear();
+  S.seq_blob.clear();
   S.name_ptr.clear();
   S.seq_ptr.clear();
+  S.name_len.clear();
+  S.seq_len.clear();
+  S.refs.clear();  // the buffers of the chunk store.size() calls back (no longer valid)
+}
+
+int nt_reader_keep(nt_reader* r, uint32_t chunks) {
+  if (!r || chunks < 2 || chunks > 4096) return NT_E_ARG;
+  if (chunks > r->store.size()) {  // the new stores come after the current one in the ring
+    r->store.insert(r->store.begin() + (ptrdiff_t)r->cur + 1, chunks - r->store.size(), nt_reader::Store());
+  }
+  return NT_OK;
 }
 
 int64_t nt_reader_next(nt_reader* r, uint64_t nrec, const char* const** names,
@@ -624,15 +621,11 @@ int64_t nt_reader_next(nt_reader* r, uint64_t nrec, const char* const** names,
                        const uint64_t** seq_lens) {
   if (!r || !names || !name_lens || !seqs || !seq_lens || nrec == 0) return NT_E_ARG;
   clear_store(r);
-  const int64_t n = read_records(r, nrec, false);
+  const int64_t n = read_records(r, nrec, false, nullptr);
   if (n < 0) return NT_E_ARG;
   auto& S = r->c();
-  S.name_ptr.resize((size_t)n);
-  S.seq_ptr.resize((size_t)n);
-  for (int64_t i = 0; i < n; ++i) {
-    S.name_ptr[i] = S.names_blob.data() + S.name_off[i];
-    S.seq_ptr[i] = S.seqs_blob.data() + S.seq_off[i];
-  }
+  for (int64_t i = 0; i < n; ++i)  // joined sequences: the blob no longer grows
+    if (S.seq_blob[i]) S.seq_ptr[i] = S.seqs_blob.data() + S.seq_off[i];
   *names = S.name_ptr.data();
   *name_lens = S.name_len.data();
   *seqs = S.seq_ptr.data();
@@ -643,10 +636,12 @@ int64_t nt_reader_next(nt_reader* r, uint64_t nrec, const char* const** names,
 
 int64_t nt_reader_skip(nt_reader* r, uint64_t nrec, const uint64_t** seq_lens) {
   if (!r || !seq_lens || nrec == 0) return NT_E_ARG;
-  clear_store(r);
-  const int64_t n = read_records(r, nrec, true);
+  r->skip_cur ^= 1;
+  auto& L = r->skip_len[r->skip_cur];
+  L.clear();
+  const int64_t n = read_records(r, nrec, true, &L);
   if (n < 0) return NT_E_ARG;
-  *seq_lens = r->c().seq_len.data();
+  *seq_lens = L.data();
   r->records_total += (uint64_t)n;
   return n;
 }

@@ -13,6 +13,10 @@
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
 
+#include <dlfcn.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -155,20 +159,99 @@ std::string call_source(const NtProgram& P) {
   return s;
 }
 
-// hiprtc-compiles src into a loaded module
-bool compile_module(int device, const std::string& src, hipModule_t& mod, std::string& err) {
-  hiprtcProgram prog;
+// ---- on-disk code-object cache: a hiprtc build of the calling kernel takes
+// 5-20 s (the scan's 1-3 s), once per pattern set; the code object is kept
+// under $NT_JIT_CACHE (default $XDG_CACHE_HOME/nanotel or ~/.cache/nanotel),
+// keyed by a hash of everything that determines it: the program source, the
+// embedded headers (so a rebuilt library with changed kernels misses), the
+// options, the target and the hiprtc version.  NT_JIT_CACHE=0 turns it off;
+// an unwritable directory only means no cache.
+uint64_t fnv1a(uint64_t h, const void* p, size_t n) {
+  const unsigned char* c = (const unsigned char*)p;
+  for (size_t i = 0; i < n; ++i) h = (h ^ c[i]) * 1099511628211ull;
+  return h;
+}
+
+// $NT_JIT_CACHE, else jitcache/ next to libnanotel.so (in-tree: it travels
+// with the tree, and __graft_entry__.build() fills it for the benchmark's
+// pattern sets), else ~/.cache/nanotel when that one is not writable
+std::string cache_dir() {
+  const char* v = std::getenv("NT_JIT_CACHE");
+  if (v && std::strcmp(v, "0") == 0) return "";
+  if (v && *v) return v;
+  Dl_info di;
+  if (dladdr((const void*)&fnv1a, &di) && di.dli_fname) {
+    std::string d = di.dli_fname;
+    const size_t k = d.rfind('/');
+    d = (k == std::string::npos ? std::string(".") : d.substr(0, k)) + "/jitcache";
+    (void)mkdir(d.c_str(), 0755);
+    if (access(d.c_str(), W_OK | X_OK) == 0) return d;
+  }
+  const char* x = std::getenv("XDG_CACHE_HOME");
+  if (x && *x) return std::string(x) + "/nanotel";
+  const char* h = std::getenv("HOME");
+  return h && *h ? std::string(h) + "/.cache/nanotel" : "";
+}
+
+bool cache_read(const std::string& path, std::vector<char>& code) {
+  FILE* f = std::fopen(path.c_str(), "rb");
+  if (!f) return false;
+  std::fseek(f, 0, SEEK_END);
+  const long n = std::ftell(f);
+  std::fseek(f, 0, SEEK_SET);
+  bool ok = n > 0;
+  if (ok) {
+    code.resize((size_t)n);
+    ok = std::fread(code.data(), 1, (size_t)n, f) == (size_t)n;
+  }
+  std::fclose(f);
+  return ok;
+}
+
+void cache_write(const std::string& dir, const std::string& path, const std::vector<char>& code) {
+  std::string d;  // mkdir -p
+  for (size_t i = 0; i <= dir.size(); ++i) {
+    if (i == dir.size() || dir[i] == '/') {
+      if (!d.empty()) (void)mkdir(d.c_str(), 0755);
+    }
+    if (i < dir.size()) d += dir[i];
+  }
+  const std::string tmp = path + ".tmp." + std::to_string((long)getpid()) + "." +
+                          std::to_string((unsigned long long)(uintptr_t)&code);
+  FILE* f = std::fopen(tmp.c_str(), "wb");
+  if (!f) return;
+  const bool ok = std::fwrite(code.data(), 1, code.size(), f) == code.size();
+  if (std::fclose(f) == 0 && ok) (void)std::rename(tmp.c_str(), path.c_str());  // atomic publish
+  else (void)std::remove(tmp.c_str());
+}
+
+// The code object of src for arch (--offload-arch=...): from the on-disk
+// cache, else compiled by hiprtc (and cached).
+bool get_code(const std::string& arch, const std::string& src, std::vector<char>& code, std::string& err) {
   const char* hdrs[] = {kJitCommon, kJitDevice, kJitScan, kJitTScan, kJitCall};
   const char* names[] = {"nt_common.h", "nt_device.h", "nt_scan.h", "nt_tscan.h", "nt_call.h"};
+  const std::string dir = cache_dir();
+  std::string cpath;
+  if (!dir.empty()) {
+    uint64_t h = 1469598103934665603ull;
+    h = fnv1a(h, src.data(), src.size());
+    for (const char* x : hdrs) h = fnv1a(h, x, std::strlen(x));
+    h = fnv1a(h, arch.data(), arch.size());
+    const char* xo = std::getenv("NT_JIT_OPTS");
+    if (xo) h = fnv1a(h, xo, std::strlen(xo));
+    int maj = 0, mnr = 0;
+    (void)hiprtcVersion(&maj, &mnr);
+    h = fnv1a(h, &maj, sizeof maj);
+    h = fnv1a(h, &mnr, sizeof mnr);
+    char hex[24];
+    std::snprintf(hex, sizeof hex, "%016llx", (unsigned long long)h);
+    cpath = dir + "/nt_" + hex + ".co";
+    if (cache_read(cpath, code)) return true;
+  }
+  hiprtcProgram prog;
   if (hiprtcCreateProgram(&prog, src.c_str(), "nt_jit.hip", 5, hdrs, names) != HIPRTC_SUCCESS) {
     err = "hiprtcCreateProgram failed";
     return false;
-  }
-  hipDeviceProp_t prop;
-  std::string arch = "--offload-arch=gfx950";
-  if (hipGetDeviceProperties(&prop, device) == hipSuccess) {
-    std::string a = prop.gcnArchName;
-    arch = "--offload-arch=" + a.substr(0, a.find(':'));
   }
   std::vector<std::string> extra;  // NT_JIT_OPTS: extra compiler options (tuning experiments)
   if (const char* v = std::getenv("NT_JIT_OPTS")) {
@@ -201,9 +284,27 @@ bool compile_module(int device, const std::string& src, hipModule_t& mod, std::s
   }
   size_t n = 0;
   hiprtcGetCodeSize(prog, &n);
-  std::vector<char> code(n);
+  code.resize(n);
   hiprtcGetCode(prog, code.data());
   hiprtcDestroyProgram(&prog);
+  if (!cpath.empty()) cache_write(dir, cpath, code);
+  return true;
+}
+
+std::string device_arch(int device) {
+  hipDeviceProp_t prop;
+  std::string arch = "--offload-arch=gfx950";
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess) {
+    std::string a = prop.gcnArchName;
+    arch = "--offload-arch=" + a.substr(0, a.find(':'));
+  }
+  return arch;
+}
+
+// src as a loaded module on the calling thread's device
+bool compile_module(int device, const std::string& src, hipModule_t& mod, std::string& err) {
+  std::vector<char> code;
+  if (!get_code(device_arch(device), src, code, err)) return false;
   const hipError_t he = hipModuleLoadData(&mod, code.data());
   if (he != hipSuccess) {
     err = std::string("hipModuleLoadData: ") + hipGetErrorString(he);
@@ -297,9 +398,17 @@ void* nt_cjit_get(int device, const NtProgram& P, std::string& err) {
   const std::string src = call_source(P);
   const char* xo = std::getenv("NT_JIT_OPTS");
   const std::string key = std::to_string(device) + "\n" + (xo ? xo : "") + "\n" + src;
-  std::lock_guard<std::mutex> lk(g_mu);
-  auto it = g_ccache.find(key);
-  if (it == g_ccache.end()) {
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto it = g_ccache.find(key);
+    if (it != g_ccache.end()) {
+      if (!it->second.fn) err = it->second.err;
+      return (void*)it->second.fn;
+    }
+  }
+  // built without the lock (seconds): other contexts' lookups go on meanwhile;
+  // a build that loses a race to the same key is dropped
+  {
     CallEntry e;
     auto build = [&](const std::string& s) {
       if (compile_module(device, s, e.mod, e.err) &&
@@ -331,10 +440,16 @@ void* nt_cjit_get(int device, const NtProgram& P, std::string& err) {
         e.fn = f1;
       }
     }
-    it = g_ccache.emplace(key, e).first;
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto it = g_ccache.find(key);
+    if (it == g_ccache.end()) {
+      it = g_ccache.emplace(key, e).first;
+    } else if (e.mod) {
+      (void)hipModuleUnload(e.mod);
+    }
+    if (!it->second.fn) err = it->second.err;
+    return (void*)it->second.fn;
   }
-  if (!it->second.fn) err = it->second.err;
-  return (void*)it->second.fn;
 }
 
 hipError_t nt_cjit_launch(void* fn, int grid, hipStream_t stream, const NtProgram* prog, const NtBatch* B,
@@ -344,4 +459,19 @@ hipError_t nt_cjit_launch(void* fn, int grid, hipStream_t stream, const NtProgra
   NtOut o = *O;
   void* args[] = {&prog, &b, &o, &tmask, &thr, &thr_size, &fix_last};
   return hipModuleLaunchKernel((hipFunction_t)fn, (unsigned)grid, 1, 1, 256, 1, 1, 0, stream, args, nullptr);
+}
+
+// Fill the on-disk cache with the program's code objects (the scan module and
+// the calling kernel, at the default occupancy and at the 2-waves/SIMD
+// fallback for spilling builds) without a device: __graft_entry__.build()
+// does this for the benchmark's pattern sets, so a fresh GPU box skips hiprtc.
+int nt_jit_prebuild_program(const NtProgram& P, const std::string& arch) {
+  const std::string a = "--offload-arch=" + arch;
+  std::vector<char> code;
+  std::string err;
+  if (!get_code(a, jit_source(P), code, err)) return -7;
+  const std::string cs = call_source(P);
+  if (!get_code(a, cs, code, err)) return -7;
+  if (!get_code(a, "#define NT_CALL_WAVES_PER_EU 2\n" + cs, code, err)) return -7;
+  return 0;
 }

@@ -104,6 +104,8 @@ SIGNATURES = {
                                          ctypes.POINTER(ctypes.c_double)]),
     "nt_kernel_launches": (ctypes.c_int64, [_P]),
     "nt_call_jit_state": (ctypes.c_int, [_P]),
+    "nt_call_jit_wait": (ctypes.c_int, [_P]),
+    "nt_jit_prebuild": (ctypes.c_int, [ctypes.POINTER(NtParams), ctypes.c_char_p]),
     "nt_analyze_host": (ctypes.c_int, [_P, _P, _P, ctypes.c_uint64, _P, _P, _P, _P, _P, _P]),
     "nt_filter_call": (ctypes.c_int, [_P, _P, _P]),
     "nt_filter_host": (ctypes.c_int, [_P, _P, _P, ctypes.c_uint64, _P]),
@@ -119,6 +121,7 @@ SIGNATURES = {
     "nt_reader_next": (ctypes.c_int64, [_P, ctypes.c_uint64, ctypes.POINTER(ctypes.c_void_p),
                                         ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p),
                                         ctypes.POINTER(ctypes.c_void_p)]),
+    "nt_reader_keep": (ctypes.c_int, [_P, ctypes.c_uint32]),
     "nt_reader_skip": (ctypes.c_int64, [_P, ctypes.c_uint64, ctypes.POINTER(ctypes.c_void_p)]),
     "nt_synth_device": (ctypes.c_int, [_P, ctypes.POINTER(NtSynthParams), ctypes.c_uint64, _P]),
     "nt_uniform_layout_device": (ctypes.c_int, [_P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int32,

@@ -116,6 +116,11 @@ class NanoTel:
         the patterns (hiprtc), False for the ahead-of-time one."""
         return bool(lib().nt_call_jit_state(self._h))
 
+    def call_jit_wait(self):
+        """Wait for the background build of the calling kernel specialised for
+        the patterns (started by nt_compile); True when it is available."""
+        return bool(_check(lib().nt_call_jit_wait(self._h), self._h))
+
     def synchronize(self):
         _check(lib().nt_synchronize(self._h), self._h)
 
@@ -133,6 +138,12 @@ class NanoTel:
         ptrs = (ctypes.c_char_p * max(1, n))(*bseqs)
         lens = np.array([len(b) for b in bseqs], np.uint64)
         return self._analyze(ctypes.addressof(ptrs), lens, n, want_windows, want_hits)
+
+    def analyze_pointers(self, ptrs, lens, want_windows=False, want_hits=False):
+        """analyze() of reads given as host addresses (a uint64 array of
+        `const char*`, e.g. several reader chunks' sequences joined) and lengths."""
+        ptrs = np.ascontiguousarray(ptrs, np.uint64)
+        return self._analyze(ptrs.ctypes.data, lens, int(ptrs.size), want_windows, want_hits)
 
     def analyze_chunk(self, chunk, want_windows=False, want_hits=False):
         """analyze() of an io.Reader chunk, zero-copy (the reader's buffers)."""
@@ -287,6 +298,17 @@ def bundle_layout_host(planes, blk_off, lengths, plan, subseq_length):
                                        bs.ctypes.data, plan.n_bundles, int(subseq_length), out.ctypes.data,
                                        int(plan.tplane_bytes)))
     return out[:plan.tplane_bytes // 4]
+
+
+def jit_prebuild(patterns, tvr_patterns=None, subseq_length=100, min_density=0.6, check_right_edge=False,
+                 rc=False, arch="gfx950"):
+    """nt_jit_prebuild (no device): the kernels specialised for this parameter
+    set go into the on-disk code-object cache (jitcache/ beside the library)."""
+    pat = patterns.encode() if isinstance(patterns, str) else patterns
+    tvr = None if tvr_patterns is None else (tvr_patterns.encode() if isinstance(tvr_patterns, str)
+                                             else tvr_patterns)
+    prm = NtParams(pat, tvr, int(subseq_length), float(min_density), int(bool(check_right_edge)), int(bool(rc)), 0)
+    _check(lib().nt_jit_prebuild(ctypes.byref(prm), arch.encode()))
 
 
 def synth_params(seed=20260501, first_read=0, read_len=50000, p_tract=0.5, sub_rate=0.02,

@@ -130,34 +130,64 @@ def _plot_jobs(nt, res, order, lens, ser, save_path):
     return jobs
 
 
-def _scan_chunk(nt, ch, use_filter, write_reads, log, want_windows=False):
-    """Scan + call one chunk (after --use_filter when on).  Returns
-    (rel_serials, row_order, rel_max, result, names, lengths, {read: seq})
-    over the reads that were scanned."""
-    names, lens = ch.names(), ch.lengths.copy()
-    if use_filter:
-        keep = np.flatnonzero(nt.filter_chunk(ch))
-        if keep.size == 0:
-            log("No read have passed the filteration at run_with_rc_and_filter!")
-            return None, np.zeros(0, np.int64), shard.SKIPPED, None, [], lens[:0], {}
-        seqs = [ch.seq(int(j)) for j in keep]
-        res = nt.analyze(seqs, want_windows=want_windows)
-        names = [names[int(j)] for j in keep]
-        lens = lens[keep]
-        get = seqs.__getitem__
-    else:
-        res = nt.analyze_chunk(ch, want_windows=want_windows)
-        get = lambda j: ch.seq(j)  # noqa: E731
-    rel, order, rmax = shard.chunk_relative(res["telomeric"])
-    seqs = {int(j): get(int(j)) for j in order} if write_reads else {}
-    return rel, order, rmax, res, names, lens, seqs
+# One device call covers several of the reference's nrec-record chunks (they
+# stay the units of serials and rows): the calling kernel specialised for the
+# patterns runs on batches of >= 65,536 reads (nt_host.cpp), so a call takes
+# ceil(65536 / nrec) rounds of chunks, at most kGroupRounds and at most
+# kGroupBases bases per rank.
+kCallReads = 65536
+kGroupRounds = 16
+kGroupBases = 4_000_000_000
+
+
+def _group_rounds(nrec):
+    return max(1, min(kGroupRounds, -(-kCallReads // max(1, nrec))))
+
+
+class _View(dict):
+    """One chunk's slice of a grouped result (window-count offsets stay global)."""
+
+
+def _scan_group(nt, chunks, use_filter, write_reads, log, want_windows=False):
+    """Scan + call the reads of several chunks in ONE device call (after
+    --use_filter, per chunk, when on).  Returns per chunk (rel_serials,
+    row_order, rel_max, result view, name_of(j), lengths, {read: seq}) over
+    the reads that were scanned; rel_max is shard.SKIPPED for a chunk that
+    --use_filter emptied."""
+    parts = []
+    for ch in chunks:
+        idx = np.arange(ch.n)
+        if use_filter:
+            idx = np.flatnonzero(nt.filter_chunk(ch))
+            if idx.size == 0:
+                log("No read have passed the filteration at run_with_rc_and_filter!")
+        parts.append((ch, idx))
+    ptrs = np.concatenate([ch.pointers()[idx] for ch, idx in parts]) if parts else np.zeros(0, np.uint64)
+    lens = np.concatenate([ch.lengths[idx] for ch, idx in parts]) if parts else np.zeros(0, np.uint64)
+    res = nt.analyze_pointers(ptrs, lens, want_windows=want_windows) if ptrs.size else None
+    out, a = [], 0
+    for ch, idx in parts:
+        b = a + idx.size
+        if idx.size == 0:
+            out.append((None, np.zeros(0, np.int64), shard.SKIPPED, None, None, lens[:0], {}))
+            continue
+        v = _View({k: res[k][a:b] for k in ("start", "end", "density", "flags", "width", "telomeric") if k in res})
+        if want_windows:
+            v["win_off"], v["n_windows"], v["win_counts"] = res["win_off"][a:b], res["n_windows"][a:b], \
+                res["win_counts"]
+        rel, order, rmax = shard.chunk_relative(v["telomeric"])
+        name_of = (lambda c, ix: (lambda j: c.name(int(ix[j]))))(ch, idx)
+        seqs = {int(j): ch.seq(int(idx[int(j)])) for j in order} if write_reads else {}
+        out.append((rel, order, rmax, v, name_of, lens[a:b], seqs))
+        a = b
+    return out
 
 
 class _Prefetch:
-    """Chunk k+1 is read on a worker thread while chunk k is scanned: the C++
-    reader keeps two chunk buffers in turn and ctypes drops the GIL.  Chunks
-    this rank does not scan (own(k) false) are passed over with the reader's
-    count-only skip path: record boundaries and lengths, no copies."""
+    """Chunk k+1 is read on a worker thread while chunk k is scanned (the C++
+    reader keeps the last chunks valid, nt_reader_keep, and ctypes drops the
+    GIL).  Chunks this rank does not scan (own(k) false) are passed over with
+    the reader's count-only skip path: record boundaries and lengths, no copies."""
 
     def __init__(self, rdr, nrec, own=lambda k: True):
         self._rdr, self._nrec, self._own = rdr, nrec, own
@@ -230,6 +260,8 @@ def run(input_path, save_path, patterns, fmt="fastq", nrec=10000, rc=False, min_
     tvr = tvr_patterns is not None
     rdr = Reader(input_path, fmt)
     files = rdr.files()
+    g = _group_rounds(nrec)  # rounds of chunks per device call
+    rdr.keep(g + 2)          # this rank's chunks of a group stay valid, plus the one read ahead
     # chunk k of the stream is scanned by rank k % world (rounds of `world`
     # chunks); the other ranks pass over it with the reader's skip path
     src = _Prefetch(rdr, nrec, own=lambda k: k % world == rank)
@@ -243,47 +275,57 @@ def run(input_path, save_path, patterns, fmt="fastq", nrec=10000, rc=False, min_
     s_next, m_run = 1.0, shard.NEG_INF  # serial_start of the next chunk, running max(Serial)
     t0 = time.time()
     failure = None
-    # rounds of `world` chunks: rank r scans chunk r of the round; one
-    # all_reduce per round fixes the serial_starts (and carries an error flag,
-    # so that a rank that fails stops every rank at the same round instead of
-    # leaving them blocked in the next collective)
+    # groups of up to g rounds of `world` chunks: rank r scans chunk r of each
+    # round, the group's in one device call; one all_reduce per group fixes the
+    # serial_starts (and carries an error flag, so that a rank that fails stops
+    # every rank at the same group instead of leaving them blocked in the next
+    # collective).  Every rank reads the same stream, so the groups' extents
+    # (the rounds, the bases cap) agree.
     while True:
-        own = None
-        n_round = 0
+        own = []  # (chunk's place in the group, chunk)
+        n_grp, ended = 0, False
         try:
-            for r in range(world):
-                ch = src.next_chunk()
-                if ch is None:
+            bases = 0
+            for _ in range(g):
+                for r in range(world):
+                    ch = src.next_chunk()
+                    if ch is None:
+                        ended = True
+                        break
+                    lengths_all.append(ch.lengths.copy())
+                    bases += int(ch.lengths.sum())
+                    if r == rank:
+                        log(f"processing chunk {k + n_grp + 1} ...")
+                        own.append((n_grp, ch))
+                    n_grp += 1
+                if ended or bases >= kGroupBases * world:
                     break
-                n_round += 1
-                lengths_all.append(ch.lengths.copy())
-                if r == rank:
-                    log(f"processing chunk {k + r + 1} ...")
-                    own = (r,) + _scan_chunk(nt, ch, use_filter, write_reads, log, want_windows=plot)
+            scanned = _scan_group(nt, [ch for _, ch in own], use_filter, write_reads, log, want_windows=plot)
         except Exception as ex:  # noqa: BLE001 -- re-raised after the collective
-            failure = ex
-        maxima, failed = shard.exchange_rel_max({own[0]: own[3]} if own else {}, world, device=coll_dev,
-                                                failed=failure is not None)
+            failure, scanned = ex, []
+        local = {own[i][0]: scanned[i][2] for i in range(len(scanned))}
+        maxima, failed = shard.exchange_rel_max(local, g * world, device=coll_dev, failed=failure is not None)
         if failed:
             break
-        starts = np.empty(n_round, np.float64)
-        for r in range(n_round):  # the reference's recurrence, chunk by chunk
+        starts = np.empty(n_grp, np.float64)
+        for r in range(n_grp):  # the reference's recurrence, chunk by chunk
             starts[r], s_next, m_run = shard.advance(s_next, m_run, float(maxima[r]))
         try:
-            if own is not None and own[4] is None:
-                local_rows[k + own[0]] = []  # --use_filter kept no read of this chunk
-            elif own is not None:
-                r, rel, order, _, res, names, lens, seqs = own
-                ser = shard.assign_chunk_serials(rel, starts[r])
-                local_rows[k + r] = chunk_rows(res, names, lens, ser, order, nt.n_pass)
+            for (pos, _), (rel, order, _, res, name_of, lens, seqs) in zip(own, scanned):
+                if res is None:
+                    local_rows[k + pos] = []  # --use_filter kept no read of this chunk
+                    continue
+                ser = shard.assign_chunk_serials(rel, starts[pos])
+                names = {int(j): name_of(int(j)) for j in order}
+                local_rows[k + pos] = chunk_rows(res, names, lens, ser, order, nt.n_pass)
                 for f in pending:  # the previous chunk's files (errors surface here)
                     f.result()
                 pending = []
                 now, last_inf = _targets(ser, order)
                 jobs = _plot_jobs(nt, res, order, lens, ser, save_path) if plot else []
-                job_of = {int(j): jb for j, jb in zip(_plot_rows(res, order), jobs)}
+                job_of = {int(j): jb for j, jb in zip(_plot_rows(res, order), jobs)} if plot else {}
                 if last_inf is not None:
-                    held = (k + r, (names[last_inf], seqs.get(last_inf), rc), job_of.get(last_inf))
+                    held = (k + pos, (names[last_inf], seqs.get(last_inf), rc), job_of.get(last_inf))
                 if write_reads:
                     pending += [writers.submit(_write_read, os.path.join(
                         reads_dir, f"{r_as_character(float(ser[j]))}.fasta.gz"), names[j], seqs[j], rc)
@@ -296,8 +338,8 @@ def run(input_path, save_path, patterns, fmt="fastq", nrec=10000, rc=False, min_
                     pending += [pool.submit(plots.write_read_plots, *a, jpeg=plot_jpeg, **kw) for a, kw in jobs]
         except Exception as ex:  # noqa: BLE001
             failure = ex
-        k += n_round
-        if n_round < world:
+        k += n_grp
+        if ended:
             break
     try:
         for f in pending:

@@ -27,7 +27,7 @@ from ._lib import NanoTelError, lib
 
 class Chunk:
     """One nt_reader_next() chunk; valid through the next next_chunk() call
-    (the reader double-buffers), not after the one that follows."""
+    (or the next keep()-1 calls), not after."""
 
     def __init__(self, n, names_p, name_lens_p, seqs_p, seq_lens_p):
         self.n = int(n)
@@ -49,6 +49,12 @@ class Chunk:
 
     def seq(self, i):
         return ctypes.string_at(self._sp[i], int(self.lengths[i]))
+
+    def pointers(self):
+        """The sequences' host addresses (uint64 array, a view of the reader's)."""
+        if not self.n:
+            return np.zeros(0, np.uint64)
+        return np.ctypeslib.as_array((ctypes.c_uint64 * self.n).from_address(self.seq_ptrs))
 
 
 class SkippedChunk:
@@ -84,6 +90,12 @@ class Reader:
         if n == 0:
             return None
         return Chunk(n, a, b, c, d)
+
+    def keep(self, chunks):
+        """nt_reader_keep: the last `chunks` chunks stay valid (default 2)."""
+        rc = lib().nt_reader_keep(self._h, int(chunks))
+        if rc != 0:
+            raise NanoTelError(int(rc), "nt_reader_keep")
 
     def skip_chunk(self, nrec):
         """The next nrec records without copying names or sequences

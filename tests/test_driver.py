@@ -37,6 +37,10 @@ class OracleNanoTel:
     def analyze_chunk(self, ch, want_windows=False):
         return self.analyze([ch.seq(i) for i in range(ch.n)], want_windows)
 
+    def analyze_pointers(self, ptrs, lens, want_windows=False):
+        import ctypes
+        return self.analyze([ctypes.string_at(int(p), int(n)) for p, n in zip(ptrs, lens)], want_windows)
+
     def analyze(self, seqs, want_windows=False):
         n = len(seqs)
         res = {"start": np.full((n, 3), -1, np.int32), "end": np.full((n, 3), -1, np.int32),
@@ -56,10 +60,12 @@ class OracleNanoTel:
             if want_windows:
                 res["n_windows"][i] = len(r["win_counts"][0])
                 res["wins"].append(r["win_counts"])
+        # the real result's layout: win_off locates a read's counts in win_counts
+        res["win_off"], res["win_counts"] = np.arange(n), res["wins"]
         return res
 
     def window_counts(self, res, read, p):
-        return res["wins"][read][p]
+        return res["win_counts"][int(res["win_off"][read])][p]
 
     def close(self):
         pass
@@ -282,16 +288,13 @@ def test_inf_serials_write_the_last_read_once():
 
 
 class FailingNanoTel(OracleNanoTel):
-    """Raises on the second chunk it scans (rank 1 in a 2-rank run)."""
+    """Raises on the device call it makes on rank 1 of a 2-rank run."""
 
-    calls = 0
-
-    def analyze_chunk(self, ch, want_windows=False):
+    def analyze_pointers(self, ptrs, lens, want_windows=False):
         import torch.distributed as dist
-        FailingNanoTel.calls += 1
-        if dist.is_initialized() and dist.get_rank() == 1 and FailingNanoTel.calls == 2:
+        if dist.is_initialized() and dist.get_rank() == 1:
             raise RuntimeError("injected scan failure")
-        return super().analyze_chunk(ch, want_windows)
+        return super().analyze_pointers(ptrs, lens, want_windows)
 
 
 def _failing_rank(rank, world, port, inp, out, q):
