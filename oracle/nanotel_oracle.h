@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define NTO_MAX_PAT 16   /* patterns per list (after unique) */
+#define NTO_MAX_PAT 64   /* patterns per list (after unique) */
 #define NTO_MAX_M   64   /* longest pattern accepted by the parser */
 
 /* Error codes (negative). */

@@ -24,7 +24,7 @@
 #include <stdint.h>
 #endif
 
-#define NT_MAX_PAT 8      // unique patterns per list (--patterns / --tvr_patterns)
+#define NT_MAX_PAT 64     // unique patterns per list (--patterns / --tvr_patterns)
 #define NT_MAX_M 18       // testit::assert(str_length(pattern) <= 18), NanoTel.R:589,647
 #define NT_MAX_TVR_M 32   // TVRs are only length-limited by the 32-bit start words
 #define NT_MAX_PASS 3

@@ -20,6 +20,7 @@
 #include "nanotel.h"
 #include "nt_common.h"
 #include "nt_rng.h"
+#include "nt_pack.h"
 
 extern "C" {
 uint32_t nt_dev_wave_words(int single, int n_hits, int np, uint32_t nw_cap);
@@ -59,6 +60,8 @@ hipError_t nt_jit_launch(void* fn, int grid, size_t lds_bytes, hipStream_t strea
                          const NtProgram* prog, const uint32_t* thr, const NtBatch* B,
                          const NtOut* O, uint64_t* tmask, unsigned long long* queue,
                          uint32_t len_lo, uint32_t len_hi, uint32_t claim, uint32_t nstatic, uint32_t wave_words, uint32_t* gscr);
+
+using namespace nt_host;
 
 namespace {
 
@@ -101,216 +104,6 @@ struct DevBuf {
     if (p) (void)hipFree(p);
   }
 };
-
-// Biostrings DNA_ALPHABET codes (A=1 C=2 G=4 T=8, IUPAC = OR, '-'=16 '+'=32 '.'=64);
-// lower case letters are upper-cased by DNAString().
-struct LetterTab {
-  uint8_t t[256] = {};
-  LetterTab() {
-    const char* up = "ACGTMRWSYKVHDBN";
-    const uint8_t codes[] = {1, 2, 4, 8, 3, 5, 9, 6, 10, 12, 7, 11, 13, 14, 15};
-    for (int i = 0; i < 15; ++i) {
-      t[(unsigned char)up[i]] = codes[i];
-      t[(unsigned char)(up[i] - 'A' + 'a')] = codes[i];
-    }
-    t[(unsigned char)'-'] = 16;
-    t[(unsigned char)'+'] = 32;
-    t[(unsigned char)'.'] = 64;
-  }
-};
-uint8_t letter_code(unsigned char c) {
-  static const LetterTab tab;  // thread-safe one-time init (the packer runs on many threads)
-  return tab.t[c];
-}
-
-// 2-bit code for A/C/G/T (either case), else -1.
-inline int base2(unsigned char c) {
-  switch (c) {
-    case 'A': case 'a': return 0;
-    case 'C': case 'c': return 1;
-    case 'G': case 'g': return 2;
-    case 'T': case 't': return 3;
-    default: return -1;
-  }
-}
-
-inline uint8_t complement_code(uint8_t x) {
-  return (uint8_t)((x & 0xF0) | ((x & 1) << 3) | ((x & 8) >> 3) | ((x & 2) << 1) | ((x & 4) >> 1));
-}
-
-// 32 bases at a time: the 2-bit code of A/C/G/T (either case) is
-// lo = bit1 ^ bit2, hi = bit2 of the ASCII byte (A 0x41 -> 00, C 0x43 -> 01,
-// G 0x47 -> 10, T 0x54 -> 11).  pack32 returns false when any of the 32
-// bytes is not A/C/G/T; the caller then takes the per-base path (exceptions,
-// bad letters).  AVX2 when the host has it (runtime dispatch), else scalar.
-__attribute__((target("avx2"))) static bool pack32_avx2(const unsigned char* p, uint32_t& lo,
-                                                        uint32_t& hi) {
-  const __m256i v = _mm256_loadu_si256((const __m256i*)p);
-  const __m256i l = _mm256_or_si256(v, _mm256_set1_epi8(0x20));
-  const __m256i ok = _mm256_or_si256(
-      _mm256_or_si256(_mm256_cmpeq_epi8(l, _mm256_set1_epi8('a')), _mm256_cmpeq_epi8(l, _mm256_set1_epi8('c'))),
-      _mm256_or_si256(_mm256_cmpeq_epi8(l, _mm256_set1_epi8('g')), _mm256_cmpeq_epi8(l, _mm256_set1_epi8('t'))));
-  if ((uint32_t)_mm256_movemask_epi8(ok) != 0xFFFFFFFFu) return false;
-  const uint32_t b1 = (uint32_t)_mm256_movemask_epi8(_mm256_slli_epi16(v, 6));
-  const uint32_t b2 = (uint32_t)_mm256_movemask_epi8(_mm256_slli_epi16(v, 5));
-  lo = b1 ^ b2;
-  hi = b2;
-  return true;
-}
-
-static bool pack32_scalar(const unsigned char* p, uint32_t& lo, uint32_t& hi) {
-  uint32_t l = 0, h = 0;
-  for (int i = 0; i < 32; ++i) {
-    const int c = base2(p[i]);
-    if (c < 0) return false;
-    l |= (uint32_t)(c & 1) << i;
-    h |= (uint32_t)(c >> 1) << i;
-  }
-  lo = l;
-  hi = h;
-  return true;
-}
-
-static const bool g_avx2 = __builtin_cpu_supports("avx2");
-
-inline bool pack32(const unsigned char* p, uint32_t& lo, uint32_t& hi) {
-  return g_avx2 ? pack32_avx2(p, lo, hi) : pack32_scalar(p, lo, hi);
-}
-
-// 32 x 32 bit transpose: y[i] bit s = x[s] bit i (32 reads' plane words of
-// one 32-base block -> the T-layout words of its 32 positions, bit s = slot s).
-// AVX2: a byte transpose of the 32 rows into 4 registers (register b, byte s
-// = byte b of x[s]: in-lane byte shuffle, dword permute, 64-bit 4x4 transpose),
-// then bit k of every byte by one shift + movemask per output word.
-__attribute__((target("avx2"))) static void transpose32_avx2(const uint32_t* x, uint32_t* y) {
-  const __m256i bsh = _mm256_setr_epi8(0, 4, 8, 12, 1, 5, 9, 13, 2, 6, 10, 14, 3, 7, 11, 15,
-                                       0, 4, 8, 12, 1, 5, 9, 13, 2, 6, 10, 14, 3, 7, 11, 15);
-  const __m256i dperm = _mm256_setr_epi32(0, 4, 1, 5, 2, 6, 3, 7);
-  __m256i B[4];
-  for (int g = 0; g < 4; ++g) {
-    // lane h, dword b = byte b of rows 8g+4h .. 8g+4h+3; then qword b = byte b of rows 8g .. 8g+7
-    const __m256i a = _mm256_shuffle_epi8(_mm256_loadu_si256((const __m256i*)(x + 8 * g)), bsh);
-    B[g] = _mm256_permutevar8x32_epi32(a, dperm);
-  }
-  const __m256i t0 = _mm256_unpacklo_epi64(B[0], B[1]), t1 = _mm256_unpackhi_epi64(B[0], B[1]);
-  const __m256i t2 = _mm256_unpacklo_epi64(B[2], B[3]), t3 = _mm256_unpackhi_epi64(B[2], B[3]);
-  const __m256i Y[4] = {_mm256_permute2x128_si256(t0, t2, 0x20), _mm256_permute2x128_si256(t1, t3, 0x20),
-                        _mm256_permute2x128_si256(t0, t2, 0x31), _mm256_permute2x128_si256(t1, t3, 0x31)};
-  for (int b = 0; b < 4; ++b) {
-    y[8 * b + 7] = (uint32_t)_mm256_movemask_epi8(Y[b]);
-    y[8 * b + 6] = (uint32_t)_mm256_movemask_epi8(_mm256_slli_epi16(Y[b], 1));
-    y[8 * b + 5] = (uint32_t)_mm256_movemask_epi8(_mm256_slli_epi16(Y[b], 2));
-    y[8 * b + 4] = (uint32_t)_mm256_movemask_epi8(_mm256_slli_epi16(Y[b], 3));
-    y[8 * b + 3] = (uint32_t)_mm256_movemask_epi8(_mm256_slli_epi16(Y[b], 4));
-    y[8 * b + 2] = (uint32_t)_mm256_movemask_epi8(_mm256_slli_epi16(Y[b], 5));
-    y[8 * b + 1] = (uint32_t)_mm256_movemask_epi8(_mm256_slli_epi16(Y[b], 6));
-    y[8 * b + 0] = (uint32_t)_mm256_movemask_epi8(_mm256_slli_epi16(Y[b], 7));
-  }
-}
-
-static void transpose32_scalar(const uint32_t* x, uint32_t* y) {
-  for (int i = 0; i < 32; ++i) {
-    uint32_t w = 0;
-    for (int s = 0; s < 32; ++s) w |= ((x[s] >> i) & 1u) << s;
-    y[i] = w;
-  }
-}
-
-// number of non-A/C/G/T bytes in s[0, n)
-static uint64_t count_non_acgt(const unsigned char* s, uint64_t n) {
-  uint64_t e = 0, i = 0;
-  uint32_t lo, hi;
-  for (; i + 32 <= n; i += 32)
-    if (!pack32(s + i, lo, hi))
-      for (int k = 0; k < 32; ++k) e += base2(s[i + k]) < 0;
-  for (; i < n; ++i) e += base2(s[i]) < 0;
-  return e;
-}
-
-int64_t window_count(int64_t n, int L) {
-  if (n <= 0 || L <= 0) return 0;
-  int64_t c = (n - 1) / L + 1;                      // seq(1, n, by = L)
-  const int64_t last_start = 1 + (c - 1) * (int64_t)L;
-  if ((double)(n - last_start) < (double)L / 2.0) c -= 1;  // NanoTel.R:220
-  return c;
-}
-
-// 32-base blocks in a read's slot: whole 64-base segments (16-byte loads)
-inline uint64_t read_blocks(uint64_t n) { return 2 * ((n + 63) / 64); }
-
-template <class F>
-void parallel_for(uint64_t n, F&& f) {
-  unsigned nt = std::thread::hardware_concurrency();
-  if (nt == 0) nt = 1;
-  if (nt > 32) nt = 32;
-  if (n < 64 || nt == 1) {
-    for (uint64_t i = 0; i < n; ++i) f(i);
-    return;
-  }
-  std::vector<std::thread> th;
-  const uint64_t chunk = (n + nt - 1) / nt;
-  for (unsigned t = 0; t < nt; ++t) {
-    const uint64_t lo = t * chunk, hi = std::min<uint64_t>(n, lo + chunk);
-    if (lo >= hi) break;
-    th.emplace_back([lo, hi, &f] {
-      for (uint64_t i = lo; i < hi; ++i) f(i);
-    });
-  }
-  for (auto& x : th) x.join();
-}
-
-// One token list of --patterns / --tvr_patterns: str_split(x, "\\s+"), as.list
-// when > 1 token, unique() (NanoTel.R:2322-2334, 328, 362).
-int parse_tokens(const char* s, std::vector<std::string>& uniq, bool& is_list, std::string& err) {
-  std::vector<std::string> toks;
-  const char* p = s;
-  auto ws = [](char c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r' || c == '\f' || c == '\v'; };
-  for (;;) {
-    const char* b = p;
-    while (*p && !ws(*p)) ++p;
-    toks.emplace_back(b, p);
-    if (!*p) break;
-    while (*p && ws(*p)) ++p;
-  }
-  is_list = toks.size() > 1;
-  for (auto& t : toks) {
-    if (t.empty()) {
-      err = "empty pattern (leading/trailing whitespace in the pattern list)";
-      return NT_E_PATTERN;
-    }
-    if (std::find(uniq.begin(), uniq.end(), t) == uniq.end()) uniq.push_back(t);
-  }
-  return NT_OK;
-}
-
-int build_pat(const std::string& s, int max_m, NtPat& P, std::string& err) {
-  if ((int)s.size() > max_m) {
-    err = "pattern '" + s + "' is longer than " + std::to_string(max_m) + " letters";
-    return max_m == NT_MAX_M ? NT_E_PATTERN : NT_E_LIMIT;
-  }
-  std::memset(&P, 0, sizeof P);
-  P.m = (int32_t)s.size();
-  P.fixed = 1;
-  for (char ch : s)
-    if (std::strchr("WSMKRYBDHVN", ch)) P.fixed = 0;  // uppercase-only regex, NanoTel.R:334
-  for (int j = 0; j < P.m; ++j) {
-    const uint8_t c = letter_code((unsigned char)s[j]);
-    if (!c) {
-      err = "pattern '" + s + "' has a letter outside DNA_ALPHABET";
-      return NT_E_PATTERN;
-    }
-    P.code[j] = c;
-    uint8_t ts = 0, te = 0;
-    for (int b = 0; b < 4; ++b) {
-      const uint8_t bc = (uint8_t)(1u << b);
-      if (P.fixed ? (c == bc) : ((c & bc) != 0)) ts |= (uint8_t)(1u << b);
-      if (c == bc) te |= (uint8_t)(1u << b);
-    }
-    P.tt_scan[j] = ts;
-    P.tt_eq[j] = te;
-  }
-  return NT_OK;
-}
 
 }  // namespace
 
@@ -484,98 +277,6 @@ int nt_synchronize(nt_ctx* ctx) {
   return e == hipSuccess ? NT_OK : hip_fail(ctx, e, "hipStreamSynchronize");
 }
 
-int64_t nt_window_count(int64_t n, int32_t subseq_length) { return window_count(n, subseq_length); }
-uint64_t nt_window_rows(int64_t nw) { return nw <= 0 ? 0 : NT_WIN_ROWS((uint64_t)nw); }
-
-uint64_t nt_read_blocks(uint64_t n) { return read_blocks(n); }
-
-// The program of a parameter set (host only): patterns, passes, the divisor
-// magic and the telomeric threshold table.
-static int make_program(const nt_params* prm, NtProgram& P, std::vector<uint32_t>& thr, std::string& err) {
-  if (!prm) return NT_E_ARG;
-  if (!prm->patterns) { err = "Missing required parameter:  --patterns"; return NT_E_ARG; }
-  if (prm->subseq_length <= 0) { err = "--subseq_length must be >= 1"; return NT_E_ARG; }
-  if (prm->subseq_length > 43690)
-    { err = "--subseq_length > 43690 overflows the uint16 window counts"; return NT_E_LIMIT; }
-  std::memset(&P, 0, sizeof P);
-  std::vector<std::string> pats, tvrs;
-  bool pat_list = false, tvr_list = false;
-  int rc = parse_tokens(prm->patterns, pats, pat_list, err);
-  if (rc) return rc;
-  if (pats.size() > NT_MAX_PAT) { err = "more than 8 unique patterns"; return NT_E_LIMIT; }
-  for (size_t i = 0; i < pats.size(); ++i) {
-    rc = build_pat(pats[i], NT_MAX_M, P.pat[i], err);
-    if (rc) return rc;
-  }
-  if (prm->tvr_patterns) {
-    rc = parse_tokens(prm->tvr_patterns, tvrs, tvr_list, err);
-    if (rc) return rc;
-    if (tvrs.size() > NT_MAX_PAT) { err = "more than 8 unique TVR patterns"; return NT_E_LIMIT; }
-    for (size_t i = 0; i < tvrs.size(); ++i) {
-      rc = build_pat(tvrs[i], NT_MAX_TVR_M, P.tvr[i], err);
-      if (rc) return rc;
-    }
-  }
-  P.n_pat = (int32_t)pats.size();
-  P.n_tvr = (int32_t)tvrs.size();
-  P.n_pass = prm->tvr_patterns ? 3 : 2;
-  P.raw_p1 = (!pat_list && P.pat[0].fixed) ? 1 : 0;  // NanoTel.R:347-355
-  P.L = prm->subseq_length;
-  P.right_edge = prm->check_right_edge ? 1 : 0;
-  P.legacy_no_ext = prm->legacy_no_ext ? 1 : 0;
-  P.n_hits = 2 * P.n_pat + P.n_tvr;
-  P.min_density = prm->min_density;
-  // floor(p / L) by multiply-shift: l = ceil(log2 L), M = floor(2^(32+l) / L) + 1
-  // is exact for every p < 2^32 (error < 2^-l <= 1/L).
-  {
-    uint32_t l = 0;
-    while ((1ull << l) < (uint64_t)P.L) ++l;
-    P.div_s = 32 + l;
-    P.div_m = (uint64_t)((((unsigned __int128)1) << (32 + l)) / (uint64_t)P.L) + 1;
-    // 32-bit form for p < 2^31: M = floor(2^(31+l) / L) + 1 < 2^32, error < 2^-l <= 1/L
-    if (P.L >= 2) {
-      const uint64_t m32 = ((1ull << (31 + l)) / (uint64_t)P.L) + 1;
-      if (m32 > 0xFFFFFFFFull) { err = "divisor magic overflow"; return NT_E_LIMIT; }
-      P.div32_m = (uint32_t)m32;
-      P.div32_s = l - 1;
-    } else {
-      P.div32_m = 0;
-      P.div32_s = 0;
-    }
-  }
-  // Telomeric class (NanoTel.R:749-758): -5 iff !(count / width < min_density).
-  // fl(c / w) is monotone in c, so the class is count >= thr[w] with thr[w]
-  // the smallest such count -- found here with the very fp64 division R does.
-  const uint32_t wmax = (uint32_t)P.L + (uint32_t)(P.L + 1) / 2 + 1;
-  thr.assign(wmax + 1, 0);
-  for (uint32_t w = 1; w <= wmax; ++w) {
-    uint32_t c = 0;
-    while (c <= w && ((double)c / (double)w < P.min_density)) ++c;
-    thr[w] = c;  // w + 1 = never telomeric
-  }
-  P.thr_size = wmax + 1;
-  // 8-bit window counts when every window is under 256 bases: the last window
-  // (merged with a short tail by split_telo) is < 1.5 L wide
-  P.cnt8 = P.L <= 170 ? 1 : 0;
-  for (int i = 0; i < P.n_pat + P.n_tvr; ++i) {
-    NtPat& X = i < P.n_pat ? P.pat[i] : P.tvr[i - P.n_pat];
-    for (int j = 0; j < X.m; ++j)
-      for (int b = 0; b < 4; ++b) {
-        X.tm_scan[j][b] = ((X.tt_scan[j] >> b) & 1u) ? 0xFFFFFFFFu : 0u;
-        X.tm_eq[j][b] = ((X.tt_eq[j] >> b) & 1u) ? 0xFFFFFFFFu : 0u;
-      }
-    X.onehot = 1;
-    for (int j = 0; j < X.m; ++j) {
-      const uint32_t t = X.tt_scan[j];
-      if (t != 1 && t != 2 && t != 4 && t != 8) { X.onehot = 0; continue; }
-      const uint32_t c = t == 1 ? 0 : t == 2 ? 1 : t == 4 ? 2 : 3;  // base code l + 2h
-      X.xl[j] = (c & 1u) ? 0u : 0xFFFFFFFFu;
-      X.xh[j] = (c & 2u) ? 0u : 0xFFFFFFFFu;
-    }
-  }
-  return NT_OK;
-}
-
 int nt_compile(nt_ctx* ctx, const nt_params* prm, nt_program_info* info) {
   if (!ctx || !prm) return NT_E_ARG;
   NtProgram P;
@@ -617,139 +318,6 @@ int nt_compile(nt_ctx* ctx, const nt_params* prm, nt_program_info* info) {
     info->count_bytes = ctx->prog.cnt8 ? 1 : 2;
   }
   return NT_OK;
-}
-
-int nt_pack_count(const char* const* seqs, const uint64_t* lens, uint64_t n_reads,
-                  int32_t subseq_length, uint64_t* total_blocks, uint64_t* total_windows,
-                  uint64_t* total_exc, uint64_t* max_len, uint64_t* bad_read) {
-  if ((!seqs || !lens) && n_reads) return NT_E_ARG;
-  std::vector<uint64_t> exc(n_reads, 0);
-  std::vector<int> bad(n_reads, 0);
-  parallel_for(n_reads, [&](uint64_t r) {
-    const unsigned char* s = (const unsigned char*)seqs[r];
-    uint64_t e = 0;
-    int b = lens[r] == 0 ? 2 : 0;
-    uint32_t lo, hi;
-    for (uint64_t i = 0; i < lens[r] && !b;) {
-      if (i + 32 <= lens[r] && pack32(s + i, lo, hi)) {
-        i += 32;
-        continue;
-      }
-      const uint64_t end = std::min<uint64_t>(lens[r], i + 32);
-      for (; i < end && !b; ++i) {
-        if (base2(s[i]) >= 0) continue;
-        if (letter_code(s[i])) ++e; else b = 1;
-      }
-    }
-    exc[r] = e;
-    bad[r] = b;
-  });
-  uint64_t tb = 0, tw = 0, te = 0, ml = 0;
-  for (uint64_t r = 0; r < n_reads; ++r) {
-    if (bad[r]) {
-      if (bad_read) *bad_read = r;
-      return bad[r] == 2 ? NT_E_EMPTY_READ : NT_E_LETTER;
-    }
-    tb += read_blocks(lens[r]);
-    tw += NT_WIN_ROWS((uint64_t)window_count((int64_t)lens[r], subseq_length));
-    te += exc[r];
-    ml = std::max(ml, lens[r]);
-  }
-  if (total_blocks) *total_blocks = tb;
-  if (total_windows) *total_windows = tw;
-  if (total_exc) *total_exc = te;
-  if (max_len) *max_len = ml;
-  return NT_OK;
-}
-
-// The planes of one read (reverse-complemented when rc): 32 bases per step
-// on runs of plain bases, per base around anything else.  Non-ACGT letters
-// are A in the planes and, when exc_pos is given, listed at exc_pos/exc_code
-// (IUPAC code, complemented under rc).  Returns the number of non-ACGT
-// letters, or -1 if one is outside DNA_ALPHABET.
-static int64_t pack_one(const unsigned char* s, uint64_t n, int rc, uint32_t* out, uint32_t* exc_pos,
-                        uint8_t* exc_code) {
-  int64_t e = 0;
-  bool bad = false;
-  for (uint64_t blk = 0; blk * 32 < n; ++blk) {
-    uint32_t lo = 0, hi = 0;
-    if (blk * 32 + 32 <= n) {  // whole block of plain bases: 32 at a time
-      // reverse complement: base i of the block is the complement of q[31 - i]
-      const unsigned char* q = rc ? s + (n - 32 - blk * 32) : s + blk * 32;
-      if (pack32(q, lo, hi)) {
-        if (rc) {
-          lo = ~__builtin_bitreverse32(lo);
-          hi = ~__builtin_bitreverse32(hi);
-        }
-        out[2 * blk] = lo;
-        out[2 * blk + 1] = hi;
-        continue;
-      }
-    }
-    for (uint32_t i = 0; i < 32 && blk * 32 + i < n; ++i) {
-      const uint64_t pos = blk * 32 + i;
-      // reverseComplement: position pos of the RC read is the complement of n-1-pos
-      const unsigned char ch = rc ? s[n - 1 - pos] : s[pos];
-      int c = base2(ch);
-      if (c < 0) {
-        uint8_t code = letter_code(ch);
-        if (!code) bad = true;
-        if (exc_pos && code) {
-          exc_pos[e] = (uint32_t)pos;
-          exc_code[e] = rc ? complement_code(code) : code;
-        }
-        ++e;
-        c = 0;  // planes hold A at exception positions
-      } else if (rc) {
-        c = 3 - c;
-      }
-      lo |= (uint32_t)(c & 1) << i;
-      hi |= (uint32_t)((c >> 1) & 1) << i;
-    }
-    out[2 * blk] = lo;
-    out[2 * blk + 1] = hi;
-  }
-  if ((n + 31) / 32 < read_blocks(n)) {  // zero the pad block of the 64-base segment
-    out[2 * ((n + 31) / 32)] = 0u;
-    out[2 * ((n + 31) / 32) + 1] = 0u;
-  }
-  return bad ? -1 : e;
-}
-
-int nt_pack_reads(const char* const* seqs, const uint64_t* lens, uint64_t n_reads, int32_t rc,
-                  int32_t subseq_length, uint32_t* planes, uint64_t* blk_off, uint32_t* len,
-                  uint64_t* win_off, uint32_t* exc_off, uint32_t* exc_pos, uint8_t* exc_code) {
-  if (n_reads && (!seqs || !lens || !planes || !blk_off || !len || !win_off)) return NT_E_ARG;
-  // prefix sums (serial, cheap), then the per-read fill in parallel
-  std::vector<uint64_t> eoff(n_reads + 1, 0);
-  uint64_t b = 0, w = 0;
-  for (uint64_t r = 0; r < n_reads; ++r) {
-    if (lens[r] > 0xFFFFFFFFull) return NT_E_LIMIT;
-    blk_off[r] = b;
-    win_off[r] = w;
-    len[r] = (uint32_t)lens[r];
-    b += read_blocks(lens[r]);
-    w += NT_WIN_ROWS((uint64_t)window_count((int64_t)lens[r], subseq_length));
-  }
-  if (exc_off) {
-    std::vector<uint64_t> cnt(n_reads, 0);
-    parallel_for(n_reads, [&](uint64_t r) {
-      const unsigned char* s = (const unsigned char*)seqs[r];
-      cnt[r] = count_non_acgt(s, lens[r]);
-    });
-    for (uint64_t r = 0; r < n_reads; ++r) eoff[r + 1] = eoff[r] + cnt[r];
-    for (uint64_t r = 0; r <= n_reads; ++r) {
-      if (eoff[r] > 0xFFFFFFFFull) return NT_E_LIMIT;
-      exc_off[r] = (uint32_t)eoff[r];
-    }
-  }
-  std::atomic<int> bad{0};
-  parallel_for(n_reads, [&](uint64_t r) {
-    const int64_t k = pack_one((const unsigned char*)seqs[r], lens[r], rc, planes + 2 * blk_off[r],
-                               exc_off ? exc_pos + eoff[r] : nullptr, exc_off ? exc_code + eoff[r] : nullptr);
-    if (k < 0 || (k > 0 && !exc_off)) bad.store(1);
-  });
-  return bad.load() ? NT_E_LETTER : NT_OK;
 }
 
 // Read distribution of the scan (scan_reads): the 8 per-XCD queues, ~64 kb
@@ -1105,78 +673,6 @@ int nt_bundle_plan(nt_ctx* ctx, const uint32_t* len, const uint8_t* has_exc, uin
   return NT_OK;
 }
 
-// The T-layout of one bundle on the host (nt_common.h): stripes [g0, g0 +
-// nst) of tp, every word written (zeros past a read's end and in the unused
-// half of the last row when L is odd).  Block w of the 32 slots' plane words
-// -> 32 positions; position p = block k = p / L (stripe k / 64, lane k % 64),
-// offset o = p % L (row o / 2, half o % 2).
-static void tlayout_bundle(const uint32_t* planes, const uint64_t* blk_off, const uint32_t* len,
-                           const uint32_t* slots, uint64_t g0, uint64_t nst, uint32_t L, uint32_t* tp) {
-  const uint64_t T = (L + 1) / 2;
-  uint32_t* base = tp + g0 * T * 64 * 4;
-  std::memset(base, 0, nst * T * 64 * 16);
-  uint64_t n_max = 0;
-  const uint32_t* pl[NT_BUNDLE];
-  uint64_t ln[NT_BUNDLE];
-  for (int s = 0; s < NT_BUNDLE; ++s) {
-    const uint32_t r = slots[s];
-    ln[s] = r != 0xFFFFFFFFu ? len[r] : 0;
-    pl[s] = r != 0xFFFFFFFFu ? planes + 2 * blk_off[r] : nullptr;
-    n_max = std::max(n_max, ln[s]);
-  }
-  n_max = std::min<uint64_t>(n_max, nst * 64 * L);
-  alignas(32) uint32_t xl[32], xh[32], yl[32], yh[32];
-  uint64_t k = 0, o = 0;  // block and offset of position 32 w
-  for (uint64_t w = 0; 32 * w < n_max; ++w) {
-    for (int s = 0; s < NT_BUNDLE; ++s) {
-      const int64_t nb = (int64_t)ln[s] - 32 * (int64_t)w;  // valid bases of the word
-      const uint32_t m = nb >= 32 ? ~0u : nb <= 0 ? 0u : ((1u << nb) - 1u);
-      xl[s] = m ? pl[s][2 * w] & m : 0u;
-      xh[s] = m ? pl[s][2 * w + 1] & m : 0u;
-    }
-    if (g_avx2) {
-      transpose32_avx2(xl, yl);
-      transpose32_avx2(xh, yh);
-    } else {
-      transpose32_scalar(xl, yl);
-      transpose32_scalar(xh, yh);
-    }
-    const int np = (int)std::min<uint64_t>(32, n_max - 32 * w);
-    uint64_t kk = k, oo = o;
-    for (int i = 0; i < np; ++i) {
-      uint32_t* q = base + (((kk >> 6) * T + (oo >> 1)) * 64 + (kk & 63)) * 4 + 2 * (oo & 1);
-      q[0] = yl[i];
-      q[1] = yh[i];
-      if (++oo == L) {
-        oo = 0;
-        ++kk;
-      }
-    }
-    o += 32;
-    while (o >= L) {
-      o -= L;
-      ++k;
-    }
-  }
-}
-
-int nt_bundle_layout_host(const uint32_t* planes, const uint64_t* blk_off, const uint32_t* len,
-                          const uint32_t* bnd_read, const uint64_t* bnd_stripe, uint64_t n_bundles,
-                          int32_t subseq_length, uint32_t* tplanes, uint64_t tplane_bytes) {
-  if (n_bundles == 0) return NT_OK;
-  if (!planes || !blk_off || !len || !bnd_read || !bnd_stripe || !tplanes) return NT_E_ARG;
-  if (subseq_length < 1 || subseq_length > 170) return NT_E_ARG;
-  const uint64_t L = (uint64_t)subseq_length, T = (L + 1) / 2;
-  if (bnd_stripe[n_bundles] * T * 64 * 16 > tplane_bytes) return NT_E_ARG;
-  for (uint64_t b = 0; b < n_bundles; ++b)
-    if (bnd_stripe[b + 1] < bnd_stripe[b]) return NT_E_ARG;
-  parallel_for(n_bundles, [&](uint64_t b) {
-    tlayout_bundle(planes, blk_off, len, bnd_read + NT_BUNDLE * b, bnd_stripe[b], bnd_stripe[b + 1] - bnd_stripe[b],
-                   (uint32_t)L, tplanes);
-  });
-  return NT_OK;
-}
-
 int nt_bundle_layout(nt_ctx* ctx, const nt_batch* batch, uint32_t* tplanes, uint64_t tplane_bytes) {
   if (!ctx || !batch || (batch->n_bundles && !tplanes)) return NT_E_ARG;
   if (!ctx->compiled) return fail(ctx, NT_E_STATE, "nt_compile() not called");
@@ -1480,96 +976,6 @@ int nt_analyze_host(nt_ctx* ctx, const char* const* seqs, const uint64_t* lens, 
   return NT_OK;
 }
 
-int64_t nt_assign_serials(const uint8_t* is_telo, uint64_t n, double* serial_start_io,
-                          double* max_serial_io, double* serial_out, int64_t* order_out) {
-  if (!serial_start_io || !max_serial_io || (n && (!is_telo || !serial_out || !order_out)))
-    return NT_E_ARG;
-  const uint64_t groups = 8;  // groups_length (NanoTel.R:2234)
-  const double ss = *serial_start_io;
-  double mx = *max_serial_io;
-  int64_t rows = 0;
-  for (uint64_t j = 0; j < n; ++j) serial_out[j] = std::nan("");
-  auto run = [&](uint64_t first, uint64_t stride, double serial) {
-    // search_patterns: current_serial advances only on telomeric reads (NanoTel.R:2050-2070)
-    for (uint64_t j = first; j < n; j += stride) {
-      if (!is_telo[j]) continue;
-      serial_out[j] = serial;
-      order_out[rows++] = (int64_t)j;
-      if (serial > mx) mx = serial;
-      serial = serial + 1.0;
-    }
-  };
-  if (n < groups) {
-    run(0, 1, ss);  // plan(sequential) (NanoTel.R:2236-2239)
-  } else {
-    // split(1:n, f = 1:8): group g = reads g, g+8, ...; serial_start of group g is
-    // serial_start + number of reads in groups < g (NanoTel.R:2245-2252)
-    uint64_t before = 0;
-    for (uint64_t g = 0; g < groups; ++g) {
-      run(g, groups, (double)before + ss);
-      before += (n - g + groups - 1) / groups;
-    }
-  }
-  *max_serial_io = mx;
-  *serial_start_io = mx + 1.0;  // max(df_summary$Serial) + 1 (NanoTel.R:2258)
-  return rows;
-}
-
-int64_t nt_rows_columns(const int32_t* start, const int32_t* end, const double* density,
-                        const uint64_t* lens, uint64_t n_reads, int32_t n_pass,
-                        const double* serial, const int64_t* order, int64_t rows,
-                        double* col_serial, int32_t* col_length, double* col_density,
-                        int32_t* col_start, int32_t* col_end, int32_t* col_width) {
-  if (rows < 0 || n_pass < 1 || n_pass > NT_MAX_PASS) return NT_E_ARG;
-  if (rows == 0) return 0;
-  if (!start || !end || !density || !lens || !serial || !order || !col_serial || !col_length ||
-      !col_density || !col_start || !col_end || !col_width)
-    return NT_E_ARG;
-  double na_real;
-  const uint64_t na_bits = NT_NA_REAL_BITS;
-  std::memcpy(&na_real, &na_bits, sizeof na_real);
-  for (int64_t i = 0; i < rows; ++i) {
-    const int64_t j = order[i];
-    if (j < 0 || (uint64_t)j >= n_reads) return NT_E_ARG;
-    if (lens[j] > 0x7FFFFFFFull) return NT_E_LIMIT;
-    col_serial[i] = serial[j];
-    col_length[i] = (int32_t)lens[j];  // length(current_seq_unlist), integer
-    for (int p = 0; p < n_pass; ++p) {
-      const int64_t o = (int64_t)p * rows + i;
-      const int32_t s = start[3 * j + p], e = end[3 * j + p];
-      if (s == -1) {  // start(telo_position) == -1: NA columns (NanoTel.R:1926-1940)
-        col_density[o] = na_real;
-        col_start[o] = col_end[o] = col_width[o] = NT_NA_INT32;
-      } else {
-        col_density[o] = density[3 * j + p];
-        col_start[o] = s;
-        col_end[o] = e;
-        col_width[o] = (int32_t)((int64_t)e - s + 1);  // width(IRanges(s, e))
-      }
-    }
-  }
-  return rows;
-}
-
-static NtSynth to_synth(const nt_synth_params* sp) {
-  NtSynth S;
-  S.seed = sp->seed;
-  S.first_read = sp->first_read;
-  S.read_len = sp->read_len;
-  auto u24 = [](double p) {
-    if (!(p > 0)) return 0u;
-    if (p >= 1) return 1u << 24;
-    return (uint32_t)std::llround(p * 16777216.0);
-  };
-  S.p_tract_u24 = u24(sp->p_tract);
-  S.sub_u24 = u24(sp->sub_rate);
-  S.variant_u24 = u24(sp->variant_rate);
-  S.tract_min = sp->tract_min;
-  S.tract_max = std::max(sp->tract_max, sp->tract_min);
-  S.rc_layout = sp->rc_layout;
-  return S;
-}
-
 int nt_synth_device(nt_ctx* ctx, const nt_synth_params* sp, uint64_t n_reads, uint32_t* planes_dev) {
   if (!ctx || !sp || (!planes_dev && n_reads)) return NT_E_ARG;
   if (sp->read_len == 0) return fail(ctx, NT_E_ARG, "read_len must be > 0");
@@ -1588,16 +994,6 @@ int nt_uniform_layout_device(nt_ctx* ctx, uint64_t n_reads, uint64_t read_len, i
   hipError_t e = nt_dev_launch_uniform_layout(n_reads, nblk, read_len, nw, blk_off_dev, len_dev,
                                               win_off_dev, ctx->stream);
   return e == hipSuccess ? NT_OK : hip_fail(ctx, e, "launch nt_layout_kernel");
-}
-
-int nt_synth_ascii(const nt_synth_params* sp, uint64_t read_index, char* out) {
-  if (!sp || !out) return NT_E_ARG;
-  const NtSynth S = to_synth(sp);
-  const uint64_t r = S.first_read + read_index;
-  const NtSynthRead R = nt_synth_read(S, r);
-  static const char kBase[4] = {'A', 'C', 'G', 'T'};
-  for (uint64_t p = 0; p < S.read_len; ++p) out[p] = kBase[nt_synth_base(S, R, r, p)];
-  return NT_OK;
 }
 
 }  // extern "C"

@@ -13,7 +13,7 @@
 #pragma once
 #include <stdint.h>
 
-#if defined(__HIPCC__)
+#if defined(HIP_INCLUDE_HIP_HIP_RUNTIME_H)  // with the HIP runtime: host and device
 #define NT_HD __host__ __device__ __forceinline__
 #else
 #define NT_HD static inline

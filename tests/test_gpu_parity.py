@@ -183,7 +183,29 @@ def test_random_reads_specialised_call(cfg, monkeypatch):
     assert nt.call_jit(), "the specialised calling kernel did not run"
 
 
-def _random_reads(cfg, jit):
+# more than 8 patterns per list (the reference takes any number: NanoTel.R:2322-2334)
+MANY = [
+    dict(patterns="TTAGGG TCAGGG TGAGGG TTGGGG CTAGGG TTAGGC GGGTTA TTTAGG TTAGGA", tvr_patterns="TTCGGG"),
+    dict(patterns="TTAGGG TCAGGG YYAGGG TTAGG TTAGGGTTAGGG CCCTAA CCCTRA TTAGGN GGGTTAG TTGGG AAAAAAAAAA TAGGG",
+         tvr_patterns="TTAGGGTTAGGGTTAGGGTTAGGGTTAGGGTT TGAGGG"),
+]
+
+
+@pytest.mark.parametrize("cfg", MANY, ids=["9_equal_len", "12_mixed_32_letter_tvr"])
+@pytest.mark.parametrize("jit", [True, False], ids=["jit", "aot"])
+def test_many_patterns(cfg, jit):
+    nt = _random_reads(cfg, jit, check_tscan=False)
+    if jit:
+        assert nt.tscan == (cfg is MANY[0])  # equal-length lists take the bundle scan
+
+
+def test_many_patterns_specialised_call(monkeypatch):
+    monkeypatch.setenv("NT_CALL_JIT", "1")
+    nt = _random_reads(MANY[0], True, check_tscan=False)
+    assert nt.call_jit(), "the specialised calling kernel did not run"
+
+
+def _random_reads(cfg, jit, check_tscan=True):
     rng = np.random.default_rng(zlib.crc32(str(sorted(cfg.items())).encode()))
     seqs = []
     right = cfg.get("check_right_edge", False)
@@ -195,7 +217,8 @@ def _random_reads(cfg, jit):
         seqs.append(_telo_read(rng, n, motif=motif, where=where,
                                exc=0.002 if i % 5 == 0 else 0.0, lower=0.01 if i % 7 == 0 else 0.0))
     nt = _nt(jit=jit, **cfg)
-    assert nt.tscan == jit
+    if check_tscan:
+        assert nt.tscan == jit
     orow = oracle_rows(seqs, cfg["patterns"], tvr=cfg.get("tvr_patterns"), L=cfg.get("subseq_length", 100),
                        min_density=cfg.get("min_density", 0.6), right_edge=right, rc=cfg.get("rc", False))
     _check_both(nt, seqs, orow)
@@ -279,7 +302,7 @@ def test_device_synth_matches_host_generator():
         assert dev == host
 
 
-def _device_batch(nt, sp, n, read_len, L=100):
+def _device_batch(nt, sp, n, read_len, L=100, hits=True):
     """Synthetic reads generated on the device + the uniform layout (bench path)."""
     import torch
     from nanotel_amd import read_blocks, window_count, window_rows
@@ -297,7 +320,7 @@ def _device_batch(nt, sp, n, read_len, L=100):
         end=torch.empty(n * 3, dtype=torch.int32, device="cuda"),
         dens=torch.empty(n * 3, dtype=torch.float64, device="cuda"),
         flags=torch.zeros(n, dtype=torch.uint8, device="cuda"),
-        hits=torch.zeros(n * nt.n_hits, dtype=torch.int32, device="cuda"),
+        hits=torch.zeros(n * nt.n_hits if hits else 1, dtype=torch.int32, device="cuda"),
     )
     nt.synth_device(sp, n, t["planes"].data_ptr())
     nt.uniform_layout_device(n, read_len, t["blk_off"].data_ptr(), t["lens"].data_ptr(),
@@ -502,6 +525,60 @@ def test_host_tlayout_matches_device_mixed_lengths():
     nt.synchronize()
     dev = tp.cpu().numpy().view(np.uint32)
     assert np.array_equal(host, dev), np.flatnonzero(host != dev)[:8]
+
+
+# BASELINE.json configs[2], [3] (10M x 50 kb, bundle scan: planes 125 GB + the
+# T-layout 128 GB resident) and one GPU's shard of configs[4] (12.5M x 50 kb,
+# 156 GB of planes, per-read scan): the bench's full-size batches, sampled
+# against the oracle on reads regenerated on the host (nt_synth_ascii) --
+# the first and last reads (the last bundles: block offsets past 2^31,
+# T-layout words past 2^32) and reads spread over the whole batch; every row
+# field and every window count of every pass (NanoTel.R:717-766, 1080-1155).
+FULL_CONFIGS = {
+    "c3": ("YYAGGG", None, 10_000_000, 0.05, True),
+    "c4": ("TTAGGG TCAGGG", "TGAGGG TTGGGG", 10_000_000, 0.05, True),
+    "c5_shard": ("TTAGGG", None, 12_500_000, 0.0, False),
+}
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("name", list(FULL_CONFIGS))
+def test_full_size_config_sampled_vs_oracle(name):
+    import torch
+    from nanotel_amd import synth_params, synth_read_ascii
+    pats, tvr, n, var, bundle = FULL_CONFIGS[name]
+    read_len = 50_000
+    nt = _nt(patterns=pats, tvr_patterns=tvr)
+    sp = synth_params(read_len=read_len, first_read=0, variant_rate=var)
+    t = _device_batch(nt, sp, n, read_len, hits=False)
+    b = keep = None
+    if bundle:
+        b, keep = _device_bundles(nt, t, n, read_len)
+    nt.scan_call_device(t["planes"].data_ptr(), t["blk_off"].data_ptr(), t["lens"].data_ptr(),
+                        t["win_off"].data_ptr(), n, n * t["rows"], read_len, t["start"].data_ptr(),
+                        t["end"].data_ptr(), t["dens"].data_ptr(), t["flags"].data_ptr(), t["wc"].data_ptr(),
+                        bundles=b)
+    nt.synchronize()
+    flags = t["flags"]
+    assert int((flags & 0x80).eq(0).sum()) == 0, "a read was not processed"
+    n_telo = int(((flags & 1) != 0).sum())
+    # the sample: 256 first, 384 last (12 bundles), 1400 spread over the batch
+    idx = np.unique(np.concatenate([np.arange(256), np.arange(n - 384, n),
+                                    np.linspace(256, n - 385, 1400).astype(np.int64)]))
+    it = torch.from_numpy(idx).cuda()
+    res = {"start": t["start"].view(n, 3)[it].cpu().numpy(), "end": t["end"].view(n, 3)[it].cpu().numpy(),
+           "density": t["dens"].view(n, 3)[it].cpu().numpy(), "flags": flags[it].cpu().numpy()}
+    res["telomeric"] = (res["flags"] & 1) != 0
+    rows = t["rows"]
+    res["win_counts"] = t["wc"].view(n, nt.n_pass * rows)[it].cpu().numpy().view(nt.count_dtype).reshape(-1)
+    res["win_off"] = np.arange(idx.size, dtype=np.int64) * rows
+    res["n_windows"] = np.full(idx.size, t["nw"], np.int64)
+    del t, keep, it
+    torch.cuda.empty_cache()
+    seqs = [synth_read_ascii(sp, int(i)) for i in idx]
+    compare(nt, res, oracle_rows(seqs, pats, tvr=tvr, want_hits=False), check_hits=False)
+    assert res["telomeric"].sum() > idx.size // 4 and n_telo > n // 4
+    nt.close()
 
 
 def test_odd_block_offset_is_reported():
