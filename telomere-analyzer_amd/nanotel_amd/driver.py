@@ -5,7 +5,7 @@ Mirrors run_future_worker_chuncks + the main script of NanoTel.R
 scan + call every chunk on the GPU (one nt_analyze_host per chunk, which
 replaces the 8 forked search_patterns of NanoTel.R:2234-2258), assign serials
 (A15), write reads/<serial>.fasta.gz for telomeric reads (NanoTel.R:1869-1873),
-then <basename>_summary.csv, reads_ids.txt and run.log (NanoTel.R:2340-2433).
+then <basename>_summary.csv, reads_ids.txt and log/run.log (NanoTel.R:2340-2433).
 
 With torch.distributed initialised (one process per GPU), chunks are dealt
 round-robin to ranks and the serials are fixed by one all_reduce (shard.py);
@@ -26,6 +26,8 @@ from . import plots, shard
 from .analysis import write_analysis
 from .api import NanoTel, rows_columns
 from .io import Reader, csv_field, format_double, format_int, r_as_character, write_fasta_gz
+from .runlog import RunLog, r_time
+from . import __version__
 
 VERSION = "Telomere Analyzer  version v1.1.9-beta 2026-02-19"
 
@@ -83,14 +85,46 @@ def write_summary_csv(path, rows, tvr, sci_threshold=None):
             f.write(format_row(r, sci_threshold) + "\n")
 
 
-def _summary_stats(v):
-    """R summary(): Min, 1st Qu., Median, Mean, 3rd Qu., Max (type-7 quantiles)."""
-    v = np.asarray([x for x in v if x is not None], np.float64)
-    if v.size == 0:
-        return "no values"
-    q = np.quantile(v, [0, 0.25, 0.5, 0.75, 1.0])
-    return (f"Min. {q[0]:g}  1st Qu. {q[1]:g}  Median {q[2]:g}  Mean {v.mean():g}  "
-            f"3rd Qu. {q[3]:g}  Max. {q[4]:g}")
+def _write_run_log(save_path, t0, input_path, files, patterns, tvr_patterns, rc, subseq_length, min_density,
+                   lengths, rows, tvr):
+    """<save_path>/log/run.log: the messages of NanoTel.R:2347-2427 and 2510-2514
+    in logr's layout (runlog.py), in the order the reference prints them."""
+    import torch
+    log = RunLog(save_path, t0, versions=f"nanotel_amd {__version__}; torch {torch.__version__}; "
+                                         f"HIP {getattr(torch.version, 'hip', None)}")
+    log.print(VERSION)
+    log.print(f"Work started at: {r_time(t0)}")
+    log.print("############### The input argumetns for this run: ################")
+    if rc:
+        log.print("Reverse complement was applied on the input reads.")
+    log.print(f"The patterns to search: {patterns}")
+    log.print(f"The sub-sequence length  is: {subseq_length}")
+    log.print(f"The minimal density for a telomeric subseq: {r_as_character(float(min_density))}")
+    if tvr:
+        log.print(f"Additional Telomere variant repeats patterns were added: {tvr_patterns}")
+    log.print("##################################################################")
+    log.print("The input files:")
+    for p in (files if os.path.isdir(input_path) else [input_path]):
+        log.print(p)
+    n = int(lengths.size)
+    log.print(f"Total reads in sample: {n}")
+    log.print("Summary statistics of the sample reads length:")
+    log.summary([int(x) for x in lengths])
+    log.print(f"Number of reads which identified as Telomeric: {len(rows)}")
+    pct = r_as_character(round(100 * len(rows) / n, 2)) if n else "NaN"
+    log.print(f"% of total reads: {pct}%")
+    log.print("Summary statistics for the Telomeric reads:")
+    log.print("reads length:")
+    log.summary([r[2] for r in rows])
+    log.print("Telomere length:")
+    log.summary([r[6] for r in rows])
+    log.print("Telomere length with 1 mismatch allowed:")
+    log.summary([r[10] for r in rows])
+    if tvr:
+        log.print("Telomere length with 1 mismatch allowed + tvr patterns.:")
+        log.summary([r[14] for r in rows])
+    log.print(f"Work ended at: {r_time()}")
+    log.close()  # log_close(footer = FALSE)
 
 
 def _write_read(path, name, seq, rc):
@@ -379,31 +413,6 @@ def run(input_path, save_path, patterns, fmt="fastq", nrec=10000, rc=False, min_
             f.write(r[1] + "\n")
     if analysis:  # --analysis post-processing (NanoTel.R:2437-2508)
         write_analysis(save_path, barcode, rows, columns(tvr), format_row, sci_threshold)
-    with open(os.path.join(save_path, "run.log"), "w") as f:
-        f.write(VERSION + "\n")
-        f.write(f"Work started at: {time.strftime('%Y-%m-%d %H:%M:%S', time.localtime(t0))}\n")
-        f.write("############### The input argumetns for this run: ################\n")
-        if rc:
-            f.write("Reverse complement was applied on the input reads.\n")
-        f.write(f"The patterns to search: {patterns}\n")
-        f.write(f"The sub-sequence length  is: {subseq_length}\n")
-        f.write(f"The minimal density for a telomeric subseq: {min_density}\n")
-        if tvr:
-            f.write(f"Additional Telomere variant repeats patterns were added: {tvr_patterns}\n")
-        f.write("##################################################################\n")
-        f.write("The input files:\n")
-        for p in files:
-            f.write(p + "\n")
-        f.write(f"Total reads in sample: {lengths.size}\n")
-        f.write(f"Summary statistics of the sample reads length: {_summary_stats(lengths)}\n")
-        f.write(f"Number of reads which identified as Telomeric: {len(rows)}\n")
-        pct = round(100 * len(rows) / lengths.size, 2) if lengths.size else float("nan")
-        f.write(f"% of total reads: {pct}%\n")
-        f.write(f"Telomere length: {_summary_stats([r[6] for r in rows])}\n")
-        f.write(f"Telomere length with 1 mismatch allowed: {_summary_stats([r[10] for r in rows])}\n")
-        if tvr:
-            f.write("Telomere length with 1 mismatch allowed + tvr patterns.: "
-                    f"{_summary_stats([r[14] for r in rows])}\n")
-        f.write(f"Work ended at: {time.strftime('%Y-%m-%d %H:%M:%S')} "
-                f"({time.time() - t0:.1f} s, {world} GPU(s))\n")
+    _write_run_log(save_path, t0, input_path, files, patterns, tvr_patterns, rc, subseq_length, min_density,
+                   lengths, rows, tvr)
     return rows, lengths
