@@ -216,6 +216,11 @@ int nt_analyze_host(nt_ctx* ctx, const char* const* seqs, const uint64_t* lens, 
                     int32_t* start, int32_t* end, double* density, uint8_t* flags,
                     void* win_counts, uint32_t* hits);
 
+/* Host-path phase times of the context's nt_analyze_host calls (seconds,
+ * cumulative): [0] layout of the batch, [1] 2-bit packing, [2] T-layout,
+ * [3] uploads enqueued, [4] device work + downloads, [5] row checks. */
+int nt_host_times(const nt_ctx* ctx, double* t6);
+
 /* --- --use_filter pre-filter ----------------------------------------------
  * Replaces filter_reads(samples, patterns, do_rc = FALSE, right_edge) +
  * filter_density (NanoTel.R:2083-2103, 2121-2163) as called per chunk from

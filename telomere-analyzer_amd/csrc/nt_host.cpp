@@ -146,7 +146,14 @@ struct nt_ctx {
   DevBuf wc, start, end, dens, flags, hits, scratch, tmask, thr, queue;
   DevBuf tplanes, bnd_read, bnd_stripe, list;  // upload_reads' bundle layout
   HostBuf h_planes, h_meta, h_tplanes;  // upload_reads staging
+  // host-path phase times (s, cumulative; nt_host_times): layout, pack,
+  // T-layout, uploads, the device work and downloads, the row checks
+  double host_t[6] = {};
 };
+
+static double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
 
 static int fail(nt_ctx* ctx, int code, const std::string& msg) {
   if (ctx) ctx->err = msg;
@@ -766,6 +773,12 @@ static int upload_reads(nt_ctx* ctx, const char* const* seqs, const uint64_t* le
   // the layout depends on the lengths only: blk_off | win_off | len straight
   // into pinned staging, then ONE pass over the letters packs the planes
   // (nt_pack_count + nt_pack_reads read them twice)
+  double tp = now_s();
+  auto lap = [&](int k) {
+    const double t = now_s();
+    ctx->host_t[k] += t - tp;
+    tp = t;
+  };
   const size_t meta_bytes = n_reads * (8 + 8 + 4);
   if ((e = ctx->h_meta.ensure(meta_bytes)) != hipSuccess) return hip_fail(ctx, e, "hipHostMalloc(meta)");
   uint64_t* h_blk = (uint64_t*)ctx->h_meta.p;
@@ -786,6 +799,7 @@ static int upload_reads(nt_ctx* ctx, const char* const* seqs, const uint64_t* le
   uint32_t* hp = (uint32_t*)ctx->h_planes.p;
   hp[pw - 2] = hp[pw - 1] = 0u;
   const int rc_flag = ctx->params.rc;
+  lap(0);
   std::vector<int64_t> cnt(n_reads);
   parallel_for(n_reads, [&](uint64_t r) {
     cnt[r] = pack_one((const unsigned char*)seqs[r], lens[r], rc_flag, hp + 2 * h_blk[r], nullptr, nullptr);
@@ -815,6 +829,7 @@ static int upload_reads(nt_ctx* ctx, const char* const* seqs, const uint64_t* le
                  h_ecode.data() + h_eoff[r]);
     });
   }
+  lap(1);
 #define NT_UP_PTR(buf, ptr, bytes)                                                           \
   e = ctx->buf.ensure(bytes);                                                                \
   if (e != hipSuccess) return hip_fail(ctx, e, "hipMalloc(" #buf ")");                       \
@@ -853,10 +868,12 @@ static int upload_reads(nt_ctx* ctx, const char* const* seqs, const uint64_t* le
     h_list.resize(nl);
   }
   if (nb) {
+    lap(3);
     if ((e = ctx->h_tplanes.ensure(tpb)) != hipSuccess) return hip_fail(ctx, e, "hipHostMalloc(tplanes)");
     int rc = nt_bundle_layout_host(hp, h_blk, h_len, h_bread.data(), h_bstripe.data(), nb, L,
                                    (uint32_t*)ctx->h_tplanes.p, tpb);
     if (rc) return fail(ctx, rc, "nt_bundle_layout_host");
+    lap(2);
     NT_UP_PTR(tplanes, ctx->h_tplanes.p, tpb);
     NT_UP(bnd_read, h_bread);
     NT_UP(bnd_stripe, h_bstripe);
@@ -875,6 +892,7 @@ static int upload_reads(nt_ctx* ctx, const char* const* seqs, const uint64_t* le
                 nb ? (const uint32_t*)ctx->bnd_read.p : nullptr,
                 nb ? (const uint64_t*)ctx->bnd_stripe.p : nullptr, nb,
                 nl && nb ? (const uint32_t*)ctx->list.p : nullptr, nb ? nl : 0};
+  lap(3);
   *max_len = ml;
   return NT_OK;
 }
@@ -946,6 +964,7 @@ int nt_analyze_host(nt_ctx* ctx, const char* const* seqs, const uint64_t* lens, 
   if ((e = ctx->hits.ensure(std::max<uint64_t>(1, nh) * 4)) != hipSuccess) return hip_fail(ctx, e, "hipMalloc(hits)");
   nt_out O{ctx->wc.p, (int32_t*)ctx->start.p, (int32_t*)ctx->end.p,
            (double*)ctx->dens.p, (uint8_t*)ctx->flags.p, hits ? (uint32_t*)ctx->hits.p : nullptr};
+  double t0 = now_s();
   rc = nt_scan_call(ctx, &B, &O, ml);
   if (rc) return rc;
   std::vector<uint8_t> h_flags(n_reads);
@@ -961,6 +980,8 @@ int nt_analyze_host(nt_ctx* ctx, const char* const* seqs, const uint64_t* lens, 
 #undef NT_DOWN
   e = hipStreamSynchronize(ctx->stream);
   if (e != hipSuccess) return hip_fail(ctx, e, "hipStreamSynchronize");
+  const double t1 = now_s();
+  ctx->host_t[4] += t1 - t0;
   if (flags) std::memcpy(flags, h_flags.data(), n_reads);
   for (uint64_t r = 0; r < n_reads; ++r) {
     const uint8_t f = h_flags[r];
@@ -973,6 +994,13 @@ int nt_analyze_host(nt_ctx* ctx, const char* const* seqs, const uint64_t* lens, 
     if (f & NT_FLAG_ERR_WIDTH)
       return fail(ctx, NT_E_NEG_WIDTH, "read " + std::to_string(r) + ": negative IRanges width");
   }
+  ctx->host_t[5] += now_s() - t1;
+  return NT_OK;
+}
+
+int nt_host_times(const nt_ctx* ctx, double* t6) {
+  if (!ctx || !t6) return NT_E_ARG;
+  for (int i = 0; i < 6; ++i) t6[i] = ctx->host_t[i];
   return NT_OK;
 }
 

@@ -107,6 +107,7 @@ SIGNATURES = {
     "nt_call_jit_wait": (ctypes.c_int, [_P]),
     "nt_jit_prebuild": (ctypes.c_int, [ctypes.POINTER(NtParams), ctypes.c_char_p]),
     "nt_analyze_host": (ctypes.c_int, [_P, _P, _P, ctypes.c_uint64, _P, _P, _P, _P, _P, _P]),
+    "nt_host_times": (ctypes.c_int, [_P, _P]),
     "nt_filter_call": (ctypes.c_int, [_P, _P, _P]),
     "nt_filter_host": (ctypes.c_int, [_P, _P, _P, ctypes.c_uint64, _P]),
     "nt_assign_serials": (ctypes.c_int64, [_P, ctypes.c_uint64, ctypes.POINTER(ctypes.c_double),

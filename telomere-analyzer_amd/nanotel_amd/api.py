@@ -116,6 +116,12 @@ class NanoTel:
         the patterns (hiprtc), False for the ahead-of-time one."""
         return bool(lib().nt_call_jit_state(self._h))
 
+    def host_times(self):
+        """nt_host_times: cumulative seconds of the host path's phases."""
+        t = np.zeros(6, np.float64)
+        _check(lib().nt_host_times(self._h, t.ctypes.data), self._h)
+        return dict(zip(("layout", "pack", "tlayout", "upload", "device", "checks"), t.tolist()))
+
     def call_jit_wait(self):
         """Wait for the background build of the calling kernel specialised for
         the patterns (started by nt_compile); True when it is available."""

@@ -273,8 +273,9 @@ def _targets(ser, order):
 def run(input_path, save_path, patterns, fmt="fastq", nrec=10000, rc=False, min_density=0.6,
         subseq_length=100, check_right_edge=False, tvr_patterns=None, legacy_no_ext=False,
         device=0, write_reads=True, sci_threshold=None, use_filter=False, analysis=False,
-        plot=True, plot_jpeg=True, log=print):
-    """Run the pipeline; returns (summary rows, all read lengths) on rank 0."""
+        plot=True, plot_jpeg=True, log=print, stats=None):
+    """Run the pipeline; returns (summary rows, all read lengths) on rank 0.
+    stats: a dict filled with the run's phase times (seconds)."""
     import torch.distributed as dist
     dist_on = dist.is_available() and dist.is_initialized()
     rank = dist.get_rank() if dist_on else 0
@@ -315,6 +316,7 @@ def run(input_path, save_path, patterns, fmt="fastq", nrec=10000, rc=False, min_
     # every rank at the same group instead of leaving them blocked in the next
     # collective).  Every rank reads the same stream, so the groups' extents
     # (the rounds, the bases cap) agree.
+    tm = {"read_wait": 0.0, "scan": 0.0, "rows_files": 0.0, "collectives": 0.0}
     while True:
         own = []  # (chunk's place in the group, chunk)
         n_grp, ended = 0, False
@@ -322,7 +324,9 @@ def run(input_path, save_path, patterns, fmt="fastq", nrec=10000, rc=False, min_
             bases = 0
             for _ in range(g):
                 for r in range(world):
+                    tr = time.perf_counter()
                     ch = src.next_chunk()
+                    tm["read_wait"] += time.perf_counter() - tr
                     if ch is None:
                         ended = True
                         break
@@ -334,16 +338,21 @@ def run(input_path, save_path, patterns, fmt="fastq", nrec=10000, rc=False, min_
                     n_grp += 1
                 if ended or bases >= kGroupBases * world:
                     break
+            ts = time.perf_counter()
             scanned = _scan_group(nt, [ch for _, ch in own], use_filter, write_reads, log, want_windows=plot)
+            tm["scan"] += time.perf_counter() - ts
         except Exception as ex:  # noqa: BLE001 -- re-raised after the collective
             failure, scanned = ex, []
         local = {own[i][0]: scanned[i][2] for i in range(len(scanned))}
+        tc = time.perf_counter()
         maxima, failed = shard.exchange_rel_max(local, g * world, device=coll_dev, failed=failure is not None)
+        tm["collectives"] += time.perf_counter() - tc
         if failed:
             break
         starts = np.empty(n_grp, np.float64)
         for r in range(n_grp):  # the reference's recurrence, chunk by chunk
             starts[r], s_next, m_run = shard.advance(s_next, m_run, float(maxima[r]))
+        tw = time.perf_counter()
         try:
             for (pos, _), (rel, order, _, res, name_of, lens, seqs) in zip(own, scanned):
                 if res is None:
@@ -372,6 +381,7 @@ def run(input_path, save_path, patterns, fmt="fastq", nrec=10000, rc=False, min_
                     pending += [pool.submit(plots.write_read_plots, *a, jpeg=plot_jpeg, **kw) for a, kw in jobs]
         except Exception as ex:  # noqa: BLE001
             failure = ex
+        tm["rows_files"] += time.perf_counter() - tw
         k += n_grp
         if ended:
             break
@@ -401,6 +411,10 @@ def run(input_path, save_path, patterns, fmt="fastq", nrec=10000, rc=False, min_
             raise failure
         raise RuntimeError("NanoTel: another rank failed (see its error)")
     rows = shard.gather_rows(local_rows)
+    if stats is not None:
+        stats.update(tm)
+        stats.update({"host_" + k: v for k, v in nt.host_times().items()} if hasattr(nt, "host_times") else {})
+        stats["groups_rounds"] = g
     rdr.close()
     nt.close()
     if rank != 0:
@@ -415,4 +429,6 @@ def run(input_path, save_path, patterns, fmt="fastq", nrec=10000, rc=False, min_
         write_analysis(save_path, barcode, rows, columns(tvr), format_row, sci_threshold)
     _write_run_log(save_path, t0, input_path, files, patterns, tvr_patterns, rc, subseq_length, min_density,
                    lengths, rows, tvr)
+    if stats is not None:
+        stats["total"] = time.time() - t0
     return rows, lengths

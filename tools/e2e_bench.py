@@ -84,10 +84,12 @@ def main():
     for key, write_reads, plot in runs:
         save = os.path.join(a.dir, "out_" + key)
         t = time.perf_counter()
+        st = {}
         rows, _ = driver.run(inp, save, "TTAGGG", fmt="fastq", nrec=a.nrec, write_reads=write_reads,
-                             plot=plot, log=lambda *x: None)
+                             plot=plot, log=lambda *x: None, stats=st)
         s = time.perf_counter() - t
-        out[key] = {"seconds": round(s, 3), "Gbases_per_s": round(bases / s / 1e9, 3), "rows": len(rows)}
+        out[key] = {"seconds": round(s, 3), "Gbases_per_s": round(bases / s / 1e9, 3), "rows": len(rows),
+                    "phases_s": {k: round(v, 4) for k, v in st.items()}}
     print(json.dumps(out))
 
 
