@@ -266,6 +266,20 @@ int64_t nt_rows_columns(const int32_t* start, const int32_t* end, const double* 
                         double* col_serial, int32_t* col_length, double* col_density,
                         int32_t* col_start, int32_t* col_end, int32_t* col_width);
 
+/* The same rows as text: summary.csv lines (write_csv, NanoTel.R:2430-2432;
+ * readr's formatting restated -- shortest round-trip doubles, integral values
+ * bare, NA, Inf, quoted names; sci_threshold > 0: integral Serials at or
+ * above it as "<digits>e<zeros>", parity unpinned) and, when ids_out is given,
+ * reads_ids.txt lines (write_lines, :2433).  names[i] / name_lens[i]: row i's
+ * sequence_ID.  Returns the CSV bytes written (ids bytes in *ids_bytes), or
+ * NT_E_LIMIT when a buffer is too small (2 * name + 3 + (3 + 4 n_pass) * 40
+ * bytes a row always suffice). */
+int64_t nt_rows_csv(const double* col_serial, const int32_t* col_length, const double* col_density,
+                    const int32_t* col_start, const int32_t* col_end, const int32_t* col_width,
+                    int64_t rows, int32_t n_pass, const char* const* names, const uint64_t* name_lens,
+                    double sci_threshold, char* csv_out, uint64_t csv_cap, char* ids_out,
+                    uint64_t ids_cap, uint64_t* ids_bytes);
+
 /* --- host ingest: FASTA/FASTQ(.gz) in nrec-record chunks ------------------ */
 /* readDNAStringSet(open_input_files(path), nrec, format) (NanoTel.R:2171-2216):
  * path = a file or a directory (files listed recursively, sorted, read as one

@@ -13,6 +13,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <future>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -67,6 +68,43 @@ namespace {
 
 constexpr uint32_t kLdsCapBytes = 64 * 1024;  // per 4-wave workgroup; longer reads: global scratch
 
+// Process-wide pool of pinned host buffers: pinning (hipHostMalloc) costs
+// milliseconds per 100 MB, so the staging of a destroyed context serves the
+// next one (up to kMax bytes kept; never freed at exit, after HIP's teardown).
+struct PinnedPool {
+  static constexpr size_t kMax = 16ull << 30;
+  std::mutex mu;
+  std::vector<std::pair<void*, size_t>> free;
+  size_t bytes = 0;
+  void* take(size_t want, size_t& cap) {
+    std::lock_guard<std::mutex> lk(mu);
+    size_t best = free.size();
+    for (size_t i = 0; i < free.size(); ++i)
+      if (free[i].second >= want && (best == free.size() || free[i].second < free[best].second)) best = i;
+    if (best == free.size()) return nullptr;
+    void* p = free[best].first;
+    cap = free[best].second;
+    bytes -= cap;
+    free.erase(free.begin() + (ptrdiff_t)best);
+    return p;
+  }
+  void give(void* p, size_t cap) {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      if (bytes + cap <= kMax) {
+        free.emplace_back(p, cap);
+        bytes += cap;
+        return;
+      }
+    }
+    (void)hipHostFree(p);
+  }
+};
+PinnedPool& pinned_pool() {
+  static PinnedPool* p = new PinnedPool;
+  return *p;
+}
+
 // Pinned host staging (hipHostMalloc), kept across calls: no page faults or
 // zero-fill per call and the uploads are DMA from page-locked memory.
 struct HostBuf {
@@ -74,16 +112,17 @@ struct HostBuf {
   size_t cap = 0;
   hipError_t ensure(size_t bytes) {
     if (bytes <= cap) return hipSuccess;
-    if (p) (void)hipHostFree(p);
+    if (p) pinned_pool().give(p, cap);
     p = nullptr;
     cap = 0;
     const size_t want = std::max<size_t>(bytes + bytes / 4, 4096);  // some headroom for the next chunk
+    if ((p = pinned_pool().take(bytes, cap))) return hipSuccess;
     hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
     if (e == hipSuccess) cap = want;
     return e;
   }
   ~HostBuf() {
-    if (p) (void)hipHostFree(p);
+    if (p) pinned_pool().give(p, cap);
   }
 };
 

@@ -584,7 +584,13 @@ int nt_reader_open(const char* path, int format, nt_reader** out) {
 void nt_reader_close(nt_reader* r) {
   if (!r) return;
   close_source(r);
-  delete r;
+  // unmapping a large input (the page tables of gigabytes) takes milliseconds:
+  // done off the caller's path (NT_READER_SYNC_CLOSE: here, e.g. for leak checks)
+  if (std::getenv("NT_READER_SYNC_CLOSE")) {
+    delete r;
+    return;
+  }
+  std::thread([r] { delete r; }).detach();
 }
 
 uint64_t nt_reader_file_count(const nt_reader* r) { return r ? r->files.size() : 0; }

@@ -9,6 +9,7 @@
 #include <immintrin.h>
 
 #include <algorithm>
+#include <charconv>
 #include <atomic>
 #include <cmath>
 #include <cstdio>
@@ -446,6 +447,105 @@ NtSynth to_synth(const nt_synth_params* sp) {
 }
 
 
+// ---- summary.csv number formatting (write_csv of readr 2.1.4, restated:
+// parity unpinned beyond Example_output; nanotel_amd/io.py format_double is
+// the same rules in Python): NA; Inf / -Inf; integral values below 1e15 as
+// integers (or "<digits>e<zeros>" at or above sci_threshold when that is > 0);
+// else the shortest round-trip decimal, fixed for exponents -4..15, else
+// "<mantissa>e<exponent>" (no '+', no zero padding).
+static char* put_double(char* o, double x, double sci_threshold) {
+  if (std::isnan(x)) {
+    std::memcpy(o, "NA", 2);
+    return o + 2;
+  }
+  if (std::isinf(x)) {
+    const char* t = x > 0 ? "Inf" : "-Inf";
+    const size_t n = std::strlen(t);
+    std::memcpy(o, t, n);
+    return o + n;
+  }
+  if (x == std::floor(x) && std::fabs(x) < 1e15) {
+    long long i = (long long)x;
+    if (sci_threshold > 0 && (double)std::llabs(i) >= sci_threshold && i % 10 == 0) {
+      if (i < 0) *o++ = '-';
+      unsigned long long u = (unsigned long long)std::llabs(i);
+      int z = 0;
+      while (u % 10 == 0) {
+        u /= 10;
+        ++z;
+      }
+      o = std::to_chars(o, o + 24, u).ptr;
+      *o++ = 'e';
+      return std::to_chars(o, o + 8, z).ptr;
+    }
+    return std::to_chars(o, o + 24, i).ptr;
+  }
+  char b[40];
+  const auto r = std::to_chars(b, b + sizeof b, x, std::chars_format::scientific);  // shortest round trip
+  *r.ptr = 0;
+  // b = [-]d[.ddd]e(+|-)XX
+  const char* p = b;
+  if (*p == '-') *o++ = *p++;
+  char dig[24];
+  int nd = 0;
+  while (*p && *p != 'e') {
+    if (*p != '.') dig[nd++] = *p;
+    ++p;
+  }
+  const int ex = std::atoi(p + 1);
+  if (ex >= -4 && ex < 16) {  // Python repr's fixed range
+    if (ex < 0) {
+      *o++ = '0';
+      *o++ = '.';
+      for (int k = 0; k < -ex - 1; ++k) *o++ = '0';
+      std::memcpy(o, dig, nd);
+      return o + nd;
+    }
+    for (int k = 0; k <= ex; ++k) *o++ = k < nd ? dig[k] : '0';
+    *o++ = '.';
+    if (nd > ex + 1) {
+      std::memcpy(o, dig + ex + 1, nd - ex - 1);
+      return o + (nd - ex - 1);
+    }
+    *o++ = '0';
+    return o;
+  }
+  *o++ = dig[0];
+  if (nd > 1) {
+    *o++ = '.';
+    std::memcpy(o, dig + 1, nd - 1);
+    o += nd - 1;
+  }
+  *o++ = 'e';
+  return std::to_chars(o, o + 8, ex).ptr;
+}
+
+static char* put_int(char* o, int32_t v) {
+  if (v == NT_NA_INT32) {
+    std::memcpy(o, "NA", 2);
+    return o + 2;
+  }
+  return std::to_chars(o, o + 16, v).ptr;
+}
+
+// readr's quoting: a field with the delimiter, a quote or a line break is
+// quoted, quotes doubled
+static char* put_field(char* o, const char* s, uint64_t n) {
+  bool q = false;
+  for (uint64_t i = 0; i < n && !q; ++i) q = s[i] == ',' || s[i] == '"' || s[i] == '\n' || s[i] == '\r';
+  if (!q) {
+    std::memcpy(o, s, n);
+    return o + n;
+  }
+  *o++ = '"';
+  for (uint64_t i = 0; i < n; ++i) {
+    if (s[i] == '"') *o++ = '"';
+    *o++ = s[i];
+  }
+  *o++ = '"';
+  return o;
+}
+
 }  // namespace nt_host
 
 using namespace nt_host;
@@ -638,3 +738,47 @@ int nt_synth_ascii(const nt_synth_params* sp, uint64_t read_index, char* out) {
 }
 
 }  // extern "C"
+
+extern "C" int64_t nt_rows_csv(const double* col_serial, const int32_t* col_length, const double* col_density,
+                               const int32_t* col_start, const int32_t* col_end, const int32_t* col_width,
+                               int64_t rows, int32_t n_pass, const char* const* names, const uint64_t* name_lens,
+                               double sci_threshold, char* csv_out, uint64_t csv_cap, char* ids_out,
+                               uint64_t ids_cap, uint64_t* ids_bytes) {
+  if (rows < 0 || n_pass < 1 || n_pass > NT_MAX_PASS || !csv_out) return NT_E_ARG;
+  if (rows && (!col_serial || !col_length || !col_density || !col_start || !col_end || !col_width || !names ||
+               !name_lens))
+    return NT_E_ARG;
+  char* o = csv_out;
+  char* const oe = csv_out + csv_cap;
+  char* d = ids_out;
+  for (int64_t i = 0; i < rows; ++i) {
+    // room for the longest row this can write: the name quoted and doubled, 3 + 4 n_pass fields
+    const uint64_t need = 2 * name_lens[i] + 3 + (uint64_t)(3 + 4 * n_pass) * 40;
+    if ((uint64_t)(oe - o) < need) return NT_E_LIMIT;
+    o = put_double(o, col_serial[i], sci_threshold);
+    *o++ = ',';
+    o = put_field(o, names[i], name_lens[i]);
+    *o++ = ',';
+    o = put_int(o, col_length[i]);
+    for (int p = 0; p < n_pass; ++p) {
+      const int64_t k = (int64_t)p * rows + i;
+      *o++ = ',';
+      o = put_double(o, col_density[k], 0.0);  // densities: never the integral sci form
+      *o++ = ',';
+      o = put_int(o, col_start[k]);
+      *o++ = ',';
+      o = put_int(o, col_end[k]);
+      *o++ = ',';
+      o = put_int(o, col_width[k]);
+    }
+    *o++ = '\n';
+    if (ids_out) {
+      if ((uint64_t)(d - ids_out) + name_lens[i] + 1 > ids_cap) return NT_E_LIMIT;
+      std::memcpy(d, names[i], name_lens[i]);
+      d += name_lens[i];
+      *d++ = '\n';
+    }
+  }
+  if (ids_bytes) *ids_bytes = ids_out ? (uint64_t)(d - ids_out) : 0;
+  return (int64_t)(o - csv_out);
+}

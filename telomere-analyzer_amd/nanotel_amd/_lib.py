@@ -114,6 +114,8 @@ SIGNATURES = {
                                            ctypes.POINTER(ctypes.c_double), _P, _P]),
     "nt_rows_columns": (ctypes.c_int64, [_P, _P, _P, _P, ctypes.c_uint64, ctypes.c_int32, _P, _P,
                                          ctypes.c_int64, _P, _P, _P, _P, _P, _P]),
+    "nt_rows_csv": (ctypes.c_int64, [_P, _P, _P, _P, _P, _P, ctypes.c_int64, ctypes.c_int32, _P, _P,
+                                     ctypes.c_double, _P, ctypes.c_uint64, _P, ctypes.c_uint64, _U64P]),
     "nt_reader_open": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
     "nt_reader_close": (None, [_P]),
     "nt_reader_file_count": (ctypes.c_uint64, [_P]),

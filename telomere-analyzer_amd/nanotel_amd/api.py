@@ -376,3 +376,27 @@ def rows_columns(res, lengths, serials, order, n_pass):
         out[k] = out[k][..., :rows]
     out["na"] = out["start"] == NA_INT32
     return out
+
+
+def rows_csv(cols, name_ptrs, name_lens, n_pass, sci_threshold=None, ids=True):
+    """nt_rows_csv: (summary.csv lines, reads_ids.txt lines) as bytes for the
+    columns of rows_columns(); name_ptrs / name_lens: each row's sequence_ID
+    (host addresses and lengths, in row order)."""
+    rows = int(cols["serial"].size)
+    if rows == 0:
+        return b"", b""
+    name_ptrs = np.ascontiguousarray(name_ptrs, np.uint64)
+    name_lens = np.ascontiguousarray(name_lens, np.uint64)
+    cap = int(2 * name_lens.sum()) + rows * (3 + (3 + 4 * n_pass) * 40)
+    out = np.empty(cap, np.uint8)
+    ids_out = np.empty(int(name_lens.sum()) + rows, np.uint8) if ids else None
+    ib = ctypes.c_uint64()
+    c = {k: np.ascontiguousarray(cols[k]) for k in ("serial", "length", "density", "start", "end", "width")}
+    n = lib().nt_rows_csv(c["serial"].ctypes.data, c["length"].ctypes.data, c["density"].ctypes.data,
+                          c["start"].ctypes.data, c["end"].ctypes.data, c["width"].ctypes.data, rows, int(n_pass),
+                          name_ptrs.ctypes.data, name_lens.ctypes.data,
+                          float(sci_threshold) if sci_threshold else 0.0, out.ctypes.data, cap,
+                          None if ids_out is None else ids_out.ctypes.data, 0 if ids_out is None else ids_out.size,
+                          ctypes.byref(ib))
+    _check(n)
+    return out[:n].tobytes(), (ids_out[:ib.value].tobytes() if ids_out is not None else b"")

@@ -24,7 +24,7 @@ import numpy as np
 
 from . import plots, shard
 from .analysis import write_analysis
-from .api import NanoTel, rows_columns
+from .api import NanoTel, rows_columns, rows_csv
 from .io import Reader, csv_field, format_double, format_int, r_as_character, write_fasta_gz
 from .runlog import RunLog, r_time
 from . import __version__
@@ -67,6 +67,54 @@ def chunk_rows(res, names, lengths, serials, order, n_pass):
                         int(c["width"][p, i])]
         rows.append(row)
     return rows
+
+
+class ChunkRows:
+    """One chunk's summary rows: their summary.csv and reads_ids.txt lines
+    (nt_rows_csv, C++) and their columns (nt_rows_columns) -- what the ranks
+    gather to rank 0 (pickled, in chunk order)."""
+
+    def __init__(self, csv, ids, cols):
+        self.csv, self.ids, self.cols = csv, ids, cols
+
+    def __len__(self):
+        return int(self.cols["serial"].size)
+
+
+class SummaryRows:
+    """The run's rows (ChunkRows in chunk order): len(), the columns of the
+    data frame (NA as NaN) and, for --analysis, the rows as Python lists."""
+
+    def __init__(self, chunks, n_pass):
+        self.chunks, self.n_pass = [c for c in chunks if c is not None], n_pass
+
+    def __len__(self):
+        return sum(len(c) for c in self.chunks)
+
+    def column(self, key, p=None):
+        """A column over all rows as float64 (pass p's for the per-pass ones; NA -> NaN)."""
+        if not self.chunks:
+            return np.zeros(0)
+        if p is None:
+            return np.concatenate([c.cols[key] for c in self.chunks]).astype(np.float64)
+        v = np.concatenate([c.cols[key][p] for c in self.chunks]).astype(np.float64)
+        v[np.concatenate([c.cols["na"][p] for c in self.chunks])] = np.nan
+        return v
+
+    def rows(self):
+        """The rows as [Serial, sequence_ID, sequence_length, (density, start,
+        end, length) per pass], None for NA (--analysis)."""
+        out = []
+        for c in self.chunks:
+            names = c.ids.decode("utf-8", "replace").split("\n")
+            k = c.cols
+            for i in range(len(c)):
+                row = [float(k["serial"][i]), names[i], int(k["length"][i])]
+                for p in range(self.n_pass):
+                    row += [None] * 4 if k["na"][p, i] else [float(k["density"][p, i]), int(k["start"][p, i]),
+                                                            int(k["end"][p, i]), int(k["width"][p, i])]
+                out.append(row)
+        return out
 
 
 def format_row(row, sci_threshold=None):
@@ -115,14 +163,14 @@ def _write_run_log(save_path, t0, input_path, files, patterns, tvr_patterns, rc,
     log.print(f"% of total reads: {pct}%")
     log.print("Summary statistics for the Telomeric reads:")
     log.print("reads length:")
-    log.summary([r[2] for r in rows])
+    log.summary(rows.column("length"))
     log.print("Telomere length:")
-    log.summary([r[6] for r in rows])
+    log.summary(rows.column("width", 0))
     log.print("Telomere length with 1 mismatch allowed:")
-    log.summary([r[10] for r in rows])
+    log.summary(rows.column("width", 1))
     if tvr:
         log.print("Telomere length with 1 mismatch allowed + tvr patterns.:")
-        log.summary([r[14] for r in rows])
+        log.summary(rows.column("width", 2))
     log.print(f"Work ended at: {r_time()}")
     log.close()  # log_close(footer = FALSE)
 
@@ -182,6 +230,18 @@ class _View(dict):
     """One chunk's slice of a grouped result (window-count offsets stay global)."""
 
 
+class _LazyNames(dict):
+    """names[j] of a chunk's rows, decoded from the reader's buffer on first use."""
+
+    def __init__(self, name_of):
+        super().__init__()
+        self._of = name_of
+
+    def __missing__(self, j):
+        v = self[j] = self._of(int(j))
+        return v
+
+
 def _scan_group(nt, chunks, use_filter, write_reads, log, want_windows=False):
     """Scan + call the reads of several chunks in ONE device call (after
     --use_filter, per chunk, when on).  Returns per chunk (rel_serials,
@@ -209,6 +269,8 @@ def _scan_group(nt, chunks, use_filter, write_reads, log, want_windows=False):
         if want_windows:
             v["win_off"], v["n_windows"], v["win_counts"] = res["win_off"][a:b], res["n_windows"][a:b], \
                 res["win_counts"]
+        np_, nl_ = ch.name_pointers()
+        v["name_ptrs"], v["name_lens"] = np_[idx], nl_[idx]
         rel, order, rmax = shard.chunk_relative(v["telomeric"])
         name_of = (lambda c, ix: (lambda j: c.name(int(ix[j]))))(ch, idx)
         seqs = {int(j): ch.seq(int(idx[int(j)])) for j in order} if write_reads else {}
@@ -316,7 +378,7 @@ def run(input_path, save_path, patterns, fmt="fastq", nrec=10000, rc=False, min_
     # every rank at the same group instead of leaving them blocked in the next
     # collective).  Every rank reads the same stream, so the groups' extents
     # (the rounds, the bases cap) agree.
-    tm = {"read_wait": 0.0, "scan": 0.0, "rows_files": 0.0, "collectives": 0.0}
+    tm = {"setup": time.time() - t0, "read_wait": 0.0, "scan": 0.0, "rows_files": 0.0, "collectives": 0.0}
     while True:
         own = []  # (chunk's place in the group, chunk)
         n_grp, ended = 0, False
@@ -356,11 +418,14 @@ def run(input_path, save_path, patterns, fmt="fastq", nrec=10000, rc=False, min_
         try:
             for (pos, _), (rel, order, _, res, name_of, lens, seqs) in zip(own, scanned):
                 if res is None:
-                    local_rows[k + pos] = []  # --use_filter kept no read of this chunk
+                    local_rows[k + pos] = None  # --use_filter kept no read of this chunk
                     continue
                 ser = shard.assign_chunk_serials(rel, starts[pos])
-                names = {int(j): name_of(int(j)) for j in order}
-                local_rows[k + pos] = chunk_rows(res, names, lens, ser, order, nt.n_pass)
+                cols = rows_columns(res, lens, ser, order, nt.n_pass)
+                csv, ids = rows_csv(cols, res["name_ptrs"][order], res["name_lens"][order], nt.n_pass,
+                                    sci_threshold)
+                local_rows[k + pos] = ChunkRows(csv, ids, cols)
+                names = _LazyNames(name_of)
                 for f in pending:  # the previous chunk's files (errors surface here)
                     f.result()
                 pending = []
@@ -410,7 +475,8 @@ def run(input_path, save_path, patterns, fmt="fastq", nrec=10000, rc=False, min_
         if failure is not None:
             raise failure
         raise RuntimeError("NanoTel: another rank failed (see its error)")
-    rows = shard.gather_rows(local_rows)
+    t_end = time.time()
+    rows = SummaryRows(shard.gather_chunks(local_rows) or [], nt.n_pass)
     if stats is not None:
         stats.update(tm)
         stats.update({"host_" + k: v for k, v in nt.host_times().items()} if hasattr(nt, "host_times") else {})
@@ -421,14 +487,18 @@ def run(input_path, save_path, patterns, fmt="fastq", nrec=10000, rc=False, min_
         return None, None
     lengths = np.concatenate(lengths_all) if lengths_all else np.zeros(0, np.uint64)
     barcode = os.path.basename(os.path.normpath(os.path.abspath(input_path)))
-    write_summary_csv(os.path.join(save_path, f"{barcode}_summary.csv"), rows, tvr, sci_threshold)
-    with open(os.path.join(save_path, "reads_ids.txt"), "w") as f:
-        for r in rows:
-            f.write(r[1] + "\n")
+    with open(os.path.join(save_path, f"{barcode}_summary.csv"), "wb") as f:  # write_csv (NanoTel.R:2430-2432)
+        f.write((",".join(columns(tvr)) + "\n").encode())
+        for c in rows.chunks:
+            f.write(c.csv)
+    with open(os.path.join(save_path, "reads_ids.txt"), "wb") as f:  # write_lines (NanoTel.R:2433)
+        for c in rows.chunks:
+            f.write(c.ids)
     if analysis:  # --analysis post-processing (NanoTel.R:2437-2508)
-        write_analysis(save_path, barcode, rows, columns(tvr), format_row, sci_threshold)
+        write_analysis(save_path, barcode, rows.rows(), columns(tvr), format_row, sci_threshold)
     _write_run_log(save_path, t0, input_path, files, patterns, tvr_patterns, rc, subseq_length, min_density,
                    lengths, rows, tvr)
     if stats is not None:
+        stats["final"] = time.time() - t_end
         stats["total"] = time.time() - t0
     return rows, lengths

@@ -50,6 +50,13 @@ class Chunk:
     def seq(self, i):
         return ctypes.string_at(self._sp[i], int(self.lengths[i]))
 
+    def name_pointers(self):
+        """The names' host addresses and lengths (uint64 arrays)."""
+        if not self.n:
+            return np.zeros(0, np.uint64), np.zeros(0, np.uint64)
+        return (np.ctypeslib.as_array((ctypes.c_uint64 * self.n).from_address(self._names_p.value)),
+                self._name_lens)
+
     def pointers(self):
         """The sequences' host addresses (uint64 array, a view of the reader's)."""
         if not self.n:

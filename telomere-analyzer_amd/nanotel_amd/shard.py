@@ -141,6 +141,23 @@ def gather_rows(local_rows, group=None, dst=0):
     return [r for _, rows in sorted(merged.items()) for r in rows]
 
 
+def gather_chunks(local, group=None, dst=0):
+    """Gather {chunk: value} from every rank to dst; returns the values in
+    chunk order on dst (None elsewhere)."""
+    import torch.distributed as dist
+    if not (dist.is_initialized() and dist.get_world_size(group) > 1):
+        return [v for _, v in sorted(local.items())]
+    world = dist.get_world_size(group)
+    out = [None] * world if dist.get_rank(group) == dst else None
+    dist.gather_object(local, out, dst=dst, group=group)
+    if out is None:
+        return None
+    merged = {}
+    for part in out:
+        merged.update(part)
+    return [v for _, v in sorted(merged.items())]
+
+
 def sequential_serials(flags_per_chunk):
     """Reference recurrence run chunk by chunk in one process (the oracle for
     the sharded path): list of per-chunk absolute serial arrays."""

@@ -125,3 +125,54 @@ def test_rows_columns_errors():
         rows_columns(res, np.array([1 << 31, 10], np.uint64), np.zeros(2), np.array([0], np.int64), 2)
     c = rows_columns(res, np.array([10, 10], np.uint64), np.zeros(2), np.zeros(0, np.int64), 2)
     assert c["serial"].size == 0
+
+
+def _python_csv(c, names, n_pass, sci):
+    from nanotel_amd.io import csv_field, format_double, format_int
+    lines = []
+    for i in range(c["serial"].size):
+        f = [format_double(float(c["serial"][i]), sci), csv_field(names[i]), format_int(int(c["length"][i]))]
+        for p in range(n_pass):
+            if c["na"][p, i]:
+                f += ["NA"] * 4
+            else:
+                f += [format_double(float(c["density"][p, i])), format_int(int(c["start"][p, i])),
+                      format_int(int(c["end"][p, i])), format_int(int(c["width"][p, i]))]
+        lines.append(",".join(f) + "\n")
+    return "".join(lines).encode()
+
+
+@pytest.mark.parametrize("sci", [None, 100000.0])
+def test_rows_csv_matches_python_writer(sci):
+    """nt_rows_csv (the C++ summary.csv writer) against the Python rules
+    (io.format_double / csv_field) on edge values: NA passes, -Inf serials,
+    large integral serials, tiny and integral densities, quoted names."""
+    import ctypes
+    from nanotel_amd.api import rows_csv
+    rng = np.random.default_rng(3)
+    n = 400
+    dens = rng.random((n, 3))
+    dens[::7] = np.round(dens[::7], 2)
+    dens[::11] = 1.0
+    dens[::13] = rng.random((len(dens[::13]), 3)) * 1e-5
+    start = rng.integers(1, 50000, (n, 3)).astype(np.int32)
+    start[::5, 1] = -1
+    end = (start + rng.integers(0, 9000, (n, 3))).astype(np.int32)
+    res = {"start": start, "end": end, "density": dens}
+    lens = rng.integers(1, 2_000_000, n).astype(np.uint64)
+    ser = rng.integers(1, 10 ** 7, n).astype(np.float64)
+    ser[::9] = 1_000_000.0
+    ser[::17] = float("-inf")
+    order = rng.permutation(n)[:300].astype(np.int64)
+    c = rows_columns(res, lens, ser, order, 3)
+    names = [f"read_{j}" + (',"x"' if j % 4 == 0 else " runid=7") for j in order]
+    bufs = [ctypes.create_string_buffer(s.encode(), len(s)) for s in names]
+    ptrs = np.array([ctypes.addressof(b) for b in bufs], np.uint64)
+    nls = np.array([len(s) for s in names], np.uint64)
+    csv, ids = rows_csv(c, ptrs, nls, 3, sci)
+    assert csv == _python_csv(c, names, 3, sci)
+    assert ids == "".join(s + "\n" for s in names).encode()
+    for x in (1e-05, 0.0001, 12345.678, 1e16 + 2, 0.5, 2.0 / 3):
+        c1 = {k: v[..., :1].copy() for k, v in c.items()}
+        c1["density"][0, 0] = x
+        assert rows_csv(c1, ptrs[:1], nls[:1], 3, sci)[0] == _python_csv(c1, names[:1], 3, sci), x

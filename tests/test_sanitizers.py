@@ -20,7 +20,7 @@ def test_host_code_under_asan_ubsan(tmp_path):
     assert r.returncode == 0, r.stderr[-4000:]
     work = tmp_path / "work"
     work.mkdir()
-    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1",
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1", NT_READER_SYNC_CLOSE="1",
                UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1")
     r = subprocess.run([str(out / "san_driver"), str(work)], capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-6000:])

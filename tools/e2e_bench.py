@@ -63,6 +63,7 @@ def main():
     ap.add_argument("--plots", action="store_true", help="also time a run with the single-read plots")
     ap.add_argument("--parts", type=int, default=1, help="write the input as a directory of this many files")
     ap.add_argument("--dir", default="/tmp/nt_e2e")
+    ap.add_argument("--profile", default="", help="cProfile the summary-only run into this file (text)")
     a = ap.parse_args()
     os.makedirs(a.dir, exist_ok=True)
     inp = os.path.join(a.dir, "run" if a.parts > 1 else "reads.fastq" + (".gz" if a.gz else ""))
@@ -85,9 +86,21 @@ def main():
         save = os.path.join(a.dir, "out_" + key)
         t = time.perf_counter()
         st = {}
+        prof = None
+        if a.profile and key == "summary_only":
+            import cProfile
+            prof = cProfile.Profile()
+            prof.enable()
         rows, _ = driver.run(inp, save, "TTAGGG", fmt="fastq", nrec=a.nrec, write_reads=write_reads,
                              plot=plot, log=lambda *x: None, stats=st)
         s = time.perf_counter() - t
+        if prof is not None:
+            import io as _io
+            import pstats
+            prof.disable()
+            buf = _io.StringIO()
+            pstats.Stats(prof, stream=buf).sort_stats("cumulative").print_stats(40)
+            open(a.profile, "w").write(buf.getvalue())
         out[key] = {"seconds": round(s, 3), "Gbases_per_s": round(bases / s / 1e9, 3), "rows": len(rows),
                     "phases_s": {k: round(v, 4) for k, v in st.items()}}
     print(json.dumps(out))
