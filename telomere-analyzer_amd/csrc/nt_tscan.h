@@ -24,15 +24,18 @@
 // the hiprtc build), and counts the covered bases of its block into 8 bit
 // planes per pass (acc[b] bit s = bit b of read s's count; counts <= L <= 170).
 //
-// Output, lane = window: the planes are transposed 8x8 within every byte, so
-// that a read's count is one shift-and-mask; the counts are stored as uint16
-// (one coalesced store per read: 64 windows x 2 bytes), the telomeric bits as
-// one ballot per read (count >= thr[L]), the checkpoints every 16 windows
-// from packed row sums.  The read ends are not masked (the T-layout holds A
+// Output, lane = window, per stripe and pass: the telomeric bits (count >=
+// thr[L]) by a bit-sliced compare and a 32 x 32 bit transpose inside each
+// half wave; the counts (uint8: L <= 170) by an 8 x 8 bit transpose within
+// every byte, a 4 x 4 byte transpose inside every quad of lanes and an LDS row
+// per read, stored from LDS as whole 128-byte lines every second stripe
+// (non-temporal); the checkpoints every 16 windows from v_dot4 sums of the
+// same rows.  Bitmask words and checkpoints wait in LDS and go out as runs of
+// a read's row (TsAux).  The read ends are not masked (the T-layout holds A
 // past a read), so the LAST window of every read -- whose width may differ
 // from L, and into which split_telo may have merged a short last block
 // (NanoTel.R:220) -- is recounted exactly by the calling kernel from the
-// per-read planes (call_fix_last, nt_kernels.hip).
+// per-read planes (call_fix_last, nt_call.h).
 #pragma once
 #include "nt_scan.h"
 
