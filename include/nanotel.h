@@ -46,7 +46,7 @@ extern "C" {
 #define NT_E_NEG_WIDTH (-6)   /* IRanges(start, end) with end < start - 1 */
 #define NT_E_HIP (-7)
 #define NT_E_NOMEM (-8)
-#define NT_E_LIMIT (-9)       /* > 64 patterns, TVR > 32 letters, subseq_length > 43690 */
+#define NT_E_LIMIT (-9)       /* > 64 patterns, TVR > 64 letters, subseq_length > 43690 */
 #define NT_E_STATE (-10)      /* nt_compile() not called */
 
 /* summary flags per read */

@@ -59,6 +59,7 @@ struct RtTableEq {
 struct RtCall {
   static constexpr int kNTvr = -1;
   static constexpr bool kMayRaw = true;  // P1 raw views possible (program's raw_p1)
+  static constexpr bool kLong = false;   // TVRs of 33..64 letters (wider neighbourhoods)
   template <class F>
   __device__ __forceinline__ static void for_pat(const NtProgram* prog, F&& f) {
     for (int p = 0; p < prog->n_pat; ++p) f(p, RtTable<0>{&prog->pat[p]});
@@ -76,6 +77,10 @@ struct RtCall {
     for (int t = 0; t < prog->n_tvr; ++t) f(t, RtTableEq<0>{&prog->tvr[t]});
   }
 };
+// The same for programs with a TVR of more than 32 letters (host dispatch).
+struct RtCallLong : RtCall {
+  static constexpr bool kLong = true;
+};
 
 // Compile-time lists (hiprtc): CtList<CtPat<m, tt...>...> of the scan truth
 // tables and of the code-equality ones, for the patterns and the TVRs.
@@ -85,6 +90,7 @@ struct CtCall {
   // raw_p1 (single fixed pattern) known: without it the raw-view marks and
   // their registers are compiled out
   static constexpr bool kMayRaw = kRaw;
+  static constexpr bool kLong = CtMaxM<Tvrs>::value > 32;
   template <class F>
   __device__ __forceinline__ static void for_pat(const NtProgram* prog, F&& f) {
     CtVisit<Pats>::run(prog->pat, f);
@@ -105,29 +111,33 @@ struct CtCall {
 
 // Hits of descriptor d at the 32 starts of each hit word h in [0, NH), from
 // the plane words Lw/Hw and validity Vw of positions [32h, 32h + 63] (words h,
-// h + 1): x0 exact, x1 <= 1 mismatch (invalid positions are mismatches).
-// Letter tests are made on the unshifted words and shifted by j.
-template <int NH, class D>
+// h + 1; with kX = 1, TVRs of 33..64 letters, [32h, 32h + 95]: words h .. h + 2):
+// x0 exact, x1 <= 1 mismatch (invalid positions are mismatches).  Letter tests
+// are made on the unshifted words and shifted by j.
+template <int NH, int kX, class D>
 __device__ __forceinline__ void words_hits(const D& d, const uint32_t* Lw, const uint32_t* Hw,
                                            const uint32_t* Vw, uint32_t* x0, uint32_t* x1) {
   constexpr int kM = D::kM;
   if constexpr (kM > 0) {
+    static_assert(kM <= 32 * (kX + 1), "pattern longer than the neighbourhood's plane words");
 #pragma unroll
     for (int h = 0; h < NH; ++h) {
       uint32_t q[kM];
 #pragma unroll
       for (int j = 0; j < kM; ++j) {
-        const uint32_t e0 = d.E(j, Lw[h], Hw[h]) & Vw[h], e1 = d.E(j, Lw[h + 1], Hw[h + 1]) & Vw[h + 1];
-        q[j] = funnel(e1, e0, (uint32_t)j);
+        const int w = h + (j >> 5);
+        const uint32_t e0 = d.E(j, Lw[w], Hw[w]) & Vw[w], e1 = d.E(j, Lw[w + 1], Hw[w + 1]) & Vw[w + 1];
+        q[j] = funnel(e1, e0, (uint32_t)(j & 31));
       }
       combine<kM, false>(q, x0[h], x1[h]);
       if (kM <= 1) x1[h] &= Vw[h];
     }
   } else {
     const int m = d.m();
+    const int m0 = m < 32 ? m : 32;
 #pragma unroll
     for (int h = 0; h < NH; ++h) x0[h] = x1[h] = 0xFFFFFFFFu;
-    for (int j = 0; j < m; ++j) {
+    for (int j = 0; j < m0; ++j) {
 #pragma unroll
       for (int h = 0; h < NH; ++h) {
         const uint32_t Ls = funnel(Lw[h + 1], Lw[h], (uint32_t)j);
@@ -135,6 +145,18 @@ __device__ __forceinline__ void words_hits(const D& d, const uint32_t* Lw, const
         const uint32_t q = d.E(j, Ls, Hs) & funnel(Vw[h + 1], Vw[h], (uint32_t)j);
         x1[h] = (x1[h] & q) | x0[h];
         x0[h] &= q;
+      }
+    }
+    if constexpr (kX > 0) {
+      for (int j = 32; j < m; ++j) {
+#pragma unroll
+        for (int h = 0; h < NH; ++h) {
+          const uint32_t Ls = funnel(Lw[h + 2], Lw[h + 1], (uint32_t)(j - 32));
+          const uint32_t Hs = funnel(Hw[h + 2], Hw[h + 1], (uint32_t)(j - 32));
+          const uint32_t q = d.E(j, Ls, Hs) & funnel(Vw[h + 2], Vw[h + 1], (uint32_t)(j - 32));
+          x1[h] = (x1[h] & q) | x0[h];
+          x0[h] &= q;
+        }
       }
     }
     if (m <= 1) {
@@ -286,16 +308,17 @@ struct Nb {
   uint32_t re[kMarks ? K + 2 : 1];
 };
 
-template <int K, bool kMarks = true>
+// kX = 1 (TVRs of 33..64 letters): one more plane word each side.
+template <int K, bool kMarks = true, int kX = 0>
 struct NbBlocks {
-  uint2 b[K + (kMarks ? 2 : 0) + 3];
+  uint2 b[K + (kMarks ? 2 : 0) + 3 + 2 * kX];
 };
 
-template <int K, bool kMarks>
-__device__ __forceinline__ void nb_fetch(const Lane& c, int q0, NbBlocks<K, kMarks>& f) {
+template <int K, bool kMarks, int kX>
+__device__ __forceinline__ void nb_fetch(const Lane& c, int q0, NbBlocks<K, kMarks, kX>& f) {
   constexpr int E = kMarks ? 1 : 0;
-  constexpr int NP = K + 2 * E + 2;
-  const int bb = (q0 >> 5) - E - 1;  // arithmetic shift: floor for q0 < 0
+  constexpr int NP = K + 2 * E + 2 + 2 * kX;
+  const int bb = (q0 >> 5) - E - 1 - kX;  // arithmetic shift: floor for q0 < 0
 #pragma unroll
   for (int t = 0; t <= NP; ++t) {
     const int b = bb + t;
@@ -305,15 +328,18 @@ __device__ __forceinline__ void nb_fetch(const Lane& c, int q0, NbBlocks<K, kMar
 
 template <class CS>
 struct Call {
+static constexpr int kX = CS::kLong ? 1 : 0;  // extra plane / hit word for TVRs of 33..64 letters
+using NbB4 = NbBlocks<4, false, kX>;
+using NbB5 = NbBlocks<5, true, kX>;
 
 template <int K, bool kMarks>
-static __device__ __forceinline__ void nb_compute(const Lane& c, int q0, const NbBlocks<K, kMarks>& f,
+static __device__ __forceinline__ void nb_compute(const Lane& c, int q0, const NbBlocks<K, kMarks, kX>& f,
                                            Nb<K, kMarks>& nb) {
   constexpr int E = kMarks ? 1 : 0;  // extra word each side
   constexpr int NC = K + 2 * E;      // coverage words computed, i = -E..K-1+E
-  constexpr int NP = NC + 2;         // plane words, positions [q0 + 32i, +31], i = -E-1..K+E
-  constexpr int NH = NC + 1;         // hit words, starts [q0 + 32i, +31], i = -E-1..K-1+E
-  constexpr int T0 = -E - 1;         // index of plane / hit word 0
+  constexpr int NP = NC + 2 + 2 * kX;  // plane words, positions [q0 + 32i, +31], i = -E-1-kX..K+E+kX
+  constexpr int NH = NC + 1 + kX;    // hit words, starts [q0 + 32i, +31], i = -E-1-kX..K-1+E
+  constexpr int T0 = -E - 1 - kX;    // index of plane / hit word 0
   nb.q0 = q0;
   uint32_t Lw[NP], Hw[NP], Vw[NP];
   const uint32_t sh = (uint32_t)(q0 & 31);
@@ -337,22 +363,22 @@ static __device__ __forceinline__ void nb_compute(const Lane& c, int q0, const N
     launder_words<NP>(Lw, Lp);
     launder_words<NP>(Hw, Hp);
     launder_words<NP>(Vw, Vp);
-    words_hits<NH>(d, Lp, Hp, Vp, x0, x1);
+    words_hits<NH, kX>(d, Lp, Hp, Vp, x0, x1);
     if (c.rc.n_exc) {
 #pragma unroll
       for (int h = 0; h < NH; ++h)
         patch_exceptions(c.rc, (int64_t)q0 + 32 * (h + T0), 0, c.n - 1, *d.P, false, x0[h], x1[h]);
     }
-    // coverage word ci (i = ci - E) from hit words i and i - 1
+    // coverage word ci (i = ci - E) from hit words i and i - 1 (patterns <= 18 letters)
 #pragma unroll
     for (int ci = 0; ci < NC; ++ci)
-      nb.cov[ci + 1 - E] |= spread<kM>(c.k ? x1[ci + 1] : x0[ci + 1], c.k ? x1[ci] : x0[ci], m);
+      nb.cov[ci + 1 - E] |= spread<kM>(c.k ? x1[ci + 1 + kX] : x0[ci + 1 + kX], c.k ? x1[ci + kX] : x0[ci + kX], m);
     if constexpr (kMarks) {
       if (CS::kMayRaw && c.raw && pi == 0) {
 #pragma unroll
         for (int ci = 0; ci < NC; ++ci) {
-          nb.rs[ci] = x0[ci + 1];
-          nb.re[ci] = m > 1 ? funnel(x0[ci + 1], x0[ci], (uint32_t)(32 - (m - 1))) : x0[ci + 1];
+          nb.rs[ci] = x0[ci + 1 + kX];
+          nb.re[ci] = m > 1 ? funnel(x0[ci + 1 + kX], x0[ci + kX], (uint32_t)(32 - (m - 1))) : x0[ci + 1 + kX];
         }
       }
     }
@@ -365,7 +391,7 @@ static __device__ __forceinline__ void nb_compute(const Lane& c, int q0, const N
       launder_words<NP>(Lw, Lp);
       launder_words<NP>(Hw, Hp);
       launder_words<NP>(Vw, Vp);
-      words_hits<NH>(d, Lp, Hp, Vp, x0, x1);
+      words_hits<NH, kX>(d, Lp, Hp, Vp, x0, x1);
       if (c.rc.n_exc) {
 #pragma unroll
         for (int h = 0; h < NH; ++h)
@@ -373,12 +399,17 @@ static __device__ __forceinline__ void nb_compute(const Lane& c, int q0, const N
       }
       if (c.use_tvr) {
 #pragma unroll
-        for (int ci = 0; ci < NC; ++ci) nb.cov[ci + 1 - E] |= spread<kM>(x0[ci + 1], x0[ci], d.m());
+        for (int ci = 0; ci < NC; ++ci) {
+          if constexpr (kX > 0)
+            nb.cov[ci + 1 - E] |= spread_long<kM>(x0[ci + 2], x0[ci + 1], x0[ci], d.m());
+          else
+            nb.cov[ci + 1 - E] |= spread<kM>(x0[ci + 1], x0[ci], d.m());
+        }
       }
     });
   }
 #pragma unroll
-  for (int ci = 0; ci < NC; ++ci) nb.cov[ci + 1 - E] &= Vw[ci + 1];
+  for (int ci = 0; ci < NC; ++ci) nb.cov[ci + 1 - E] &= Vw[ci + 1 + kX];
 }
 
 // |coverage ∩ [a, b]|, [a, b] within [q0, q0 + 32K)
@@ -437,7 +468,7 @@ static __device__ __forceinline__ int nb_max_end(const Lane& c, const Nb<K>& nb,
 static __device__ __forceinline__ int cov_count2(const Lane& c, int x1, int y1, int x2, int y2) {
   int t = 0;
   while (x1 <= y1 || x2 <= y2) {
-    NbBlocks<4, false> f1, f2;
+    NbB4 f1, f2;
     nb_fetch(c, x1, f1);
     nb_fetch(c, x2, f2);
 NT_CALL_SITE_LOOP
@@ -618,17 +649,17 @@ static __device__ __forceinline__ Pos find_right_telo(const Lane& c, bool& err) 
 // and get_accurate_end (NanoTel.R:1692-1721) only ranges in [e-100, e+49]
 // (0-based; the offsets are hard-coded in the reference), so each is one
 // neighbourhood, [s-42, s+118) and [e-102, e+58); both fetched in one batch.
-static __device__ __forceinline__ void accurate_fetch(const Lane& c, int s, int e, NbBlocks<5>& fs, NbBlocks<5>& fe) {
+static __device__ __forceinline__ void accurate_fetch(const Lane& c, int s, int e, NbB5& fs, NbB5& fe) {
   nb_fetch(c, s - 42, fs);
   nb_fetch(c, e - 102, fe);
 }
 
-static __device__ __forceinline__ void accurate_both(const Lane& c, int s, int e, const NbBlocks<5>& fs,
-                                                     const NbBlocks<5>& fe, int& s_acc, int& e_acc) {
+static __device__ __forceinline__ void accurate_both(const Lane& c, int s, int e, const NbB5& fs,
+                                                     const NbB5& fe, int& s_acc, int& e_acc) {
   s_acc = -1;
   e_acc = -1;
   // one neighbourhood computation site, start side then end side
-  NbBlocks<5> f = fs;
+  NbB5 f = fs;
 NT_CALL_SITE_LOOP
   for (int i = 0; i < 2; ++i, f = fe) {
     if ((i ? e : s) == -1) continue;
@@ -735,13 +766,23 @@ static __device__ __forceinline__ void pw_at(const Lane& c, const Pw<K>& w, int 
 template <int K, class D>
 static __device__ __forceinline__ void hits_at_w(const Lane& c, const Pw<K>& w, const D& d, int base, int vlo,
                                                  int vhi, uint32_t& a0, uint32_t& a1) {
-  uint32_t Lw[2], Hw[2], Vw[2];
-  pw_at(c, w, base, Lw[0], Hw[0]);
-  pw_at(c, w, base + 32, Lw[1], Hw[1]);
-  Vw[0] = range_mask(base, vlo, vhi);
-  Vw[1] = range_mask((int64_t)base + 32, vlo, vhi);
-  words_hits<1>(d, Lw, Hw, Vw, &a0, &a1);
-  if (c.rc.n_exc) patch_exceptions(c.rc, base, vlo, vhi, *d.P, true, a0, a1);
+  // A TVR of more than 32 letters (exact only) never matches inside the
+  // <= 18-base sub-sequence of a step: no hits.
+  if constexpr (D::kM > 32) {
+    a0 = a1 = 0u;
+  } else {
+    if (d.m() > 32) {
+      a0 = a1 = 0u;
+      return;
+    }
+    uint32_t Lw[2], Hw[2], Vw[2];
+    pw_at(c, w, base, Lw[0], Hw[0]);
+    pw_at(c, w, base + 32, Lw[1], Hw[1]);
+    Vw[0] = range_mask(base, vlo, vhi);
+    Vw[1] = range_mask((int64_t)base + 32, vlo, vhi);
+    words_hits<1, 0>(d, Lw, Hw, Vw, &a0, &a1);
+    if (c.rc.n_exc) patch_exceptions(c.rc, base, vlo, vhi, *d.P, true, a0, a1);
+  }
 }
 
 // max end (right) / min start (left) of the fixed=TRUE matches of the pass's
@@ -840,7 +881,7 @@ static __device__ __forceinline__ void call_pass(Lane& c, int& out_s, int& out_e
 #ifndef NT_DBG_NO_ACC
   // get_accurate_* neighbourhoods fetched with the wrapper's density loads
   // (one memory round trip less); refetched if the wrapper re-runs the call
-  NbBlocks<5> fs, fe;
+  NbB5 fs, fe;
   if (NT_CALL_ACC_EARLY) accurate_fetch(c, tp.s, tp.e, fs, fe);
 #endif
 #ifdef NT_DBG_NO_WRAP

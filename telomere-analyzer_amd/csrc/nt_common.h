@@ -26,7 +26,7 @@
 
 #define NT_MAX_PAT 64     // unique patterns per list (--patterns / --tvr_patterns)
 #define NT_MAX_M 18       // testit::assert(str_length(pattern) <= 18), NanoTel.R:589,647
-#define NT_MAX_TVR_M 32   // TVRs are only length-limited by the 32-bit start words
+#define NT_MAX_TVR_M 64   // TVRs: two overflow words per segment / neighbourhood word (nt_scan.h, nt_call.h)
 #define NT_MAX_PASS 3
 #define NT_WIN_ROWS(nw) (((nw) + 63) & ~63ull)  // windows of a padded count row
 

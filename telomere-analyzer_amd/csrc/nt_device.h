@@ -116,6 +116,23 @@ __device__ __forceinline__ uint32_t spread(uint32_t h, uint32_t hprev, int m) {
   return c;
 }
 
+// The same for m up to 64 (TVRs): hit words of this and the two previous 32
+// starts.
+template <int kM = 0>
+__device__ __forceinline__ uint32_t spread_long(uint32_t h, uint32_t hp, uint32_t hpp, int m) {
+  uint32_t c = h;
+  if constexpr (kM > 0) {
+#pragma unroll
+    for (int j = 1; j < kM && j <= 32; ++j) c |= funnel(h, hp, (uint32_t)(32 - j));
+#pragma unroll
+    for (int j = 33; j < kM; ++j) c |= funnel(hp, hpp, (uint32_t)(64 - j));
+  } else {
+    for (int j = 1; j < m && j <= 32; ++j) c |= funnel(h, hp, (uint32_t)(32 - j));
+    for (int j = 33; j < m; ++j) c |= funnel(hp, hpp, (uint32_t)(64 - j));
+  }
+  return c;
+}
+
 // ---------------------------------------------------------------- exceptions
 
 __device__ __forceinline__ int32_t exc_lower_bound(const ReadCtx& rc, int64_t x) {

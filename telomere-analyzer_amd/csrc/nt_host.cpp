@@ -30,12 +30,12 @@ hipError_t nt_dev_launch(const NtProgram* prog, const uint32_t* thr, const NtBat
                          const NtOut* O, uint64_t* tmask, unsigned long long* queue,
                          uint32_t len_lo, uint32_t len_hi, uint32_t claim, uint32_t nstatic,
                          int single, int one, int m6, int lds, uint32_t wave_words, uint32_t* gscr,
-                         int grid, int call_grid, hipStream_t stream);
+                         int grid, hipStream_t stream);
 hipError_t nt_dev_set_lds_limit(uint32_t bytes);
 int nt_dev_scan_blocks_per_cu(int single, int one, int m6, int lds, size_t lds_bytes);
 hipError_t nt_dev_launch_call(const NtProgram* prog, const NtBatch* B, const NtOut* O,
                               const uint64_t* tmask, const uint32_t* thr, uint32_t thr_size, int fix_last,
-                              int call_grid, hipStream_t stream);
+                              int long_tvr, int call_grid, hipStream_t stream);
 hipError_t nt_dev_launch_bundle(const NtBatch* B, uint64_t n_stripes, uint32_t* tp, int L, uint32_t div_m,
                                 uint32_t div_s, hipStream_t stream, int cu_count);
 hipError_t nt_dev_launch_synth(const NtSynth* S, uint32_t* planes, uint64_t n_reads,
@@ -247,12 +247,19 @@ static void* call_jit_fn(nt_ctx* ctx, uint64_t n_reads) {
   return ctx->cjit_fn;
 }
 
+// a TVR of more than 32 letters: the calling kernel with wider neighbourhoods
+static int long_tvr(const NtProgram& P) {
+  for (int i = 0; i < P.n_tvr; ++i)
+    if (P.tvr[i].m > 32) return 1;
+  return 0;
+}
+
 static hipError_t launch_call(nt_ctx* ctx, void* cfn, const NtBatch* B, const NtOut* O, const uint64_t* tm,
                               int fix_last, int grid, hipStream_t s) {
   const uint32_t* thr = (const uint32_t*)ctx->thr.p;
   const uint32_t ts = (uint32_t)ctx->thr_h.size();
   return cfn ? nt_cjit_launch(cfn, grid, s, ctx->prog_dev, B, O, tm, thr, ts, fix_last)
-             : nt_dev_launch_call(ctx->prog_dev, B, O, tm, thr, ts, fix_last, grid, s);
+             : nt_dev_launch_call(ctx->prog_dev, B, O, tm, thr, ts, fix_last, long_tvr(ctx->prog), grid, s);
 }
 
 static int hip_fail(nt_ctx* ctx, hipError_t e, const char* what) {
@@ -619,7 +626,7 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
                         (uint32_t*)dbg);
     else
       e = nt_dev_launch(ctx->prog_dev, (const uint32_t*)ctx->thr.p, &Bk, &Ok, tmk, q, 0u, (uint32_t)len_cap, claim, nstatic,
-                        single, one, m6, 1, ww_lds, nullptr, (int)grid, 0, ctx->stream);
+                        single, one, m6, 1, ww_lds, nullptr, (int)grid, ctx->stream);
     if (dbg && e == hipSuccess) {
       uint64_t h[9];
       (void)hipStreamSynchronize(ctx->stream);
@@ -636,7 +643,7 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
                           &Bk, &Ok, tmk, q + NT_QUEUE_WORDS, (uint32_t)len_cap, 0xFFFFFFFFu, 1u, 0u, ww_g, (uint32_t*)ctx->scratch.p);
       else
         e = nt_dev_launch(ctx->prog_dev, (const uint32_t*)ctx->thr.p, &Bk, &Ok, tmk, q + NT_QUEUE_WORDS, (uint32_t)len_cap,
-                          0xFFFFFFFFu, 1u, 0u, single, 0, 0, 0, ww_g, (uint32_t*)ctx->scratch.p, (int)grid_g, 0,
+                          0xFFFFFFFFu, 1u, 0u, single, 0, 0, 0, ww_g, (uint32_t*)ctx->scratch.p, (int)grid_g,
                           ctx->stream);
       if (e != hipSuccess) return hip_fail(ctx, e, "launch nt_scan_kernel<global>");
     }

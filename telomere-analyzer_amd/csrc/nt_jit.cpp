@@ -71,7 +71,9 @@ const char* const kTypedefs =
 // m >= 2 and whose TVRs share one length, with subseq_length L <= 170 (8-bit
 // window counts of the transposed output) and 2 (max m - 1) < L (the read's
 // last window, recounted by the calling kernel, holds every position whose
-// letters reach past the read end).  Others take the per-read scan only.
+// letters reach past the read end), and patterns / TVRs of at most 32 letters
+// (the walk's history registers grow with the longest).  Others take the
+// per-read scan only.
 bool nt_tscan_eligible(const NtProgram& P) {
   if (P.n_pat < 1 || P.L > 170) return false;
   int mp = P.pat[0].m, mt = P.n_tvr ? P.tvr[0].m : 0;
@@ -80,7 +82,7 @@ bool nt_tscan_eligible(const NtProgram& P) {
   for (int i = 1; i < P.n_tvr; ++i)
     if (P.tvr[i].m != mt) return false;
   const int M = mp > mt ? mp : mt;
-  return mp >= 2 && 2 * (M - 1) < P.L;
+  return mp >= 2 && M <= 32 && 2 * (M - 1) < P.L;
 }
 
 namespace {

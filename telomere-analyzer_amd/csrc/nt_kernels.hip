@@ -51,6 +51,8 @@ nt_scan_kernel(const NtProgram* __restrict__ prog, const uint32_t* __restrict__ 
 // The calling kernel (nt_call.h) with run-time pattern lists; the
 // hiprtc-specialised twin (compile-time patterns) is built by nt_jit.cpp.
 NT_CALL_KERNEL(nt_call_kernel, RtCall)
+// programs with a TVR of more than 32 letters (wider neighbourhoods)
+NT_CALL_KERNEL(nt_call_kernel_long, RtCallLong)
 
 
 // ============================================================ synthetic reads
@@ -283,10 +285,6 @@ nt_filter_kernel(const NtProgram* __restrict__ prog, NtBatch B, uint8_t* __restr
 
 extern "C" {
 
-hipError_t nt_dev_launch_call(const NtProgram* prog, const NtBatch* B, const NtOut* O,
-                              const uint64_t* tmask, const uint32_t* thr, uint32_t thr_size, int fix_last,
-                              int call_grid, hipStream_t stream);
-
 // per-wave scan scratch words for reads with at most nw_cap windows
 uint32_t nt_dev_wave_words(int single, int n_hits, int np, uint32_t nw_cap) {
   const uint32_t w = (single ? 0u : (uint32_t)n_hits * 64u) + (uint32_t)(np < 2 ? 2 : np) * (nw_cap + 1u);
@@ -329,7 +327,7 @@ hipError_t nt_dev_launch(const NtProgram* prog, const uint32_t* thr, const NtBat
                          const NtOut* O, uint64_t* tmask, unsigned long long* queue,
                          uint32_t len_lo, uint32_t len_hi, uint32_t claim, uint32_t nstatic,
                          int single, int one, int m6, int lds, uint32_t wave_words, uint32_t* gscr,
-                         int grid, int call_grid, hipStream_t stream) {
+                         int grid, hipStream_t stream) {
   const size_t lds_bytes = lds ? (size_t)wave_words * 4u * nt::kNWaves : 0;
   bool done = false;
 #define NT_LAUNCH(S, G, SI, O_, M)                                                             \
@@ -342,9 +340,7 @@ hipError_t nt_dev_launch(const NtProgram* prog, const uint32_t* thr, const NtBat
   NT_SCAN_VARIANTS(NT_LAUNCH)
 #undef NT_LAUNCH
   if (!done) return hipErrorInvalidValue;
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess || call_grid <= 0) return e;
-  return nt_dev_launch_call(prog, B, O, tmask, thr, 0, 0, call_grid, stream);
+  return hipGetLastError();
 }
 
 // resident 256-thread blocks per CU of the scan variant (grid sizing)
@@ -365,9 +361,13 @@ int nt_dev_scan_blocks_per_cu(int single, int one, int m6, int lds, size_t lds_b
 
 hipError_t nt_dev_launch_call(const NtProgram* prog, const NtBatch* B, const NtOut* O,
                               const uint64_t* tmask, const uint32_t* thr, uint32_t thr_size, int fix_last,
-                              int call_grid, hipStream_t stream) {
-  hipLaunchKernelGGL(nt::nt_call_kernel, dim3(call_grid), dim3(256), 0, stream, prog, *B, *O, tmask, thr,
-                     thr_size, fix_last);
+                              int long_tvr, int call_grid, hipStream_t stream) {
+  if (long_tvr)
+    hipLaunchKernelGGL(nt::nt_call_kernel_long, dim3(call_grid), dim3(256), 0, stream, prog, *B, *O, tmask, thr,
+                       thr_size, fix_last);
+  else
+    hipLaunchKernelGGL(nt::nt_call_kernel, dim3(call_grid), dim3(256), 0, stream, prog, *B, *O, tmask, thr,
+                       thr_size, fix_last);
   return hipGetLastError();
 }
 

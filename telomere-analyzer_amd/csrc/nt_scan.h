@@ -263,7 +263,8 @@ struct Seg {
 // Hits of pattern d at the 64 starts of the segment: a0 exact, a1 <= 1
 // mismatch (matchPattern max.mismatch 0 / 1; letters outside the read are
 // mismatches).  Letter tests are made on the unshifted words and shifted by
-// j (v_alignbit); the next segment's word-A tests come from lane+1 by DPP.
+// j (v_alignbit); the next segment's word-A tests come from lane+1 by DPP,
+// and for letters j >= 32 (TVRs of 33..64 letters) its word-B tests too.
 template <bool kValid, bool kExact, class D>
 __device__ __forceinline__ void seg_hits(const D& d, const Seg& s, uint32_t& a0A, uint32_t& a1A,
                                          uint32_t& a0B, uint32_t& a1B) {
@@ -275,8 +276,14 @@ __device__ __forceinline__ void seg_hits(const D& d, const Seg& s, uint32_t& a0A
       eB &= s.VB;
     }
     const uint32_t eN = from_next_lane(eA);
-    qA = funnel(eB, eA, (uint32_t)j);
-    qB = funnel(eN, eB, (uint32_t)j);
+    if (j < 32) {
+      qA = funnel(eB, eA, (uint32_t)j);
+      qB = funnel(eN, eB, (uint32_t)j);
+    } else {
+      const uint32_t eNB = from_next_lane(eB);
+      qA = funnel(eN, eB, (uint32_t)(j - 32));
+      qB = funnel(eNB, eN, (uint32_t)(j - 32));
+    }
   };
   if constexpr (kM > 0) {
     uint32_t qa[kM], qb[kM];
@@ -308,12 +315,28 @@ __device__ __forceinline__ void seg_hits(const D& d, const Seg& s, uint32_t& a0A
 
 // OR into (cA, cB, ov) the coverage of hit starts hA (word A) and hB (word
 // B): bit i covered iff a start in [i-m+1, i] (trim + IRanges::reduce).
-// ov = coverage spilling into the next segment's word A.  kM > 0: span
-// doubling on the 96-bit value (ov:B:A).
+// ov = coverage spilling into the next segment's word A, ovB (m > 32 only:
+// TVRs) into its word B.  kM > 0: span doubling on the 96-bit value (ov:B:A),
+// 128-bit (ovB:ov:B:A) for kM > 32.
 template <int kM>
 __device__ __forceinline__ void seg_spread(uint32_t hA, uint32_t hB, int m, uint32_t& cA,
-                                           uint32_t& cB, uint32_t& ov) {
-  if constexpr (kM > 0) {
+                                           uint32_t& cB, uint32_t& ov, uint32_t& ovB) {
+  if constexpr (kM > 32) {
+    uint32_t w0 = hA, w1 = hB, w2 = 0u, w3 = 0u;
+#pragma unroll
+    for (int s = 1; s < kM;) {
+      const int t = 2 * s <= kM ? s : kM - s;  // <= 32
+      w3 |= funnel(w3, w2, (uint32_t)(32 - t));
+      w2 |= funnel(w2, w1, (uint32_t)(32 - t));
+      w1 |= funnel(w1, w0, (uint32_t)(32 - t));
+      if (t < 32) w0 |= w0 << t;
+      s += t;
+    }
+    cA |= w0;
+    cB |= w1;
+    ov |= w2;
+    ovB |= w3;
+  } else if constexpr (kM > 0) {
     uint32_t w0 = hA, w1 = hB, w2 = 0u;
 #pragma unroll
     for (int s = 1; s < kM;) {
@@ -326,6 +349,17 @@ __device__ __forceinline__ void seg_spread(uint32_t hA, uint32_t hB, int m, uint
     cA |= w0;
     cB |= w1;
     ov |= w2;
+  } else if (m > 32) {
+    const uint64_t v = (uint64_t)hA | ((uint64_t)hB << 32);
+    uint64_t lo = v, hi = 0ull;
+    for (int j = 1; j < m; ++j) {
+      lo |= v << j;
+      hi |= v >> (64 - j);
+    }
+    cA |= (uint32_t)lo;
+    cB |= (uint32_t)(lo >> 32);
+    ov |= (uint32_t)hi;
+    ovB |= (uint32_t)(hi >> 32);
   } else {
     cA |= hA;
     cB |= hB;
@@ -350,6 +384,7 @@ struct SingleSet {  // --patterns with one unique pattern, no TVRs
   static constexpr int kNPat = 1;
   static constexpr int kNHits = 2;
   static constexpr int kNPass = 2;  // 0 = read from the program
+  static constexpr bool kLongTvr = false;  // TVRs of > 32 letters possible (a second carry word)
   template <class F>
   __device__ __forceinline__ static void for_pat(const NtProgram* prog, F&& f) {
     f(0, D{&prog->pat[0]});
@@ -363,6 +398,7 @@ struct GenericSet {  // any program: run-time lists
   static constexpr int kNPat = 0;
   static constexpr int kNHits = 1;
   static constexpr int kNPass = 0;
+  static constexpr bool kLongTvr = true;
   template <class F>
   __device__ __forceinline__ static void for_pat(const NtProgram* prog, F&& f) {
     for (int p = 0; p < prog->n_pat; ++p) f(p, RtTable<0>{&prog->pat[p]});
@@ -388,6 +424,16 @@ struct CtPat {
 template <class... P>
 struct CtList {
   static constexpr int kN = sizeof...(P);
+};
+// Longest pattern of a compile-time list (0 for an empty one).
+template <class List>
+struct CtMaxM {
+  static constexpr int value = 0;
+};
+template <class H, class... T>
+struct CtMaxM<CtList<H, T...>> {
+  static constexpr int kRest = CtMaxM<CtList<T...>>::value;
+  static constexpr int value = H::kM > kRest ? H::kM : kRest;
 };
 template <int I, class Head, class... Tail>
 struct CtAt {
@@ -422,6 +468,7 @@ struct CtSet {
   static constexpr bool kRegHits = true;
   static constexpr int kNHits = 2 * kNPat + kNTvr;
   static constexpr int kNPass = kNTvr > 0 ? 3 : 2;
+  static constexpr bool kLongTvr = CtMaxM<Tvrs>::value > 32;
   template <class F>
   __device__ __forceinline__ static void for_pat(const NtProgram* prog, F&& f) {
     CtVisit<Pats>::run(prog->pat, f);
@@ -496,6 +543,7 @@ __device__ __forceinline__ bool dbg_ok(DbgRec* d, int kind, uint64_t idx, uint64
 template <int kNHits>
 struct ScanState {
   uint32_t ov0, ov1, ov2;  // overflow carried into the next chunk's lane 0
+  uint32_t ov2b;           // pass 2 overflow into lane 0's word B (TVRs > 32 letters)
   uint32_t T0, T1, T2;     // covered bases before this chunk, per pass
   uint32_t acc[kNHits];    // register hit counters (per lane)
 };
@@ -541,11 +589,12 @@ __device__ __forceinline__ void scan_chunk(const NtProgram* __restrict__ prog, c
         hitacc[(n_pat + p) * kWave + lane] += h1;
       }
     }
-    seg_spread<decltype(d)::kM>(a0A, a0B, d.m(), cA0, cB0, ov0);
-    seg_spread<decltype(d)::kM>(a1A, a1B, d.m(), cA1, cB1, ov1);
+    uint32_t ovx = 0u;  // (patterns are <= 18 letters)
+    seg_spread<decltype(d)::kM>(a0A, a0B, d.m(), cA0, cB0, ov0, ovx);
+    seg_spread<decltype(d)::kM>(a1A, a1B, d.m(), cA1, cB1, ov1, ovx);
   });
   const bool three = S::kNPass == 3 || (S::kNPass == 0 && np == 3);
-  uint32_t cA2 = 0u, cB2 = 0u, ov2 = 0u;
+  uint32_t cA2 = 0u, cB2 = 0u, ov2 = 0u, ov2b = 0u;
   if (three) {  // P3 = P2 U exact TVR matches
     cA2 = cA1;
     cB2 = cB1;
@@ -562,7 +611,7 @@ __device__ __forceinline__ void scan_chunk(const NtProgram* __restrict__ prog, c
         if constexpr (S::kRegHits) st.acc[2 * S::kNPat + t] += h0;
         else hitacc[(2 * n_pat + t) * kWave + lane] += h0;
       }
-      seg_spread<decltype(d)::kM>(a0A, a0B, d.m(), cA2, cB2, ov2);
+      seg_spread<decltype(d)::kM>(a0A, a0B, d.m(), cA2, cB2, ov2, ov2b);
     });
   }
   // coverage spilled from the previous segment (lane 0: previous chunk's lane 62)
@@ -573,6 +622,10 @@ __device__ __forceinline__ void scan_chunk(const NtProgram* __restrict__ prog, c
   if (three) {
     cA2 |= from_prev_lane(ov2, st.ov2);
     st.ov2 = __builtin_amdgcn_readlane(ov2, kWave - 2);
+    if constexpr (S::kLongTvr) {
+      cB2 |= from_prev_lane(ov2b, st.ov2b);
+      st.ov2b = __builtin_amdgcn_readlane(ov2b, kWave - 2);
+    }
   }
   if (kValid) {  // trim to [1, n]
     cA0 &= s.VA;
@@ -765,7 +818,7 @@ __device__ __forceinline__ void scan_reads(const NtProgram* __restrict__ prog,
 
     // ------------------------------------------------------------ scan
     ScanState<S::kNHits> st;
-    st.ov0 = st.ov1 = st.ov2 = 0u;
+    st.ov0 = st.ov1 = st.ov2 = st.ov2b = 0u;
     st.T0 = st.T1 = st.T2 = 0u;
 #pragma unroll
     for (int c = 0; c < S::kNHits; ++c) st.acc[c] = 0u;

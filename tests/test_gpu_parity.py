@@ -205,6 +205,76 @@ def test_many_patterns_specialised_call(monkeypatch):
     assert nt.call_jit(), "the specialised calling kernel did not run"
 
 
+# TVRs of 33..64 letters (the reference takes TVRs of any length: NanoTel.R:
+# 360-393; the scan carries a second overflow word, the calling kernel wider
+# neighbourhoods).  The TVR motif ACCCTG is >= 2 letters from every pattern, so
+# P3 differs from P2 exactly where the long TVR matches.
+LONG_TVR = [
+    dict(patterns="TTAGGG TCAGGG CTAGGG TTAGGC GGGTTA TTTAGG TTAGGA TTCGGG TAAGGG",
+         tvr_patterns=("ACCCTG" * 7)[:40]),
+    dict(patterns="TTAGGG", tvr_patterns=("ACCCTG" * 6)[:33] + " TGAGGG"),
+    dict(patterns="TTAGGG TCAGGG", tvr_patterns=("ACCCTG" * 11)[:64] + " " + ("ACCCTGACCNTG" * 4)[:45]),
+]
+
+
+def _long_tvr_reads(seed, n_reads=150):
+    """Reads with a TTAGGG tract next to an ACCCTG tract (either order, at
+    either end or inside), TVR-only and plain reads; 1 % substitutions, IUPAC
+    exception letters in every 5th read, lower case in every 7th."""
+    rng = np.random.default_rng(seed)
+    bases = np.array(list("ACGT"))
+    seqs = []
+    for i in range(n_reads):
+        n = int(rng.choice([rng.integers(1, 400), rng.integers(400, 6000), rng.integers(6000, 30000)]))
+        s = list(bases[rng.integers(0, 4, n)])
+        a, b = int(rng.integers(0, 2500)), int(rng.integers(0, 2500))
+        kind = i % 4
+        tract = (("TTAGGG" * (a // 6 + 1))[:a] + ("ACCCTG" * (b // 6 + 1))[:b] if kind == 0 else
+                 ("ACCCTG" * (b // 6 + 1))[:b] + ("TTAGGG" * (a // 6 + 1))[:a] if kind == 1 else
+                 ("ACCCTG" * (b // 6 + 1))[:b] if kind == 2 else "")
+        tract = tract[:n]
+        at = 0 if i % 3 == 0 else (n - len(tract) if i % 3 == 1 else int(rng.integers(0, max(1, n - len(tract)))))
+        for k, ch in enumerate(tract):
+            s[at + k] = ch if rng.random() >= 0.01 else bases[rng.integers(0, 4)]
+        if i % 5 == 0:
+            for k in np.nonzero(rng.random(n) < 0.002)[0]:
+                s[k] = "NRYKMSWBDHV"[rng.integers(0, 11)]
+        if i % 7 == 0:
+            for k in np.nonzero(rng.random(n) < 0.01)[0]:
+                s[k] = s[k].lower()
+        seqs.append("".join(s))
+    return seqs
+
+
+@pytest.mark.parametrize("cfg", LONG_TVR, ids=["9_pat_40_letter_tvr", "33_letter_tvr", "64_letter_iupac_tvr"])
+@pytest.mark.parametrize("jit", [True, False], ids=["jit", "aot"])
+def test_long_tvr(cfg, jit):
+    seqs = _long_tvr_reads(zlib.crc32(str(sorted(cfg.items())).encode()))
+    nt = _nt(jit=jit, **cfg)
+    assert not nt.tscan  # the bundle scan takes patterns / TVRs of <= 32 letters
+    res, _ = _check_both(nt, seqs, oracle_rows(seqs, cfg["patterns"], tvr=cfg["tvr_patterns"]))
+    p3 = res["start"][:, 2] != -1
+    differs = (res["start"][:, 2] != res["start"][:, 1]) | (res["end"][:, 2] != res["end"][:, 1])
+    assert p3.sum() > 10 and differs.sum() > 5, "the long TVR did not change P3"
+
+
+def test_long_tvr_specialised_call(monkeypatch):
+    monkeypatch.setenv("NT_CALL_JIT", "1")
+    cfg = LONG_TVR[1]  # (a hiprtc build of seconds; LONG_TVR[0]'s takes minutes uncached)
+    seqs = _long_tvr_reads(7)
+    nt = _nt(jit=True, **cfg)
+    _check_both(nt, seqs, oracle_rows(seqs, cfg["patterns"], tvr=cfg["tvr_patterns"]))
+    assert nt.call_jit(), "the specialised calling kernel did not run"
+
+
+def test_tvr_length_limit():
+    from nanotel_amd import NanoTelError
+    _nt(patterns="TTAGGG", tvr_patterns="A" * 64)
+    with pytest.raises(NanoTelError) as e:
+        _nt(patterns="TTAGGG", tvr_patterns="A" * 65)
+    assert e.value.name == "NT_E_LIMIT"
+
+
 def _random_reads(cfg, jit, check_tscan=True):
     rng = np.random.default_rng(zlib.crc32(str(sorted(cfg.items())).encode()))
     seqs = []
