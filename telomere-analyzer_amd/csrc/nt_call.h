@@ -114,7 +114,8 @@ struct CtCall {
 // h + 1; with kX = 1, TVRs of 33..64 letters, [32h, 32h + 95]: words h .. h + 2):
 // x0 exact, x1 <= 1 mismatch (invalid positions are mismatches).  Letter tests
 // are made on the unshifted words and shifted by j.
-template <int NH, int kX, class D>
+// kExact: x0 only (a P1 kernel of the per-pass split; x1 is left undefined).
+template <int NH, int kX, class D, bool kExact = false>
 __device__ __forceinline__ void words_hits(const D& d, const uint32_t* Lw, const uint32_t* Hw,
                                            const uint32_t* Vw, uint32_t* x0, uint32_t* x1) {
   constexpr int kM = D::kM;
@@ -129,7 +130,7 @@ __device__ __forceinline__ void words_hits(const D& d, const uint32_t* Lw, const
         const uint32_t e0 = d.E(j, Lw[w], Hw[w]) & Vw[w], e1 = d.E(j, Lw[w + 1], Hw[w + 1]) & Vw[w + 1];
         q[j] = funnel(e1, e0, (uint32_t)(j & 31));
       }
-      combine<kM, false>(q, x0[h], x1[h]);
+      combine<kM, kExact>(q, x0[h], x1[h]);
       if (kM <= 1) x1[h] &= Vw[h];
     }
   } else {
@@ -143,7 +144,7 @@ __device__ __forceinline__ void words_hits(const D& d, const uint32_t* Lw, const
         const uint32_t Ls = funnel(Lw[h + 1], Lw[h], (uint32_t)j);
         const uint32_t Hs = funnel(Hw[h + 1], Hw[h], (uint32_t)j);
         const uint32_t q = d.E(j, Ls, Hs) & funnel(Vw[h + 1], Vw[h], (uint32_t)j);
-        x1[h] = (x1[h] & q) | x0[h];
+        if (!kExact) x1[h] = (x1[h] & q) | x0[h];
         x0[h] &= q;
       }
     }
@@ -154,7 +155,7 @@ __device__ __forceinline__ void words_hits(const D& d, const uint32_t* Lw, const
           const uint32_t Ls = funnel(Lw[h + 2], Lw[h + 1], (uint32_t)(j - 32));
           const uint32_t Hs = funnel(Hw[h + 2], Hw[h + 1], (uint32_t)(j - 32));
           const uint32_t q = d.E(j, Ls, Hs) & funnel(Vw[h + 2], Vw[h + 1], (uint32_t)(j - 32));
-          x1[h] = (x1[h] & q) | x0[h];
+          if (!kExact) x1[h] = (x1[h] & q) | x0[h];
           x0[h] &= q;
         }
       }
@@ -326,9 +327,16 @@ __device__ __forceinline__ void nb_fetch(const Lane& c, int q0, NbBlocks<K, kMar
   }
 }
 
-template <class CS>
+// kPass: -1 = every pass of a read on lanes of one wave (run); 0, 1, 2 = one
+// pass, a lane per read (run_pass: the per-pass split, where the pass's
+// mismatch rule, TVR use and P1's raw views are compile-time).
+template <class CS, int kPass = -1>
 struct Call {
 static constexpr int kX = CS::kLong ? 1 : 0;  // extra plane / hit word for TVRs of 33..64 letters
+static __device__ __forceinline__ int pk(const Lane& c) { return kPass >= 0 ? (kPass ? 1 : 0) : c.k; }
+static __device__ __forceinline__ bool ptvr(const Lane& c) { return kPass >= 0 ? kPass == 2 : c.use_tvr; }
+static __device__ __forceinline__ bool praw(const Lane& c) { return CS::kMayRaw && kPass <= 0 && c.raw; }
+static constexpr bool kTvrCode = CS::kNTvr != 0 && (kPass < 0 || kPass == 2);
 using NbB4 = NbBlocks<4, false, kX>;
 using NbB5 = NbBlocks<5, true, kX>;
 
@@ -363,18 +371,19 @@ static __device__ __forceinline__ void nb_compute(const Lane& c, int q0, const N
     launder_words<NP>(Lw, Lp);
     launder_words<NP>(Hw, Hp);
     launder_words<NP>(Vw, Vp);
-    words_hits<NH, kX>(d, Lp, Hp, Vp, x0, x1);
+    words_hits<NH, kX, decltype(d), kPass == 0>(d, Lp, Hp, Vp, x0, x1);
     if (c.rc.n_exc) {
 #pragma unroll
       for (int h = 0; h < NH; ++h)
         patch_exceptions(c.rc, (int64_t)q0 + 32 * (h + T0), 0, c.n - 1, *d.P, false, x0[h], x1[h]);
     }
     // coverage word ci (i = ci - E) from hit words i and i - 1 (patterns <= 18 letters)
+    const bool k1 = pk(c) != 0;
 #pragma unroll
     for (int ci = 0; ci < NC; ++ci)
-      nb.cov[ci + 1 - E] |= spread<kM>(c.k ? x1[ci + 1 + kX] : x0[ci + 1 + kX], c.k ? x1[ci + kX] : x0[ci + kX], m);
+      nb.cov[ci + 1 - E] |= spread<kM>(k1 ? x1[ci + 1 + kX] : x0[ci + 1 + kX], k1 ? x1[ci + kX] : x0[ci + kX], m);
     if constexpr (kMarks) {
-      if (CS::kMayRaw && c.raw && pi == 0) {
+      if (praw(c) && pi == 0) {
 #pragma unroll
         for (int ci = 0; ci < NC; ++ci) {
           nb.rs[ci] = x0[ci + 1 + kX];
@@ -383,7 +392,7 @@ static __device__ __forceinline__ void nb_compute(const Lane& c, int q0, const N
       }
     }
   });
-  if (CS::kNTvr != 0 && prog->n_tvr > 0) {
+  if (kTvrCode && prog->n_tvr > 0) {
     CS::for_tvr(prog, [&](int, auto d) {
       constexpr int kM = decltype(d)::kM;
       uint32_t x0[NH], x1[NH];
@@ -397,7 +406,7 @@ static __device__ __forceinline__ void nb_compute(const Lane& c, int q0, const N
         for (int h = 0; h < NH; ++h)
           patch_exceptions(c.rc, (int64_t)q0 + 32 * (h + T0), 0, c.n - 1, *d.P, false, x0[h], x1[h]);
       }
-      if (c.use_tvr) {
+      if (ptvr(c)) {
 #pragma unroll
         for (int ci = 0; ci < NC; ++ci) {
           if constexpr (kX > 0)
@@ -431,7 +440,7 @@ static __device__ __forceinline__ int nb_min_start(const Lane& c, const Nb<K>& n
 #pragma unroll
   for (int i = 0; i < K; ++i) {
     const uint32_t cur = nb.cov[i + 1];
-    const uint32_t mk = (CS::kMayRaw && c.raw) ? nb.rs[i + 1] : (cur & ~((cur << 1) | (nb.cov[i] >> 31)));
+    const uint32_t mk = praw(c) ? nb.rs[i + 1] : (cur & ~((cur << 1) | (nb.cov[i] >> 31)));
     const uint32_t m = mk & range_mask((int64_t)nb.q0 + 32 * i, a, b);
     if (!found && m) {
       res = nb.q0 + 32 * i + __builtin_ctz(m) + 1;
@@ -450,7 +459,7 @@ static __device__ __forceinline__ int nb_max_end(const Lane& c, const Nb<K>& nb,
 #pragma unroll
   for (int i = K - 1; i >= 0; --i) {
     const uint32_t cur = nb.cov[i + 1];
-    const uint32_t mk = (CS::kMayRaw && c.raw) ? nb.re[i + 1] : (cur & ~((cur >> 1) | (nb.cov[i + 2] << 31)));
+    const uint32_t mk = praw(c) ? nb.re[i + 1] : (cur & ~((cur >> 1) | (nb.cov[i + 2] << 31)));
     const uint32_t m = mk & range_mask((int64_t)nb.q0 + 32 * i, a, b);
     if (!found && m) {
       res = nb.q0 + 32 * i + (31 - __builtin_clz(m)) + 1;
@@ -792,22 +801,22 @@ template <int K>
 static __device__ __forceinline__ bool step_extreme(const Lane& c, const Pw<K>& w, int a1, int b1, bool right, int& val) {
   const NtProgram* prog = c.prog;
   const int A = a1 - 1, Bz = b1 - 1, base = A - 1;
-  const bool only_exact = c.use_tvr && c.k == 0;
+  const bool only_exact = ptvr(c) && pk(c) == 0;
   bool any = false;
   int best = right ? kIntMin : kIntMax;
   auto visit = [&](bool is_tvr, const auto& d) {
-    const int k = (is_tvr || only_exact) ? 0 : c.k;
+    const int k = (is_tvr || only_exact) ? 0 : pk(c);
     uint32_t a0, a1w;
     hits_at_w(c, w, d, base, A, Bz, a0, a1w);
     uint32_t h = k ? a1w : a0;
-    if (is_tvr && !c.use_tvr) h = 0u;  // TVRs extend P3 only
+    if (is_tvr && !ptvr(c)) h = 0u;  // TVRs extend P3 only
     if (!h) return;
     any = true;
     if (right) best = max(best, base + (31 - __builtin_clz(h)) + d.m());
     else best = min(best, base + __builtin_ctz(h) + 1);
   };
   CS::for_pat_eq(prog, [&](int, auto d) { visit(false, d); });
-  if (CS::kNTvr != 0 && prog->n_tvr > 0) CS::for_tvr_eq(prog, [&](int, auto d) { visit(true, d); });
+  if (kTvrCode && prog->n_tvr > 0) CS::for_tvr_eq(prog, [&](int, auto d) { visit(true, d); });
   if (any) val = best;
   return any;
 }
@@ -946,6 +955,78 @@ static __device__ __forceinline__ void call_pass(Lane& c, int& out_s, int& out_e
 #endif
 }
 
+// The lane of read r, pass p.
+static __device__ __forceinline__ void init_lane(Lane& c, const NtProgram* __restrict__ prog, const NtBatch& B,
+                                                 const NtOut& O, const uint64_t* __restrict__ tmask, uint64_t r,
+                                                 int p, uint64_t* tm_lds, uint32_t* pw_lds) {
+  const int np = prog->n_pass, L = prog->L;
+  const uint32_t n32 = B.len[r];
+#if NT_CALL_TM_LDS
+  c.tmw = tm_lds + threadIdx.x;
+#endif
+#if NT_CALL_PW_LDS
+  c.pws = pw_lds + threadIdx.x;
+#endif
+  c.rc.n = n32;
+  c.rc.nblk = (int32_t)((n32 + 31u) >> 5);
+  c.rc.blk = reinterpret_cast<const uint2*>(B.planes) + B.blk_off[r];
+  c.rc.n_exc = 0;
+  c.rc.exc_pos = nullptr;
+  c.rc.exc_code = nullptr;
+  if (B.exc_off) {
+    const uint32_t e0 = B.exc_off[r], e1 = B.exc_off[r + 1];
+    c.rc.n_exc = (int32_t)(e1 - e0);
+    c.rc.exc_pos = B.exc_pos + e0;
+    c.rc.exc_code = B.exc_code + e0;
+  }
+  c.prog = prog;
+  c.n = (int)n32;
+  c.L = L;
+  c.nw = (int)split_window_count(c.n, L);
+  c.nmw = (c.nw + 63) >> 6;
+  const uint64_t woff = B.win_off[r];
+  const uint64_t* tmr = tmask + aux_base(woff, r, np);
+  const uint32_t* ckr = reinterpret_cast<const uint32_t*>(tmr + np * aux_nmw(c.nw));
+  c.c8 = prog->cnt8 != 0;
+  c.cnt = static_cast<const uint8_t*>(O.win_counts) +
+          (woff * np + (uint64_t)p * NT_WIN_ROWS((uint64_t)c.nw)) * (c.c8 ? 1u : 2u);
+  c.tm = tmr + p * c.nmw;
+  c.ck = ckr + p * aux_nck(c.nw);
+  c.k = p == 0 ? 0 : 1;
+  c.use_tvr = p == 2;
+  c.raw = p == 0 && prog->raw_p1;
+}
+
+// The per-pass split (kPass >= 0): a lane per read, this pass's start / end /
+// density; an error is left in end (-2: find_right_telo on a 0-row table, -3:
+// a negative width) and the flags are made by nt_call_combine_kernel after
+// every pass's launch.  Reads the scan skipped (odd blk_off) are left to it.
+static __device__ __forceinline__ void run_pass(const NtProgram* __restrict__ prog, NtBatch B, NtOut O,
+                                                const uint64_t* __restrict__ tmask, const uint32_t* __restrict__ thr,
+                                                uint32_t thr_size, int fix_last, uint64_t* tm_lds, uint32_t* pw_lds) {
+  static_assert(kPass >= 0 && kPass < 3, "run_pass: one pass");
+  const uint64_t total = B.list ? B.n_list : B.n_reads;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t idx = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; idx < total; idx += stride) {
+    const uint64_t r = B.list ? (uint64_t)B.list[idx] : idx;
+    if (r == 0xFFFFFFFFull || (B.blk_off[r] & 1u)) continue;
+    Lane c;
+    init_lane(c, prog, B, O, tmask, r, kPass, tm_lds, pw_lds);
+#ifndef NT_DBG_NO_FIXLAST
+    if (fix_last) call_fix_last(c, thr, thr_size);
+#endif
+    int s = -1, e = -1;
+    double d = 0.0;
+    uint32_t flags = 0u;
+    call_pass(c, s, e, d, flags);
+    if (flags & NT_FLAG_ERR_RIGHT) e = -2;
+    else if (flags & NT_FLAG_ERR_WIDTH) e = -3;
+    O.start[r * 3 + kPass] = s;
+    O.end[r * 3 + kPass] = e;
+    O.density[r * 3 + kPass] = d;
+  }
+}
+
 // One lane per (read, pass): the passes of a read are independent until the
 // row is assembled, so a read's G = 2 (P1, P2) or 4 (P1-P3 and an idle lane)
 // lanes call them side by side -- half the dependent memory round trips per
@@ -958,7 +1039,7 @@ static __device__ __forceinline__ void call_pass(Lane& c, int& out_s, int& out_e
 static __device__ __forceinline__ void run(const NtProgram* __restrict__ prog, NtBatch B, NtOut O,
                                            const uint64_t* __restrict__ tmask, const uint32_t* __restrict__ thr,
                                            uint32_t thr_size, int fix_last, uint64_t* tm_lds, uint32_t* pw_lds) {
-  const int np = prog->n_pass, L = prog->L;
+  const int np = prog->n_pass;
   const int lg = np <= 2 ? 1 : 2;  // log2(G)
   // the reads: B.list[0 .. n_list) when given (~0u entries: none), else all
   const uint64_t total = (B.list ? B.n_list : B.n_reads) << lg;
@@ -974,44 +1055,10 @@ static __device__ __forceinline__ void run(const NtProgram* __restrict__ prog, N
     int w = kIntMin;
     bool align = false;
     if (in) {
-      const uint32_t n32 = B.len[r];
       align = (B.blk_off[r] & 1u) != 0;  // the scan skipped this read (layout contract)
       if (!align && p < np) {
         Lane c;
-#if NT_CALL_TM_LDS
-        c.tmw = tm_lds + threadIdx.x;
-#endif
-#if NT_CALL_PW_LDS
-        c.pws = pw_lds + threadIdx.x;
-#endif
-        c.rc.n = n32;
-        c.rc.nblk = (int32_t)((n32 + 31u) >> 5);
-        c.rc.blk = reinterpret_cast<const uint2*>(B.planes) + B.blk_off[r];
-        c.rc.n_exc = 0;
-        c.rc.exc_pos = nullptr;
-        c.rc.exc_code = nullptr;
-        if (B.exc_off) {
-          const uint32_t e0 = B.exc_off[r], e1 = B.exc_off[r + 1];
-          c.rc.n_exc = (int32_t)(e1 - e0);
-          c.rc.exc_pos = B.exc_pos + e0;
-          c.rc.exc_code = B.exc_code + e0;
-        }
-        c.prog = prog;
-        c.n = (int)n32;
-        c.L = L;
-        c.nw = (int)split_window_count(c.n, L);
-        c.nmw = (c.nw + 63) >> 6;
-        const uint64_t woff = B.win_off[r];
-        const uint64_t* tmr = tmask + aux_base(woff, r, np);
-        const uint32_t* ckr = reinterpret_cast<const uint32_t*>(tmr + np * aux_nmw(c.nw));
-        c.c8 = prog->cnt8 != 0;
-        c.cnt = static_cast<const uint8_t*>(O.win_counts) +
-                (woff * np + (uint64_t)p * NT_WIN_ROWS((uint64_t)c.nw)) * (c.c8 ? 1u : 2u);
-        c.tm = tmr + p * c.nmw;
-        c.ck = ckr + p * aux_nck(c.nw);
-        c.k = p == 0 ? 0 : 1;
-        c.use_tvr = p == 2;
-        c.raw = p == 0 && prog->raw_p1;
+        init_lane(c, prog, B, O, tmask, r, p, tm_lds, pw_lds);
 #ifndef NT_DBG_NO_FIXLAST  // timing experiments only (wrong results for bundled reads)
         if (fix_last) call_fix_last(c, thr, thr_size);
 #endif
@@ -1082,7 +1129,8 @@ static __device__ __forceinline__ void run(const NtProgram* __restrict__ prog, N
 #define NT_CALL_PW_DECL
 #define NT_CALL_PW_ARG nullptr
 #endif
-// The calling kernel NAME for pattern-set policy CS (256 threads a block).
+// The calling kernel NAME for pattern-set policy CS (256 threads a block);
+// NT_CALL_KERNEL_PASS: the pass-P kernel of the per-pass split.
 #define NT_CALL_KERNEL(NAME, CS)                                                                             \
   extern "C" __global__ void __launch_bounds__(256) NT_CALL_ATTR                                             \
   NAME(const NtProgram* __restrict__ prog, NtBatch B, NtOut O, const uint64_t* __restrict__ tmask,           \
@@ -1090,4 +1138,12 @@ static __device__ __forceinline__ void run(const NtProgram* __restrict__ prog, N
     NT_CALL_TM_DECL                                                                                          \
     NT_CALL_PW_DECL                                                                                          \
     nt::Call<CS>::run(prog, B, O, tmask, thr, thr_size, fix_last, NT_CALL_TM_ARG, NT_CALL_PW_ARG);          \
+  }
+#define NT_CALL_KERNEL_PASS(NAME, CS, P)                                                                     \
+  extern "C" __global__ void __launch_bounds__(256) NT_CALL_ATTR                                             \
+  NAME(const NtProgram* __restrict__ prog, NtBatch B, NtOut O, const uint64_t* __restrict__ tmask,           \
+       const uint32_t* __restrict__ thr, uint32_t thr_size, int fix_last) {                                  \
+    NT_CALL_TM_DECL                                                                                          \
+    NT_CALL_PW_DECL                                                                                          \
+    nt::Call<CS, P>::run_pass(prog, B, O, tmask, thr, thr_size, fix_last, NT_CALL_TM_ARG, NT_CALL_PW_ARG);  \
   }

@@ -54,9 +54,9 @@ hipError_t nt_tjit_launch(void* fn, int grid, hipStream_t stream, const NtBatch*
                           uint64_t* tmask, unsigned long long* queue, uint32_t thr_full);
 void* nt_cjit_get(int device, const NtProgram& P, std::string& err);
 int nt_jit_prebuild_program(const NtProgram& P, const std::string& arch);
-hipError_t nt_cjit_launch(void* fn, int grid, hipStream_t stream, const NtProgram* prog, const NtBatch* B,
-                          const NtOut* O, const uint64_t* tmask, const uint32_t* thr, uint32_t thr_size,
-                          int fix_last);
+hipError_t nt_cjit_launch(void* h, int np, int cu_count, hipStream_t stream, const NtProgram* prog,
+                          const NtBatch* B, const NtOut* O, const uint64_t* tmask, const uint32_t* thr,
+                          uint32_t thr_size, int fix_last);
 hipError_t nt_jit_launch(void* fn, int grid, size_t lds_bytes, hipStream_t stream,
                          const NtProgram* prog, const uint32_t* thr, const NtBatch* B,
                          const NtOut* O, uint64_t* tmask, unsigned long long* queue,
@@ -254,12 +254,18 @@ static int long_tvr(const NtProgram& P) {
   return 0;
 }
 
+// The calling of batch B (its list, or all its reads): the specialised
+// kernel(s) when cfn, else the ahead-of-time kernel with np <= 2 ? 2 : 4
+// lanes a read; at most 64 blocks a CU (grid-stride).
 static hipError_t launch_call(nt_ctx* ctx, void* cfn, const NtBatch* B, const NtOut* O, const uint64_t* tm,
-                              int fix_last, int grid, hipStream_t s) {
+                              int fix_last, hipStream_t s) {
   const uint32_t* thr = (const uint32_t*)ctx->thr.p;
   const uint32_t ts = (uint32_t)ctx->thr_h.size();
-  return cfn ? nt_cjit_launch(cfn, grid, s, ctx->prog_dev, B, O, tm, thr, ts, fix_last)
-             : nt_dev_launch_call(ctx->prog_dev, B, O, tm, thr, ts, fix_last, long_tvr(ctx->prog), grid, s);
+  const int np = ctx->prog.n_pass;
+  if (cfn) return nt_cjit_launch(cfn, np, ctx->cu_count, s, ctx->prog_dev, B, O, tm, thr, ts, fix_last);
+  const uint64_t lanes = (B->list ? B->n_list : B->n_reads) * (np <= 2 ? 2u : 4u);
+  const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((lanes + 255) / 256, (uint64_t)ctx->cu_count * 64));
+  return nt_dev_launch_call(ctx->prog_dev, B, O, tm, thr, ts, fix_last, long_tvr(ctx->prog), grid, s);
 }
 
 static int hip_fail(nt_ctx* ctx, hipError_t e, const char* what) {
@@ -461,13 +467,17 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
   nsub = std::min<uint64_t>(nsub, std::max<uint64_t>(1, batch->n_reads / 256));
   // the bundle scan's sub-batches (bundle ranges): the calling kernel of range
   // k runs on the call stream beside the bundle scan of range k+1 (the scan is
-  // bandwidth-bound, the calling latency-bound); NT_TSUB ranges, default 2
-  // (1M x 50 kb, one box, two runs each: 3.43-3.45 ms per batch at 1, 3.30-3.33 at
-  // 2, 3.38-3.41 at 3 geometric ranges, ratio 0.3)
+  // bandwidth-bound, the calling latency-bound), so only the last range's
+  // calling is exposed.  Ranges of at most NT_TSUB_BUNDLES bundles (default
+  // 16384 = 524,288 reads), at least 2, at most kMaxTsub; NT_TSUB sets the
+  // count (1M x 50 kb, one box, two runs each: 3.43-3.45 ms per batch at 1,
+  // 3.30-3.33 at 2, 3.38-3.41 at 3 geometric ranges, ratio 0.3)
   uint64_t tsub = 1;
   if (tscan) {
     nsub = 1;
-    tsub = 2;
+    uint64_t per = 16384;
+    if (const char* v = std::getenv("NT_TSUB_BUNDLES")) per = std::max<uint64_t>(1, std::strtoull(v, nullptr, 10));
+    tsub = std::max<uint64_t>(2, (batch->n_bundles + per - 1) / per);
     if (const char* v = std::getenv("NT_TSUB")) tsub = std::max<uint64_t>(1, std::strtoull(v, nullptr, 10));
     tsub = std::min<uint64_t>({tsub, std::max<uint64_t>(1, batch->n_bundles / 64), (uint64_t)nt_ctx::kMaxTsub});
   }
@@ -555,8 +565,6 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
       NtBatch Bc = B;
       Bc.list = Bt.bnd_read;
       Bc.n_list = NT_BUNDLE * Bt.n_bundles;
-      const uint64_t lanes = Bc.n_list * (np <= 2 ? 2u : 4u);
-      const int cgrid = (int)std::max<uint64_t>(1, std::min<uint64_t>((lanes + 255) / 256, (uint64_t)ctx->cu_count * 64));
       hipStream_t cs = ctx->stream;
       if (tsub > 1) {
         if ((e = hipEventRecord(ctx->ev_scan, ctx->stream)) != hipSuccess ||
@@ -565,7 +573,7 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
         cs = ctx->call_stream;
       }
       if (!dbg_skip_call &&
-          (e = launch_call(ctx, cfn, &Bc, &O, tmask, 1, cgrid, cs)) != hipSuccess)
+          (e = launch_call(ctx, cfn, &Bc, &O, tmask, 1, cs)) != hipSuccess)
         return hip_fail(ctx, e, "launch nt_call_kernel");
     }
   }
@@ -651,26 +659,19 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
       (void)hipEventRecord(ev[4 + 2 * pe], ctx->stream);
       ctx->ev_nt[ctx->n_ev - 1] = pe + 1;
     }
-    // one lane per (read, pass): 2 lanes per read, 4 with TVRs
-    const uint64_t call_lanes = nr * (np <= 2 ? 2u : 4u);
-    const uint64_t call_grid = std::max<uint64_t>(1, std::min<uint64_t>((call_lanes + 255) / 256, (uint64_t)ctx->cu_count * 64));
     if (tscan) {
       // the reads of the per-read scan (the bundled ones are called above)
-      if (n_scan > 0 && !dbg_skip_call) {
-        const uint64_t lanes = n_scan * (np <= 2 ? 2u : 4u);
-        const int cgrid = (int)std::max<uint64_t>(1, std::min<uint64_t>((lanes + 255) / 256, (uint64_t)ctx->cu_count * 64));
-        e = launch_call(ctx, cfn, &Bk, &Ok, tmk, 0, cgrid, ctx->stream);
-      }
+      if (n_scan > 0 && !dbg_skip_call) e = launch_call(ctx, cfn, &Bk, &Ok, tmk, 0, ctx->stream);
     } else if (nsub == 1) {
       if (ev) (void)hipEventRecord(ev[1], ctx->stream);
       e = dbg_skip_call ? hipSuccess
-                        : launch_call(ctx, cfn, &Bk, &Ok, tmk, 0, (int)call_grid, ctx->stream);
+                        : launch_call(ctx, cfn, &Bk, &Ok, tmk, 0, ctx->stream);
     } else {
       // calling kernel of this sub-batch on the call stream, after its scan
       if ((e = hipEventRecord(ctx->ev_scan, ctx->stream)) != hipSuccess ||
           (e = hipStreamWaitEvent(ctx->call_stream, ctx->ev_scan, 0)) != hipSuccess)
         return hip_fail(ctx, e, "stream dependency");
-      e = launch_call(ctx, cfn, &Bk, &Ok, tmk, 0, (int)call_grid, ctx->call_stream);
+      e = launch_call(ctx, cfn, &Bk, &Ok, tmk, 0, ctx->call_stream);
     }
     if (e != hipSuccess) return hip_fail(ctx, e, "launch nt_call_kernel");
   }

@@ -27,6 +27,8 @@
 
 #include "nt_common.h"
 
+extern "C" hipError_t nt_dev_launch_combine(const NtBatch* B, const NtOut* O, int np, int grid, hipStream_t stream);
+
 namespace {
 
 #include "nt_jit_src.inc"  // kJitCommon, kJitDevice, kJitScan (raw string literals)
@@ -43,9 +45,13 @@ std::map<std::string, JitEntry> g_cache;
 
 // the calling kernel's modules (a separate hiprtc program: ~20 s to build, so
 // it is built only for batches that pay for it, see nt_host.cpp)
+// fn[0]: the one-kernel form (Call::run); split: fn[p] = pass p's kernel
+// (Call<CS, p>::run_pass), then nt_call_combine_kernel.
 struct CallEntry {
   hipModule_t mod = nullptr;
-  hipFunction_t fn = nullptr;
+  hipFunction_t fn[3] = {};
+  int nfn = 0;
+  bool split = false;
   std::string err;
 };
 std::map<std::string, CallEntry> g_ccache;
@@ -142,6 +148,21 @@ NT_JIT_KERNELS(nt_scan_jit_nh, false)
   return s;
 }
 
+}  // namespace
+
+// The per-pass split of the calling kernel: a kernel per pass, each with its
+// pass's mismatch rule, TVR use and raw views compile-time and registers of
+// its own (the P1 / P2 kernels hold no TVR code), and no idle lane (the
+// one-kernel form gives a 3-pass read 4 lanes).  Default for 3-pass programs;
+// NT_CALL_SPLIT=0 / 1 forces it off / on.
+bool nt_call_split(const NtProgram& P) {
+  const char* e = std::getenv("NT_CALL_SPLIT");
+  if (e && *e) return e[0] == '1';
+  return P.n_pass == 3;
+}
+
+namespace {
+
 // The program's source of the calling kernel (nt_call.h) with its patterns as types.
 std::string call_source(const NtProgram& P) {
   std::string pats, tvrs, pats_eq, tvrs_eq;
@@ -157,7 +178,17 @@ std::string call_source(const NtProgram& P) {
   s += "#include \"nt_call.h\"\n";
   s += "using JitCall = nt::CtCall<nt::CtList<" + pats + ">, nt::CtList<" + tvrs + ">, nt::CtList<" + pats_eq +
        ">, nt::CtList<" + tvrs_eq + ">, " + (P.raw_p1 ? "true" : "false") + ">;\n";
-  s += "NT_CALL_KERNEL(nt_call_jit, JitCall)\n";
+  if (nt_call_split(P)) {
+    // per-pass occupancy: NT_CALL_WAVES_P<p> (the spill fallback sets one to 2)
+    for (int p = 0; p < P.n_pass; ++p) {
+      const std::string ps = std::to_string(p);
+      s += "#ifndef NT_CALL_WAVES_P" + ps + "\n#define NT_CALL_WAVES_P" + ps + " NT_CALL_WAVES_PER_EU\n#endif\n";
+      s += "#undef NT_CALL_ATTR\n#define NT_CALL_ATTR __attribute__((amdgpu_waves_per_eu(NT_CALL_WAVES_P" + ps + ")))\n";
+      s += "NT_CALL_KERNEL_PASS(nt_call_jit_p" + ps + ", JitCall, " + ps + ")\n";
+    }
+  } else {
+    s += "NT_CALL_KERNEL(nt_call_jit, JitCall)\n";
+  }
   return s;
 }
 
@@ -404,42 +435,52 @@ void* nt_cjit_get(int device, const NtProgram& P, std::string& err) {
     std::lock_guard<std::mutex> lk(g_mu);
     auto it = g_ccache.find(key);
     if (it != g_ccache.end()) {
-      if (!it->second.fn) err = it->second.err;
-      return (void*)it->second.fn;
+      if (!it->second.nfn) err = it->second.err;
+      return it->second.nfn ? (void*)&it->second : nullptr;
     }
   }
   // built without the lock (seconds): other contexts' lookups go on meanwhile;
   // a build that loses a race to the same key is dropped
   {
     CallEntry e;
+    e.split = nt_call_split(P);
+    const int nk = e.split ? P.n_pass : 1;
     auto build = [&](const std::string& s) {
-      if (compile_module(device, s, e.mod, e.err) &&
-          hipModuleGetFunction(&e.fn, e.mod, "nt_call_jit") != hipSuccess) {
-        e.fn = nullptr;
-        e.err = "hipModuleGetFunction(nt_call_jit)";
+      e.nfn = 0;
+      if (!compile_module(device, s, e.mod, e.err)) return;
+      for (int k = 0; k < nk; ++k) {
+        const std::string name = e.split ? "nt_call_jit_p" + std::to_string(k) : std::string("nt_call_jit");
+        if (hipModuleGetFunction(&e.fn[k], e.mod, name.c_str()) != hipSuccess) {
+          e.err = "hipModuleGetFunction(" + name + ")";
+          return;
+        }
       }
+      e.nfn = nk;
     };
     build(src);
     // Several patterns and TVRs raise the register demand of the unrolled
     // neighbourhood code: at 3 waves/SIMD (168 VGPRs) the c4 set spilled 107
     // VGPRs to scratch and called in 3.6 ms per 2M x 50 kb; at 2 (253 VGPRs, no
-    // spill) 2.0 ms.  A build that spills more than kCallScratchMax bytes a
-    // lane is redone at 2 waves/SIMD (a few spilled registers cost less than
-    // the occupancy: the 1-pattern kernels run at 3-4).
+    // spill) 2.0 ms.  A kernel that spills more than kCallScratchMax bytes a
+    // lane is rebuilt at 2 waves/SIMD (a few spilled registers cost less than
+    // the occupancy: the 1-pattern kernels run at 3-4); in the split, only the
+    // passes that spill.
     constexpr int kCallScratchMax = 64;
-    int scratch = 0;
-    const bool forced = xo && std::strstr(xo, "NT_CALL_WAVES_PER_EU");  // a tuning run sets it
-    if (e.fn && !forced &&
-        hipFuncGetAttribute(&scratch, HIP_FUNC_ATTRIBUTE_LOCAL_SIZE_BYTES, e.fn) == hipSuccess &&
-        scratch > kCallScratchMax) {
-      const hipModule_t m1 = e.mod;
-      const hipFunction_t f1 = e.fn;
-      build("#define NT_CALL_WAVES_PER_EU 2\n" + src);
-      if (e.fn) {
-        (void)hipModuleUnload(m1);
+    const bool forced = xo && std::strstr(xo, "NT_CALL_WAVES_P");  // a tuning run sets it
+    std::string redo;
+    for (int k = 0; k < e.nfn && !forced; ++k) {
+      int scratch = 0;
+      if (hipFuncGetAttribute(&scratch, HIP_FUNC_ATTRIBUTE_LOCAL_SIZE_BYTES, e.fn[k]) == hipSuccess &&
+          scratch > kCallScratchMax)
+        redo += e.split ? "#define NT_CALL_WAVES_P" + std::to_string(k) + " 2\n" : "#define NT_CALL_WAVES_PER_EU 2\n";
+    }
+    if (!redo.empty()) {
+      const CallEntry e1 = e;
+      build(redo + src);
+      if (e.nfn) {
+        (void)hipModuleUnload(e1.mod);
       } else {
-        e.mod = m1;
-        e.fn = f1;
+        e = e1;
       }
     }
     std::lock_guard<std::mutex> lk(g_mu);
@@ -449,18 +490,31 @@ void* nt_cjit_get(int device, const NtProgram& P, std::string& err) {
     } else if (e.mod) {
       (void)hipModuleUnload(e.mod);
     }
-    if (!it->second.fn) err = it->second.err;
-    return (void*)it->second.fn;
+    if (!it->second.nfn) err = it->second.err;
+    return it->second.nfn ? (void*)&it->second : nullptr;
   }
 }
 
-hipError_t nt_cjit_launch(void* fn, int grid, hipStream_t stream, const NtProgram* prog, const NtBatch* B,
-                          const NtOut* O, const uint64_t* tmask, const uint32_t* thr, uint32_t thr_size,
-                          int fix_last) {
+// The specialised calling of batch B (h from nt_cjit_get): the one kernel
+// with np <= 2 ? 2 : 4 lanes a read, or a kernel per pass with a lane a read
+// and the flag combine after them.  cu_count bounds the grid (64 blocks a CU).
+hipError_t nt_cjit_launch(void* h, int np, int cu_count, hipStream_t stream, const NtProgram* prog,
+                          const NtBatch* B, const NtOut* O, const uint64_t* tmask, const uint32_t* thr,
+                          uint32_t thr_size, int fix_last) {
+  const CallEntry& e = *static_cast<const CallEntry*>(h);
   NtBatch b = *B;
   NtOut o = *O;
   void* args[] = {&prog, &b, &o, &tmask, &thr, &thr_size, &fix_last};
-  return hipModuleLaunchKernel((hipFunction_t)fn, (unsigned)grid, 1, 1, 256, 1, 1, 0, stream, args, nullptr);
+  const uint64_t reads = B->list ? B->n_list : B->n_reads;
+  const uint64_t lanes = e.split ? reads : reads * (np <= 2 ? 2u : 4u);
+  uint64_t grid = (lanes + 255) / 256;
+  if (grid > (uint64_t)cu_count * 64) grid = (uint64_t)cu_count * 64;
+  if (grid < 1) grid = 1;
+  for (int k = 0; k < e.nfn; ++k) {
+    const hipError_t r = hipModuleLaunchKernel(e.fn[k], (unsigned)grid, 1, 1, 256, 1, 1, 0, stream, args, nullptr);
+    if (r != hipSuccess) return r;
+  }
+  return e.split ? nt_dev_launch_combine(B, O, np, (int)grid, stream) : hipSuccess;
 }
 
 // Fill the on-disk cache with the program's code objects (the scan module and
@@ -474,6 +528,15 @@ int nt_jit_prebuild_program(const NtProgram& P, const std::string& arch) {
   if (!get_code(a, jit_source(P), code, err)) return -7;
   const std::string cs = call_source(P);
   if (!get_code(a, cs, code, err)) return -7;
-  if (!get_code(a, "#define NT_CALL_WAVES_PER_EU 2\n" + cs, code, err)) return -7;
+  // the spill fallbacks a GPU may ask for (nt_cjit_get): every kernel, or the
+  // split's TVR pass alone, at 2 waves/SIMD
+  if (nt_call_split(P)) {
+    if (P.n_pass == 3 && !get_code(a, "#define NT_CALL_WAVES_P2 2\n" + cs, code, err)) return -7;
+    std::string all;
+    for (int k = 0; k < P.n_pass; ++k) all += "#define NT_CALL_WAVES_P" + std::to_string(k) + " 2\n";
+    if (!get_code(a, all + cs, code, err)) return -7;
+  } else if (!get_code(a, "#define NT_CALL_WAVES_PER_EU 2\n" + cs, code, err)) {
+    return -7;
+  }
   return 0;
 }

@@ -54,6 +54,49 @@ NT_CALL_KERNEL(nt_call_kernel, RtCall)
 // programs with a TVR of more than 32 letters (wider neighbourhoods)
 NT_CALL_KERNEL(nt_call_kernel_long, RtCallLong)
 
+// After the per-pass calling kernels (NT_CALL_KERNEL_PASS, one launch per
+// pass): the row flags of each read -- NA per pass, the errors the passes left
+// in end (-2 / -3), telomeric = max width over the passes >= 30 (NanoTel.R:
+// 1847-1868) -- and the -1 / -1 / 0 of the passes the program does not run,
+// as the one-kernel form (Call::run) writes them.
+__global__ void __launch_bounds__(256) nt_call_combine_kernel(NtBatch B, NtOut O, int np) {
+  const uint64_t total = B.list ? B.n_list : B.n_reads;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t idx = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; idx < total; idx += stride) {
+    const uint64_t r = B.list ? (uint64_t)B.list[idx] : idx;
+    if (r == 0xFFFFFFFFull) continue;
+    if (B.blk_off[r] & 1u) {  // the scan skipped this read (layout contract)
+      for (int p = 0; p < 3; ++p) {
+        O.start[r * 3 + p] = -1;
+        O.end[r * 3 + p] = -1;
+        O.density[r * 3 + p] = 0.0;
+      }
+      O.flags[r] = (uint8_t)(NT_FLAG_DONE | NT_FLAG_ERR_ALIGN);
+      continue;
+    }
+    uint32_t flags = 0u;
+    int w = -2147483647 - 1;
+    for (int p = 0; p < np; ++p) {
+      const int s0 = O.start[r * 3 + p];
+      int e0 = O.end[r * 3 + p];
+      if (e0 == -2 || e0 == -3) {
+        flags |= e0 == -2 ? NT_FLAG_ERR_RIGHT : NT_FLAG_ERR_WIDTH;
+        e0 = -1;
+        O.end[r * 3 + p] = -1;
+      }
+      if (s0 == -1) flags |= 1u << (NT_FLAG_NA_SHIFT + p);
+      w = max(w, e0 - s0 + 1);
+    }
+    for (int p = np; p < 3; ++p) {
+      O.start[r * 3 + p] = -1;
+      O.end[r * 3 + p] = -1;
+      O.density[r * 3 + p] = 0.0;
+    }
+    if (w >= 30) flags |= NT_FLAG_TELOMERIC;
+    O.flags[r] = (uint8_t)(flags | NT_FLAG_DONE);
+  }
+}
+
 
 // ============================================================ synthetic reads
 
@@ -368,6 +411,11 @@ hipError_t nt_dev_launch_call(const NtProgram* prog, const NtBatch* B, const NtO
   else
     hipLaunchKernelGGL(nt::nt_call_kernel, dim3(call_grid), dim3(256), 0, stream, prog, *B, *O, tmask, thr,
                        thr_size, fix_last);
+  return hipGetLastError();
+}
+
+hipError_t nt_dev_launch_combine(const NtBatch* B, const NtOut* O, int np, int grid, hipStream_t stream) {
+  hipLaunchKernelGGL(nt::nt_call_combine_kernel, dim3(grid), dim3(256), 0, stream, *B, *O, np);
   return hipGetLastError();
 }
 
