@@ -275,6 +275,35 @@ def test_tvr_length_limit():
     assert e.value.name == "NT_E_LIMIT"
 
 
+# Packed bundle groups (nt_common.h): bundles of short reads share stripes at
+# 16-column offsets, their bitmask words are composed across stripes, their
+# checkpoints restart per bundle.  10 kb reads (4 bundles in 7 stripes), reads
+# whose windows fill every column of their bundle (3,200 and 3,160 bases: the
+# checkpoint at window nw lies past the bundle), ragged lengths, 700-base reads.
+def _packed_reads(seed):
+    rng = np.random.default_rng(seed)
+    lens = ([10000] * 128 + [3200] * 64 + [3160] * 64 + [int(x) for x in rng.integers(1500, 4000, 96)] +
+            [700] * 32 + [int(x) for x in rng.integers(5000, 12000, 40)])
+    seqs = []
+    for i, n in enumerate(lens):
+        where = ["left", "right", "mid"][i % 3]
+        seqs.append(_telo_read(rng, n, where=where, tract=(100, min(n, 2500)), sub=0.02 if i % 2 else 0.05,
+                               lower=0.01 if i % 7 == 0 else 0.0))
+    return seqs
+
+
+@pytest.mark.parametrize("cfg", [dict(patterns="TTAGGG"), dict(patterns="TTAGGG TCAGGG", tvr_patterns="TGAGGG TTGGGG")],
+                         ids=["p2", "p3"])
+def test_packed_bundle_groups(cfg):
+    seqs = _packed_reads(11)
+    nt = _nt(**cfg)
+    assert nt.tscan
+    plan = nt.bundle_plan(np.array([len(x) for x in seqs], np.uint32))
+    assert (plan.bnd_block[:-1] % 64 != 0).sum() >= 8, "expected packed groups"
+    res = nt.analyze(seqs, want_windows=True, want_hits=False)
+    compare(nt, res, oracle_rows(seqs, cfg["patterns"], tvr=cfg.get("tvr_patterns")), check_hits=False)
+
+
 def _random_reads(cfg, jit, check_tscan=True):
     rng = np.random.default_rng(zlib.crc32(str(sorted(cfg.items())).encode()))
     seqs = []
@@ -442,9 +471,9 @@ def _device_bundles(nt, t, n, read_len):
     from nanotel_amd.api import DeviceBundles
     plan = nt.bundle_plan(np.full(n, read_len, np.uint32))
     d = dict(bnd_read=torch.from_numpy(plan.bnd_read.view(np.int32)).cuda(),
-             bnd_stripe=torch.from_numpy(plan.bnd_stripe.view(np.int64)).cuda(),
+             bnd_block=torch.from_numpy(plan.bnd_block.view(np.int64)).cuda(),
              tplanes=torch.empty(max(1, plan.tplane_bytes // 4), dtype=torch.int32, device="cuda"))
-    b = DeviceBundles(d["tplanes"].data_ptr(), d["bnd_read"].data_ptr(), d["bnd_stripe"].data_ptr(),
+    b = DeviceBundles(d["tplanes"].data_ptr(), d["bnd_read"].data_ptr(), d["bnd_block"].data_ptr(),
                       plan.n_bundles, 0, 0, plan.tplane_bytes)
     nt.bundle_layout_device(t["planes"].data_ptr(), t["blk_off"].data_ptr(), t["lens"].data_ptr(),
                             t["win_off"].data_ptr(), n, n * t["rows"], b)
@@ -588,7 +617,7 @@ def test_host_tlayout_matches_device_mixed_lengths():
     dln = torch.from_numpy(ln.view(np.int32)).cuda()
     dwo = torch.from_numpy(wo.view(np.int64)).cuda()
     br = torch.from_numpy(plan.bnd_read.view(np.int32)).cuda()
-    bs = torch.from_numpy(plan.bnd_stripe.view(np.int64)).cuda()
+    bs = torch.from_numpy(plan.bnd_block.view(np.int64)).cuda()
     tp = torch.full((plan.tplane_bytes // 4,), -1, dtype=torch.int32, device="cuda")
     bb = DeviceBundles(tp.data_ptr(), br.data_ptr(), bs.data_ptr(), plan.n_bundles, 0, 0, plan.tplane_bytes)
     nt.bundle_layout_device(dp.data_ptr(), dblk.data_ptr(), dln.data_ptr(), dwo.data_ptr(), n, int(tw.value), bb)
@@ -604,10 +633,11 @@ def test_host_tlayout_matches_device_mixed_lengths():
 # the first and last reads (the last bundles: block offsets past 2^31,
 # T-layout words past 2^32) and reads spread over the whole batch; every row
 # field and every window count of every pass (NanoTel.R:717-766, 1080-1155).
-FULL_CONFIGS = {
-    "c3": ("YYAGGG", None, 10_000_000, 0.05, True),
-    "c4": ("TTAGGG TCAGGG", "TGAGGG TTGGGG", 10_000_000, 0.05, True),
-    "c5_shard": ("TTAGGG", None, 12_500_000, 0.0, False),
+FULL_CONFIGS = {  # patterns, TVRs, reads, variant rate, bundle path, read length
+    "c3": ("YYAGGG", None, 10_000_000, 0.05, True, 50_000),
+    "c4": ("TTAGGG TCAGGG", "TGAGGG TTGGGG", 10_000_000, 0.05, True, 50_000),
+    "c5_shard": ("TTAGGG", None, 12_500_000, 0.0, False, 50_000),
+    "c10k": ("TTAGGG", None, 1_000_000, 0.0, True, 10_000),  # packed bundle groups
 }
 
 
@@ -616,8 +646,7 @@ FULL_CONFIGS = {
 def test_full_size_config_sampled_vs_oracle(name):
     import torch
     from nanotel_amd import synth_params, synth_read_ascii
-    pats, tvr, n, var, bundle = FULL_CONFIGS[name]
-    read_len = 50_000
+    pats, tvr, n, var, bundle, read_len = FULL_CONFIGS[name]
     nt = _nt(patterns=pats, tvr_patterns=tvr)
     sp = synth_params(read_len=read_len, first_read=0, variant_rate=var)
     t = _device_batch(nt, sp, n, read_len, hits=False)
@@ -671,7 +700,7 @@ def test_offsets_beyond_32_bits(path):
     # and their T-layout word offsets pass 2^32.  Reproduced without
     # allocating them: the planes / window-count / T-layout base pointers are
     # shifted down by exactly the offsets added to blk_off / win_off /
-    # bnd_stripe.  Bundle path: the bundle scan reads the shifted T-layout, the
+    # bnd_block.  Bundle path: the bundle scan reads the shifted T-layout, the
     # calling kernel the shifted planes.
     import torch
     from nanotel_amd import synth_params
@@ -691,7 +720,7 @@ def test_offsets_beyond_32_bits(path):
         b, keep = _device_bundles(nt, t, n, read_len)
         stripe_bytes = 50 * 64 * 16
         soff = (1 << 35) // stripe_bytes + 1  # stripes: T-layout offsets past 2^35 bytes (2^33 words)
-        bs = keep["bnd_stripe"] + soff
+        bs = keep["bnd_block"] + 64 * soff  # (block columns, 64 a stripe)
         bundles = DeviceBundles(b.tplanes - soff * stripe_bytes, b.bnd_read, bs.data_ptr(), b.n_bundles, 0, 0,
                                 b.tplane_bytes)
         keep["bs_shift"] = bs
