@@ -407,6 +407,9 @@ struct TPipe {
 #ifndef NT_TS_NTSTORE  // non-temporal window-count stores (experiments)
 #define NT_TS_NTSTORE 1
 #endif
+#ifndef NT_TS_PK_NTSTORE  // packed groups: non-temporal count stores (experiments)
+#define NT_TS_PK_NTSTORE 0
+#endif
 #ifndef NT_TS_XPRIME
 #define NT_TS_XPRIME 0
 #endif
@@ -970,17 +973,21 @@ __device__ __forceinline__ void tscan_bundles(const NtBatch& B, const NtOut& O, 
             }
           }
         } else {
-          // window counts, per 16 windows: lane 2 s + h = pieces 2 h, 2 h + 1 of slot s
+          // window counts, per 16 windows: lane 4 s' + q = piece q of slot 16 j + s'
+          // (a slot's pieces of one bundle are 64 contiguous bytes); through L2,
+          // which merges a line's pieces (NT_TS_PK_NTSTORE: non-temporal)
+          const int q = lane & 3;
+          const int i = q == 0 ? pi[0] : q == 1 ? pi[1] : q == 2 ? pi[2] : pi[3];
+          const int w0 = q == 0 ? pw[0] : q == 1 ? pw[1] : q == 2 ? pw[2] : pw[3];
 #pragma unroll
           for (int j = 0; j < 2; ++j) {
-            const int s = lane >> 1, h = lane & 1, q = 2 * h + j;
-            const int i = h ? pi[2 + j] : pi[j], w0 = h ? pw[2 + j] : pw[j];
+            const int s = 16 * j + (lane >> 2);
             const uint4 m = meta[i * NT_BUNDLE + s];
             if (w0 < (int)m.x && !NT_TS_DBG_NOCNT) {
               const uint4 x = *reinterpret_cast<const uint4*>(ctp + s * 32 + 4 * q);
               uint8_t* w = reinterpret_cast<uint8_t*>(O.win_counts) + u64of(m.y, m.z) * kNP +
                            (uint64_t)p * NT_WIN_ROWS((uint64_t)m.x) + w0;
-#if NT_TS_NTSTORE
+#if NT_TS_PK_NTSTORE
               typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
               const u32x4 vv = {x.x, x.y, x.z, x.w};
               __builtin_nontemporal_store(vv, reinterpret_cast<u32x4*>(w));

@@ -200,16 +200,31 @@ static void test_packer_and_tlayout(std::mt19937_64& g) {
     std::stable_sort(in.begin(), in.end(), [&](uint32_t a, uint32_t b) { return lens[a] > lens[b]; });
     const uint64_t L = 37, T = (L + 1) / 2, nb = (in.size() + 31) / 32;
     std::vector<uint32_t> bread(nb * 32, 0xFFFFFFFFu);
-    std::vector<uint64_t> bstripe(nb + 1);
-    uint64_t gs = 0;
-    for (uint64_t b = 0; b < nb; ++b) {
-      bstripe[b] = gs;
+    // block columns: bundles in pairs packed at 16-column offsets when the
+    // pair fits 8 stripes, else alone over whole stripes (nt_common.h)
+    std::vector<uint64_t> bblock(nb + 1);
+    uint64_t col = 0;
+    auto nblk = [&](uint64_t b) { return (lens[in[b * 32]] + L - 1) / L; };
+    for (uint64_t b = 0; b < nb; ++b)
       for (uint64_t s = 0; s < 32 && b * 32 + s < in.size(); ++s) bread[b * 32 + s] = in[b * 32 + s];
-      gs += ((lens[in[b * 32]] + L - 1) / L + 63) / 64;
+    for (uint64_t b = 0; b < nb;) {
+      const uint64_t w0 = (nblk(b) + 15) / 16 * 16;
+      if (b + 1 < nb && w0 + (nblk(b + 1) + 15) / 16 * 16 <= 512) {
+        bblock[b] = col;
+        bblock[b + 1] = col + w0;
+        col += w0 + (nblk(b + 1) + 15) / 16 * 16;
+        b += 2;
+      } else {
+        bblock[b] = col;
+        col += (nblk(b) + 63) / 64 * 64;
+        b += 1;
+      }
+      col = (col + 63) / 64 * 64;
     }
-    bstripe[nb] = gs;
+    bblock[nb] = col;
+    const uint64_t gs = col / 64;
     std::vector<uint32_t> tp(gs * T * 64 * 4 + 4, 0xDEADBEEFu);
-    CHECK(nt_bundle_layout_host(planes.data(), blk.data(), len.data(), bread.data(), bstripe.data(), nb, (int)L,
+    CHECK(nt_bundle_layout_host(planes.data(), blk.data(), len.data(), bread.data(), bblock.data(), nb, (int)L,
                                 tp.data(), gs * T * 64 * 16) == 0);
     CHECK(tp[gs * T * 64 * 4] == 0xDEADBEEFu);  // nothing past the buffer
     for (uint64_t b = 0; b < nb; ++b)
@@ -218,7 +233,8 @@ static void test_packer_and_tlayout(std::mt19937_64& g) {
         if (r == 0xFFFFFFFFu) continue;
         for (uint64_t p = 0; p < lens[r]; p += 1 + g() % 7) {
           const uint64_t k = p / L, o = p % L;
-          const uint64_t idx = ((bstripe[b] + k / 64) * T + o / 2) * 64 + k % 64;
+          const uint64_t c = bblock[b] + k;  // the block's column
+          const uint64_t idx = ((c / 64) * T + o / 2) * 64 + c % 64;
           const int got = (int)((tp[4 * idx + 2 * (o & 1)] >> s) & 1u) | (int)(((tp[4 * idx + 2 * (o & 1) + 1] >> s) & 1u) << 1);
           CHECK(got == code2(seqs[r][p]));
         }
