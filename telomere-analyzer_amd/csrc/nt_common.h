@@ -122,6 +122,7 @@ struct NtBatch {
   const uint32_t* bnd_read;    // [n_bundles * NT_BUNDLE]
   const uint64_t* bnd_block;   // [n_bundles + 1] first column of each bundle
   uint64_t n_bundles;
+  uint64_t bnd_last;  // bnd_block[0 .. bnd_last] are valid (a range's groups may reach past its bundles)
 };
 
 struct NtOut {

@@ -424,6 +424,7 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
             batch->exc_off, batch->exc_pos, batch->exc_code, batch->n_reads,
             tscan ? batch->list : nullptr, tscan ? batch->n_list : 0,
             tscan ? batch->tplanes : nullptr, batch->bnd_read, batch->bnd_block, tscan ? batch->n_bundles : 0};
+  B.bnd_last = B.n_bundles;
   if (tscan && batch->n_list && !batch->list) return fail(ctx, NT_E_ARG, "n_list > 0 without a list");
   const uint64_t n_scan = tscan ? batch->n_list : batch->n_reads;  // reads of the per-read scan
   NtOut O{out->win_counts, out->start, out->end, out->density, out->flags, out->hits};
@@ -551,6 +552,7 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
       Bt.bnd_read += NT_BUNDLE * b0;
       Bt.bnd_block += b0;
       Bt.n_bundles = b1 - b0;
+      Bt.bnd_last = batch->n_bundles - b0;
       const uint64_t tgrid = std::max<uint64_t>(1, std::min<uint64_t>((Bt.n_bundles + 3) / 4, (uint64_t)ctx->cu_count * tbpc));
       const int pe = ev ? ctx->ev_nt[ctx->n_ev - 1] : 0;  // event pair of this launch
       if (ev) (void)hipEventRecord(ev[3 + 2 * pe], ctx->stream);
@@ -716,11 +718,13 @@ int nt_bundle_plan(nt_ctx* ctx, const uint32_t* len, const uint8_t* has_exc, uin
   // NT_TS_GROUP bundles at multiples of 16 columns within NT_TS_FLUSH(np)
   // stripes -- the count with the smallest idle fraction (ties: fewer)
   const uint64_t fmax = NT_TS_FLUSH(ctx->prog.n_pass);
+  const char* pk = std::getenv("NT_TS_PACK");  // 0: every bundle alone (experiments)
+  const uint64_t gmax = pk && pk[0] == '0' ? 1 : NT_TS_GROUP;
   uint64_t col = 0;
   for (uint64_t b = 0; b < nb;) {
     uint64_t best = 1, used = 0, w = 0;
     double best_idle = 2.0;
-    for (uint64_t n = 1; n <= NT_TS_GROUP && b + n <= nb; ++n) {
+    for (uint64_t n = 1; n <= gmax && b + n <= nb; ++n) {
       const uint64_t k = nblk(b + n - 1);
       used += k;
       w += (k + 15) / 16 * 16;

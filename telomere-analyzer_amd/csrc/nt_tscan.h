@@ -407,9 +407,6 @@ struct TPipe {
 #ifndef NT_TS_NTSTORE  // non-temporal window-count stores (experiments)
 #define NT_TS_NTSTORE 1
 #endif
-#ifndef NT_TS_PK_NTSTORE  // packed groups: non-temporal count stores (experiments)
-#define NT_TS_PK_NTSTORE 0
-#endif
 #ifndef NT_TS_XPRIME
 #define NT_TS_XPRIME 0
 #endif
@@ -729,18 +726,19 @@ constexpr int kTsMetaWords = NT_TS_GROUP * NT_BUNDLE * 4 + NT_BUNDLE * 4;
 // alone, per 16 windows in a packed group); and the telomeric bitmask words /
 // checkpoints of kF stripes, written out together (whole runs of a read's row
 // instead of 4-byte pieces: a partly written line costs a read-modify-write in
-// the memory system).  23.5 KB at most: one workgroup per CU (the scan runs at
+// the memory system).  24 KB at most: one workgroup per CU (the scan runs at
 // one wave per SIMD) leaves room for two of the calling kernel's beside it.
 template <int kNP>
 struct TsAux {
   static constexpr int kF = NT_TS_FLUSH(kNP);                 // stripes per flush (even)
   static constexpr int kCtWords = kNP * NT_BUNDLE * 32;       // [p][s][2 stripes x 16 words]
   static constexpr int kTmWords = kNP * NT_BUNDLE * kF * 2;   // [p][s][stripe] u64
-  static constexpr int kCkWords = kNP * NT_BUNDLE * 4 * kF;   // [p][s][4 stripe + g] u32
+  static constexpr int kCkStride = 4 * kF + 1;                // + a packed group's end (a bundle's total)
+  static constexpr int kCkWords = kNP * NT_BUNDLE * kCkStride;  // [p][s][4 stripe + g] u32
   static constexpr int kWords = kCtWords + kTmWords + kCkWords;
 };
-constexpr int kTsLdsWords = kTsMetaWords + 5376;
-static_assert(TsAux<2>::kWords <= 5376 && TsAux<3>::kWords <= 5376, "LDS");
+constexpr int kTsLdsWords = kTsMetaWords + 5472;
+static_assert(TsAux<2>::kWords <= 5472 && TsAux<3>::kWords <= 5472, "LDS");
 
 // 4x4 byte transpose inside every quad of lanes: lane i of the quad gets byte
 // i of the quad's four words (byte i' from lane i') -- two DPP exchanges
@@ -806,21 +804,16 @@ __device__ __forceinline__ void tscan_bundles(const NtBatch& B, const NtOut& O, 
     const uint64_t c0 = uniform_u64(B.bnd_block[b]);
     if (c0 & 63) continue;  // inside a packed group
     // ---- the group: bundles b .. b + G - 1 up to the next one that starts a group
+    // (the four next first columns in one round trip; the batch's last entry
+    // ends its last group, a range's groups may reach into the next range)
     TsGroup gr;
-    int G = 1;
-    uint64_t x1 = uniform_u64(B.bnd_block[b + 1]), x2 = 0, x3 = 0, xe = x1;
-    if (x1 & 63) {
-      G = 2;
-      x2 = xe = uniform_u64(B.bnd_block[b + 2]);
-      if (x2 & 63) {
-        G = 3;
-        x3 = xe = uniform_u64(B.bnd_block[b + 3]);
-        if (x3 & 63) {
-          G = 4;
-          xe = uniform_u64(B.bnd_block[b + 4]);
-        }
-      }
-    }
+    const uint64_t lb = B.bnd_last;
+    const uint64_t x1 = uniform_u64(B.bnd_block[b + 1]);
+    const uint64_t x2 = uniform_u64(B.bnd_block[b + 2 <= lb ? b + 2 : lb]);
+    const uint64_t x3 = uniform_u64(B.bnd_block[b + 3 <= lb ? b + 3 : lb]);
+    const uint64_t x4 = uniform_u64(B.bnd_block[b + 4 <= lb ? b + 4 : lb]);
+    const int G = !(x1 & 63) ? 1 : !(x2 & 63) ? 2 : !(x3 & 63) ? 3 : 4;
+    const uint64_t xe = G == 1 ? x1 : G == 2 ? x2 : G == 3 ? x3 : x4;
     gr.end = (int)(xe - c0);
     gr.s1 = G > 1 ? (int)(x1 - c0) : gr.end;
     gr.s2 = G > 2 ? (int)(x2 - c0) : gr.end;
@@ -924,7 +917,7 @@ __device__ __forceinline__ void tscan_bundles(const NtBatch& B, const NtOut& O, 
 #pragma unroll
       for (int p = 0; p < kNP; ++p) {
         uint32_t* ctp = ct + p * NT_BUNDLE * 32;  // this pass's rows
-        const int half = packed ? 0 : (st & 1) * 16;  // this stripe's 16 words of a row
+        const int half = (st & 1) * 16;  // this stripe's 16 words of a row
         uint32_t W[8];
 #pragma unroll
         for (int t = 0; t < 8; ++t) W[t] = acc[p][t];
@@ -949,50 +942,28 @@ __device__ __forceinline__ void tscan_bundles(const NtBatch& B, const NtOut& O, 
         }
         tmb[((p * NT_BUNDLE + ms) * Aux::kF + fs) * 2 + mh] = tbits;
         wave_sync();
-        if (!packed) {
-          // window counts (uint8: L <= 170), every second stripe: the rows' 128
-          // windows as whole lines, store c covers slots 8 c .. 8 c + 7, lane 8 i +
-          // q = the 16 bytes (windows 16 q ..) of slot 8 c + i
-          if ((st & 1) || st == nst - 1) {
+        // window counts (uint8: L <= 170), every second stripe: the rows' 128
+        // columns, store c covers slots 8 c .. 8 c + 7, lane 8 i + q = the 16
+        // bytes (columns 16 q ..) of slot 8 c + i, to the read of the column's
+        // bundle (a bundle alone: whole 128-byte lines; packed: runs of its
+        // pieces)
+        if ((st & 1) || st == nst - 1) {
+          const int q = lane & 7, x = (st >> 1) * 2 * kWave + 16 * q;
+          const int i = gr.bundle(x), w0 = x - gr.first(i);
 #pragma unroll
-            for (int c = 0; c < (NT_TS_DBG_HALFCNT ? 2 : 4); ++c) {  // (HALFCNT: timing only)
-              const int s = 8 * c + (lane >> 3), q = lane & 7, kq = (st >> 1) * 2 * kWave + 16 * q;
-              const uint4 m = meta[s];
-              const uint4 x = *reinterpret_cast<const uint4*>(ctp + s * 32 + 4 * q);
-              if (kq < (int)m.x && !NT_TS_DBG_NOCNT) {
-                uint8_t* w = reinterpret_cast<uint8_t*>(O.win_counts) + u64of(m.y, m.z) * kNP +
-                             (uint64_t)p * NT_WIN_ROWS((uint64_t)m.x) + kq;
-#if NT_TS_NTSTORE
-                typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-                const u32x4 vv = {x.x, x.y, x.z, x.w};
-                __builtin_nontemporal_store(vv, reinterpret_cast<u32x4*>(w));
-#else
-                *reinterpret_cast<uint4*>(w) = x;
-#endif
-              }
-            }
-          }
-        } else {
-          // window counts, per 16 windows: lane 4 s' + q = piece q of slot 16 j + s'
-          // (a slot's pieces of one bundle are 64 contiguous bytes); through L2,
-          // which merges a line's pieces (NT_TS_PK_NTSTORE: non-temporal)
-          const int q = lane & 3;
-          const int i = q == 0 ? pi[0] : q == 1 ? pi[1] : q == 2 ? pi[2] : pi[3];
-          const int w0 = q == 0 ? pw[0] : q == 1 ? pw[1] : q == 2 ? pw[2] : pw[3];
-#pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            const int s = 16 * j + (lane >> 2);
+          for (int c = 0; c < (NT_TS_DBG_HALFCNT ? 2 : 4); ++c) {  // (HALFCNT: timing only)
+            const int s = 8 * c + (lane >> 3);
             const uint4 m = meta[i * NT_BUNDLE + s];
-            if (w0 < (int)m.x && !NT_TS_DBG_NOCNT) {
-              const uint4 x = *reinterpret_cast<const uint4*>(ctp + s * 32 + 4 * q);
+            const uint4 v = *reinterpret_cast<const uint4*>(ctp + s * 32 + 4 * q);
+            if (w0 < (int)m.x && x < gr.end && !NT_TS_DBG_NOCNT) {
               uint8_t* w = reinterpret_cast<uint8_t*>(O.win_counts) + u64of(m.y, m.z) * kNP +
                            (uint64_t)p * NT_WIN_ROWS((uint64_t)m.x) + w0;
-#if NT_TS_PK_NTSTORE
+#if NT_TS_NTSTORE
               typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-              const u32x4 vv = {x.x, x.y, x.z, x.w};
+              const u32x4 vv = {v.x, v.y, v.z, v.w};
               __builtin_nontemporal_store(vv, reinterpret_cast<u32x4*>(w));
 #else
-              *reinterpret_cast<uint4*>(w) = x;
+              *reinterpret_cast<uint4*>(w) = v;
 #endif
             }
           }
@@ -1019,28 +990,32 @@ __device__ __forceinline__ void tscan_bundles(const NtBatch& B, const NtOut& O, 
         const uint32_t pre1 = pfirst[1] ? 0u : pre0 + g0;
         const uint32_t pre2 = pfirst[2] ? 0u : pre1 + g1;
         const uint32_t pre3 = pfirst[3] ? 0u : pre2 + g2;
-        uint32_t* ckr = ckb + (p * NT_BUNDLE + ms) * 4 * Aux::kF + 4 * fs + 2 * mh;
-        ckr[0] = mh ? pre2 : pre0;
-        ckr[1] = mh ? pre3 : pre1;
-        // the read's total when its windows end with its bundle's last column (no
-        // later piece of the bundle holds that checkpoint)
+        uint32_t* ckr = ckb + (p * NT_BUNDLE + ms) * Aux::kCkStride + 4 * fs + 2 * mh;
+        // (packed: a bundle's first checkpoint, 0, is not kept -- its entry holds
+        // the previous bundle's total, below)
+        if (!packed || !(mh ? pfirst[2] : pfirst[0])) ckr[0] = mh ? pre2 : pre0;
+        if (!packed || !(mh ? pfirst[3] : pfirst[1])) ckr[1] = mh ? pre3 : pre1;
+        wave_sync();  // every lane has read ct and runs, and written its checkpoints
+        if (mh == 0) runs[ms * 4 + p] = pre3 + g3;
+        // the read's total at its bundle's last column: a bundle alone writes it
+        // when its windows fill every column (no later piece holds that
+        // checkpoint); a packed group keeps every bundle's at the column after it
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-          const int q = 2 * mh + j;
           const bool last = mh ? plast[2 + j] : plast[j];
-          const int i = mh ? pi[2 + j] : pi[j], w0 = mh ? pw[2 + j] : pw[j];
           const uint32_t cum = (j ? (mh ? pre3 + g3 : pre1 + g1) : (mh ? pre2 + g2 : pre0 + g0));
-          (void)q;
           if (last && !NT_TS_DBG_NOAUX) {
-            const uint4 m = meta[i * NT_BUNDLE + ms];
-            const int nw = (int)m.x;
-            if (nw > 0 && w0 + 16 == nw)
-              reinterpret_cast<uint32_t*>(tmask + aux_base(u64of(m.y, m.z), m.w, kNP) +
-                                          (uint64_t)kNP * aux_nmw(nw))[p * aux_nck(nw) + (nw >> 4)] = cum;
+            if (packed) {
+              ckr[j + 1] = cum;  // the next piece's entry
+            } else {
+              const uint4 m = meta[ms];
+              const int nw = (int)m.x;
+              if (nw > 0 && (mh ? pw[2 + j] : pw[j]) + 16 == nw)
+                reinterpret_cast<uint32_t*>(tmask + aux_base(u64of(m.y, m.z), m.w, kNP) +
+                                            (uint64_t)kNP * aux_nmw(nw))[p * aux_nck(nw) + (nw >> 4)] = cum;
+            }
           }
         }
-        wave_sync();  // every lane has read ct and runs
-        if (mh == 0) runs[ms * 4 + p] = pre3 + g3;
       }
       if (!packed) {
         // ---- flush the bitmask words and checkpoints of stripes st0 .. st
@@ -1067,41 +1042,53 @@ __device__ __forceinline__ void tscan_bundles(const NtBatch& B, const NtOut& O, 
               const int nw = (int)m.x;
               if (g < 4 * (fs + 1) && nw > 0 && 16 * jj <= nw)
                 reinterpret_cast<uint32_t*>(tmask + aux_base(u64of(m.y, m.z), m.w, kNP) + (uint64_t)kNP * aux_nmw(nw))[
-                    p * aux_nck(nw) + jj] = ckb[(p * NT_BUNDLE + s) * 4 * Aux::kF + g];
+                    p * aux_nck(nw) + jj] = ckb[(p * NT_BUNDLE + s) * Aux::kCkStride + g];
             }
           }
           wave_sync();
         }
       } else if (st == nst - 1 && !NT_TS_DBG_NOAUX) {
-        // ---- a packed group's end: every (bundle, slot)'s bitmask words, each
-        // from the stripe bits of its 64 windows (two stripes when its first
-        // column is not a multiple of 64), and its checkpoints
+        // ---- a packed group's end: each read's aux block (its bitmask words,
+        // each from the stripe bits of its 64 windows -- two stripes when its
+        // bundle's first column is not a multiple of 64 -- then its checkpoints)
+        // written whole by a half wave, one read per half wave at a time
         wave_sync();
+        constexpr int kMaxT = (kNP * (2 * Aux::kF + 4 * Aux::kF + 1) + NT_BUNDLE - 1) / NT_BUNDLE;
+        for (int e2 = 0; e2 < G * NT_BUNDLE; e2 += 8) {
 #pragma unroll
-        for (int p = 0; p < kNP; ++p) {
-          for (int e = lane; e < G * NT_BUNDLE; e += kWave) {
-            const int i = e >> 5, s = e & (NT_BUNDLE - 1);
+          for (int u = 0; u < 4; ++u) {  // 4 reads per half wave in flight
+            const int e = e2 + 2 * u + mh, i = e >> 5, s = e & (NT_BUNDLE - 1);
             const uint4 m = meta[e];
             const int nw = (int)m.x;
-            if (nw == 0) continue;
-            const int si = gr.first(i), sn = gr.next(i), c = si & 63;
-            const uint64_t ab = aux_base(u64of(m.y, m.z), m.w, kNP);
+            const int si = gr.first(i), c = si & 63;
             const int nmw = aux_nmw(nw), nck = aux_nck(nw);
-            const uint32_t* tb = tmb + (p * NT_BUNDLE + s) * Aux::kF * 2;
-            for (int k = 0; k < nmw; ++k) {
-              const int f = (si >> 6) + k;
-              uint64_t wd = u64of(tb[2 * f], tb[2 * f + 1]);
-              if (c) {
-                const uint64_t hi = f + 1 < nst ? u64of(tb[2 * f + 2], tb[2 * f + 3]) : 0ull;
-                wd = (wd >> c) | (hi << (64 - c));
+            const int nwd = 2 * kNP * nmw, tot = nw > 0 ? nwd + kNP * nck : 0;
+            uint32_t* blk = reinterpret_cast<uint32_t*>(tmask + aux_base(u64of(m.y, m.z), m.w, kNP));
+#pragma unroll
+            for (int r = 0; r < kMaxT; ++r) {
+              const int t = ms + NT_BUNDLE * r;
+              if (t >= tot) break;
+              uint32_t v;
+              if (t < nwd) {  // u32 half of word k of pass p
+                const int p = (t >= 2 * nmw) + (kNP == 3 && t >= 4 * nmw);
+                const int t1 = t - 2 * nmw * p, k = t1 >> 1, f = (si >> 6) + k;
+                const uint32_t* tb = tmb + (p * NT_BUNDLE + s) * Aux::kF * 2;
+                uint64_t wd = u64of(tb[2 * f], tb[2 * f + 1]);
+                if (c) {
+                  const uint64_t hi = f + 1 < nst ? u64of(tb[2 * f + 2], tb[2 * f + 3]) : 0ull;
+                  wd = (wd >> c) | (hi << (64 - c));
+                }
+                const int rem = nw - 64 * k;
+                if (rem < 64) wd &= (1ull << rem) - 1ull;
+                v = (t1 & 1) ? (uint32_t)(wd >> 32) : (uint32_t)wd;
+              } else {  // checkpoint jj of pass p
+                const int t2 = t - nwd;
+                const int p = (t2 >= nck) + (kNP == 3 && t2 >= 2 * nck);
+                const int jj = t2 - nck * p;
+                v = jj == 0 ? 0u : ckb[(p * NT_BUNDLE + s) * Aux::kCkStride + (si >> 4) + jj];
               }
-              const int rem = nw - 64 * k;
-              if (rem < 64) wd &= (1ull << rem) - 1ull;
-              tmask[ab + (uint64_t)p * nmw + k] = wd;
+              blk[t] = v;
             }
-            uint32_t* ckr = reinterpret_cast<uint32_t*>(tmask + ab + (uint64_t)kNP * nmw) + p * nck;
-            const uint32_t* cks = ckb + (p * NT_BUNDLE + s) * 4 * Aux::kF;
-            for (int jj = 0; 16 * jj <= nw && si + 16 * jj < sn; ++jj) ckr[jj] = cks[(si >> 4) + jj];
           }
         }
         wave_sync();
