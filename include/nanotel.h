@@ -162,11 +162,9 @@ int nt_pack_reads(const char* const* seqs, const uint64_t* lens, uint64_t n_read
  * non-ACGT letters, which stay outside the bundles, as do reads of any
  * program the bundle scan does not cover (then *n_bundles = 0).  Outputs:
  * bnd_read [ceil(n/32)*32], bnd_block [ceil(n/32)+1] (each bundle's first
- * block column: a bundle starting at a multiple of 64 starts a group, and up
- * to 4 bundles of short reads are packed into one group at multiples of 16
- * columns when that leaves fewer idle columns; bnd_block[n_bundles] is a
- * multiple of 64), list [n] (the reads left out, in order), and the bytes of
- * the T-layout buffer (bnd_block[n_bundles] / 64 stripes). */
+ * block column, a multiple of 64: every bundle starts on a stripe), list [n]
+ * (the reads left out, in order), and the bytes of the T-layout buffer
+ * (bnd_block[n_bundles] / 64 stripes). */
 int nt_bundle_plan(nt_ctx* ctx, const uint32_t* len, const uint8_t* has_exc, uint64_t n_reads,
                    uint32_t* bnd_read, uint64_t* bnd_block, uint64_t* n_bundles, uint32_t* list,
                    uint64_t* n_list, uint64_t* tplane_bytes);

@@ -94,16 +94,11 @@ struct NtProgram {
 //   sequence of block COLUMNS, 64 to a STRIPE: stripe g holds T*64 16-byte
 //   words (T = ceil(L/2)), word t*64 + l = {lo, hi of position q, lo, hi of
 //   position q+1} of column 64 g + l, q = its block's start + 2t, bit s = slot s.
-//   Bundle b owns columns [bnd_block[b], bnd_block[b+1]) (its block k is
-//   column bnd_block[b] + k; columns past its last block hold zeros).  A
-//   bundle whose first column is a multiple of 64 starts a GROUP, scanned by
-//   one wave: either that bundle alone (its columns a whole number of
-//   stripes), or up to NT_TS_GROUP bundles packed at multiples of 16 columns
-//   into at most NT_TS_FLUSH(np) stripes (short reads: a 10 kb read is 100
-//   columns, 1.56 stripes alone, 7 stripes for 4 bundles packed).
+//   Bundle b owns columns [bnd_block[b], bnd_block[b+1]) -- its block k is
+//   column bnd_block[b] + k, the columns past its last block hold zeros -- and
+//   starts on a stripe (bnd_block[b] a multiple of 64; the column form leaves
+//   room for bundles that share stripes).
 #define NT_BUNDLE 32
-#define NT_TS_GROUP 4
-#define NT_TS_FLUSH(np) ((np) == 3 ? 4 : 8)
 
 struct NtBatch {
   const uint32_t* planes;   // uint2 blocks
@@ -122,7 +117,6 @@ struct NtBatch {
   const uint32_t* bnd_read;    // [n_bundles * NT_BUNDLE]
   const uint64_t* bnd_block;   // [n_bundles + 1] first column of each bundle
   uint64_t n_bundles;
-  uint64_t bnd_last;  // bnd_block[0 .. bnd_last] are valid (a range's groups may reach past its bundles)
 };
 
 struct NtOut {

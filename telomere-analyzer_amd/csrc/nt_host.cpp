@@ -424,7 +424,6 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
             batch->exc_off, batch->exc_pos, batch->exc_code, batch->n_reads,
             tscan ? batch->list : nullptr, tscan ? batch->n_list : 0,
             tscan ? batch->tplanes : nullptr, batch->bnd_read, batch->bnd_block, tscan ? batch->n_bundles : 0};
-  B.bnd_last = B.n_bundles;
   if (tscan && batch->n_list && !batch->list) return fail(ctx, NT_E_ARG, "n_list > 0 without a list");
   const uint64_t n_scan = tscan ? batch->n_list : batch->n_reads;  // reads of the per-read scan
   NtOut O{out->win_counts, out->start, out->end, out->density, out->flags, out->hits};
@@ -552,7 +551,6 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
       Bt.bnd_read += NT_BUNDLE * b0;
       Bt.bnd_block += b0;
       Bt.n_bundles = b1 - b0;
-      Bt.bnd_last = batch->n_bundles - b0;
       const uint64_t tgrid = std::max<uint64_t>(1, std::min<uint64_t>((Bt.n_bundles + 3) / 4, (uint64_t)ctx->cu_count * tbpc));
       const int pe = ev ? ctx->ev_nt[ctx->n_ev - 1] : 0;  // event pair of this launch
       if (ev) (void)hipEventRecord(ev[3 + 2 * pe], ctx->stream);
@@ -714,34 +712,10 @@ int nt_bundle_plan(nt_ctx* ctx, const uint32_t* len, const uint8_t* has_exc, uin
   const uint64_t nb = (in.size() + NT_BUNDLE - 1) / NT_BUNDLE;
   for (uint64_t i = 0; i < nb * NT_BUNDLE; ++i) bnd_read[i] = i < in.size() ? in[i] : 0xFFFFFFFFu;
   auto nblk = [&](uint64_t b) { return ((uint64_t)len[in[b * NT_BUNDLE]] + L - 1) / L; };  // slot 0: the longest
-  // groups (nt_common.h): a bundle alone over whole stripes, or up to
-  // NT_TS_GROUP bundles at multiples of 16 columns within NT_TS_FLUSH(np)
-  // stripes -- the count with the smallest idle fraction (ties: fewer)
-  const uint64_t fmax = NT_TS_FLUSH(ctx->prog.n_pass);
-  const char* pk = std::getenv("NT_TS_PACK");  // 0: every bundle alone (experiments)
-  const uint64_t gmax = pk && pk[0] == '0' ? 1 : NT_TS_GROUP;
-  uint64_t col = 0;
-  for (uint64_t b = 0; b < nb;) {
-    uint64_t best = 1, used = 0, w = 0;
-    double best_idle = 2.0;
-    for (uint64_t n = 1; n <= gmax && b + n <= nb; ++n) {
-      const uint64_t k = nblk(b + n - 1);
-      used += k;
-      w += (k + 15) / 16 * 16;
-      const uint64_t st = (w + 63) / 64;
-      if (n > 1 && st > fmax) break;
-      const double idle = (double)(st * 64 - used) / (double)(st * 64);
-      if (idle < best_idle - 1e-12) {
-        best_idle = idle;
-        best = n;
-      }
-    }
-    for (uint64_t i = 0; i < best; ++i) {
-      bnd_block[b + i] = col;
-      col += best == 1 ? (nblk(b) + 63) / 64 * 64 : (nblk(b + i) + 15) / 16 * 16;
-    }
-    col = (col + 63) / 64 * 64;
-    b += best;
+  uint64_t col = 0;  // each bundle over whole stripes
+  for (uint64_t b = 0; b < nb; ++b) {
+    bnd_block[b] = col;
+    col += (nblk(b) + 63) / 64 * 64;
   }
   bnd_block[nb] = col;
   *n_bundles = nb;

@@ -652,19 +652,13 @@ int nt_bundle_layout_host(const uint32_t* planes, const uint64_t* blk_off, const
   const uint64_t L = (uint64_t)subseq_length, T = (L + 1) / 2;
   if (bnd_block[n_bundles] % 64 || bnd_block[n_bundles] / 64 * T * 64 * 16 > tplane_bytes) return NT_E_ARG;
   for (uint64_t b = 0; b < n_bundles; ++b) {
-    if (bnd_block[b + 1] < bnd_block[b] || bnd_block[b] % 16) return NT_E_ARG;
+    if (bnd_block[b + 1] < bnd_block[b] || bnd_block[b] % 64) return NT_E_ARG;  // bundles start on stripes
     const uint32_t r0 = bnd_read[NT_BUNDLE * b];
     if (r0 != 0xFFFFFFFFu && (len[r0] + L - 1) / L > bnd_block[b + 1] - bnd_block[b]) return NT_E_ARG;
   }
-  // one task per group (its bundles share stripes)
-  std::vector<uint64_t> g0;
-  for (uint64_t b = 0; b < n_bundles; ++b)
-    if (bnd_block[b] % 64 == 0) g0.push_back(b);
-  g0.push_back(n_bundles);
-  parallel_for(g0.size() - 1, [&](uint64_t g) {
-    for (uint64_t b = g0[g]; b < g0[g + 1]; ++b)
-      tlayout_bundle(planes, blk_off, len, bnd_read + NT_BUNDLE * b, bnd_block[b], bnd_block[b + 1], (uint32_t)L,
-                     tplanes);
+  parallel_for(n_bundles, [&](uint64_t b) {
+    tlayout_bundle(planes, blk_off, len, bnd_read + NT_BUNDLE * b, bnd_block[b], bnd_block[b + 1], (uint32_t)L,
+                   tplanes);
   });
   return NT_OK;
 }

@@ -713,32 +713,39 @@ __device__ __forceinline__ void transpose8(uint32_t (&a)[8]) {
   }
 }
 
-// Per-wave LDS of the bundle scan (uint32 words): the group's slot metadata,
-// bundle i's slot s at meta[i * 32 + s] = {nw, win_off lo, win_off hi, read}
-// (one ds_read_b128; written once per group), and runs[s * 4 + p], the covered
-// bases of slot s's read before the current stripe in pass p (for the bundle
-// whose columns reach the stripe's end).
-constexpr int kTsMetaWords = NT_TS_GROUP * NT_BUNDLE * 4 + NT_BUNDLE * 4;
+// Per-slot metadata of the bundle being scanned (per-wave LDS, written once
+// per bundle): not held in registers across the walk.  {nw, wb} first: one
+// ds_read_b128 gives a slot's count row.
+struct TSlot {
+  uint32_t nw;            // windows (0: empty slot)
+  uint32_t wb_lo, wb_hi;  // index of pass 0's window counts (win_off * np)
+  uint32_t len;
+  uint32_t ab_lo, ab_hi;  // aux_base(win_off, r, np): telomeric bitmasks, then checkpoints
+  uint32_t r, occ;
+  uint32_t run[3];        // covered bases of the windows before this stripe, per pass
+  uint32_t pad;
+};
+constexpr int kTsSlotWords = 12;
 
-// Then the count rows of two stripes per pass (row s = slot s, 32 words = 128
-// windows, 4 to a word: byte b = window 4 q + b of word q -- the uint8 counts,
-// stored as whole 128-byte lines every second stripe by a bundle scanned
-// alone, per 16 windows in a packed group); and the telomeric bitmask words /
-// checkpoints of kF stripes, written out together (whole runs of a read's row
-// instead of 4-byte pieces: a partly written line costs a read-modify-write in
-// the memory system).  24 KB at most: one workgroup per CU (the scan runs at
-// one wave per SIMD) leaves room for two of the calling kernel's beside it.
+// per-wave LDS of the bundle scan (uint32 words): the slots; the count rows
+// of two stripes per pass (row s = slot s, 32 words = 128 windows, 4 to a
+// word: byte b = window 4 q + b of word q -- the uint8 counts, stored as
+// whole 128-byte lines every second stripe); and the telomeric bitmask words
+// / checkpoints of kF stripes, written out together (whole runs of a read's
+// row instead of 4-byte pieces: a partly written line costs a
+// read-modify-write in the memory system).  22.5 KB at most: one workgroup
+// per CU (the scan runs at one wave per SIMD) leaves room for two of the
+// calling kernel's beside it.
 template <int kNP>
 struct TsAux {
-  static constexpr int kF = NT_TS_FLUSH(kNP);                 // stripes per flush (even)
+  static constexpr int kF = kNP == 3 ? 4 : 8;                 // stripes per flush (even)
   static constexpr int kCtWords = kNP * NT_BUNDLE * 32;       // [p][s][2 stripes x 16 words]
   static constexpr int kTmWords = kNP * NT_BUNDLE * kF * 2;   // [p][s][stripe] u64
-  static constexpr int kCkStride = 4 * kF + 1;                // + a packed group's end (a bundle's total)
-  static constexpr int kCkWords = kNP * NT_BUNDLE * kCkStride;  // [p][s][4 stripe + g] u32
+  static constexpr int kCkWords = kNP * NT_BUNDLE * 4 * kF;   // [p][s][4 stripe + g] u32
   static constexpr int kWords = kCtWords + kTmWords + kCkWords;
 };
-constexpr int kTsLdsWords = kTsMetaWords + 5472;
-static_assert(TsAux<2>::kWords <= 5472 && TsAux<3>::kWords <= 5472, "LDS");
+constexpr int kTsLdsWords = NT_BUNDLE * kTsSlotWords + 5376;
+static_assert(TsAux<2>::kWords <= 5376 && TsAux<3>::kWords <= 5376, "LDS");
 
 // 4x4 byte transpose inside every quad of lanes: lane i of the quad gets byte
 // i of the quad's four words (byte i' from lane i') -- two DPP exchanges
@@ -751,34 +758,17 @@ __device__ __forceinline__ uint32_t quad_byte_transpose(uint32_t x, uint32_t sel
 
 __device__ __forceinline__ uint64_t u64of(uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32) | lo; }
 
-// A group's columns: the bundle i of relative column x (first columns 0, s1,
-// s2, s3 -- the group's end for absent bundles), its block w, and whether the
-// block holds positions of the bundle's longest read (nb[i] blocks).
-// (Scalar fields, no arrays: a select over an array member became a scratch
-// array indexed at run time.)
-struct TsGroup {
-  int s1, s2, s3, end;
-  int nb0, nb1, nb2, nb3;
-  __device__ __forceinline__ int bundle(int x) const { return (x >= s1) + (x >= s2) + (x >= s3); }
-  __device__ __forceinline__ int first(int i) const { return i == 0 ? 0 : i == 1 ? s1 : i == 2 ? s2 : s3; }
-  __device__ __forceinline__ int next(int i) const { return i == 0 ? s1 : i == 1 ? s2 : i == 2 ? s3 : end; }
-  __device__ __forceinline__ int blocks(int i) const { return i == 0 ? nb0 : i == 1 ? nb1 : i == 2 ? nb2 : nb3; }
-};
-
-// The bundle scan: every group of the batch (nt_common.h), one wave per group
-// (claimed from 8 per-XCD queues over the bundles; a claimed bundle that does
-// not start a group is skipped -- its group's first bundle brings it).
+// The bundle scan: every bundle of the batch, one wave per bundle (claimed
+// from 8 per-XCD queues).
 template <class TP, class Pats, class Tvrs>
 __device__ __forceinline__ void tscan_bundles(const NtBatch& B, const NtOut& O, uint64_t* __restrict__ tmask,
                                               unsigned long long* __restrict__ queue,
                                               uint32_t thr_full, uint32_t* wlds) {
   constexpr int kL = TP::kL, kNP = TP::kNP, kT = TP::kT;
   static_assert(kL <= 170, "8-bit counts (nt_tscan_eligible)");
-  static_assert(NT_TS_GROUP == 4, "group discovery below");
   const int lane = threadIdx.x & (kWave - 1);
-  uint4* meta = reinterpret_cast<uint4*>(wlds);
-  uint32_t* runs = wlds + NT_TS_GROUP * NT_BUNDLE * 4;
-  uint32_t* ct = wlds + kTsMetaWords;  // the count rows
+  TSlot* sl = reinterpret_cast<TSlot*>(wlds);
+  uint32_t* ct = wlds + NT_BUNDLE * kTsSlotWords;  // the count rows
   using Aux = TsAux<kNP>;
   uint32_t* tmb = ct + Aux::kCtWords;  // bitmask words of the flush
   uint32_t* ckb = tmb + Aux::kTmWords;  // checkpoints of the flush
@@ -801,123 +791,91 @@ __device__ __forceinline__ void tscan_bundles(const NtBatch& B, const NtOut& O, 
     return nb;
   };
   for (uint64_t b = claim(); b < nb; b = claim()) {
-    const uint64_t c0 = uniform_u64(B.bnd_block[b]);
-    if (c0 & 63) continue;  // inside a packed group
-    // ---- the group: bundles b .. b + G - 1 up to the next one that starts a group
-    // (the four next first columns in one round trip; the batch's last entry
-    // ends its last group, a range's groups may reach into the next range)
-    TsGroup gr;
-    const uint64_t lb = B.bnd_last;
-    const uint64_t x1 = uniform_u64(B.bnd_block[b + 1]);
-    const uint64_t x2 = uniform_u64(B.bnd_block[b + 2 <= lb ? b + 2 : lb]);
-    const uint64_t x3 = uniform_u64(B.bnd_block[b + 3 <= lb ? b + 3 : lb]);
-    const uint64_t x4 = uniform_u64(B.bnd_block[b + 4 <= lb ? b + 4 : lb]);
-    const int G = !(x1 & 63) ? 1 : !(x2 & 63) ? 2 : !(x3 & 63) ? 3 : 4;
-    const uint64_t xe = G == 1 ? x1 : G == 2 ? x2 : G == 3 ? x3 : x4;
-    gr.end = (int)(xe - c0);
-    gr.s1 = G > 1 ? (int)(x1 - c0) : gr.end;
-    gr.s2 = G > 2 ? (int)(x2 - c0) : gr.end;
-    gr.s3 = G > 3 ? (int)(x3 - c0) : gr.end;
-    const bool packed = G > 1;
-    const int nst = gr.end >> 6;
-    // ---- slot metadata into LDS: lane 32 h + s = bundle 2 k + h, slot s
+    // ---- slot metadata into LDS (lanes 0..31 = slots)
+    uint32_t occ, n_max;
     {
-      uint32_t len0[NT_TS_GROUP / 2];
-#pragma unroll
-      for (int k = 0; k < NT_TS_GROUP / 2; ++k) {
-        const int i = 2 * k + mh;
-        const uint32_t r = i < G ? B.bnd_read[(b + i) * NT_BUNDLE + ms] : 0xFFFFFFFFu;
-        const bool o = r != 0xFFFFFFFFu;
-        const uint32_t len = o ? B.len[r] : 0u;
-        const uint64_t wo = o ? B.win_off[r] : 0ull;
-        meta[i * NT_BUNDLE + ms] =
-            make_uint4(o ? (uint32_t)split_window_count(len, kL) : 0u, (uint32_t)wo, (uint32_t)(wo >> 32), r);
-        len0[k] = len;
+      const uint32_t r = B.bnd_read[b * NT_BUNDLE + (lane & 31)];
+      const bool o = r != 0xFFFFFFFFu;
+      const uint32_t len = o ? B.len[r] : 0u;
+      const uint64_t wo = o ? B.win_off[r] : 0ull;
+      if (lane < NT_BUNDLE) {
+        TSlot t;
+        t.len = len;
+        t.nw = o ? (uint32_t)split_window_count(len, kL) : 0u;
+        t.r = r;
+        t.occ = o ? 1u : 0u;
+        const uint64_t wb = wo * kNP, ab = aux_base(wo, r, kNP);
+        t.wb_lo = (uint32_t)wb;
+        t.wb_hi = (uint32_t)(wb >> 32);
+        t.ab_lo = (uint32_t)ab;
+        t.ab_hi = (uint32_t)(ab >> 32);
+        t.run[0] = t.run[1] = t.run[2] = 0u;
+        t.pad = 0u;
+        sl[lane] = t;
       }
-      // slot 0 holds the longest read
-      gr.nb0 = ((int)__builtin_amdgcn_readlane((int)len0[0], 0) + kL - 1) / kL;
-      gr.nb1 = ((int)__builtin_amdgcn_readlane((int)len0[0], 32) + kL - 1) / kL;
-      gr.nb2 = ((int)__builtin_amdgcn_readlane((int)len0[1], 0) + kL - 1) / kL;
-      gr.nb3 = ((int)__builtin_amdgcn_readlane((int)len0[1], 32) + kL - 1) / kL;
-      if (lane < NT_BUNDLE) *reinterpret_cast<uint4*>(runs + 4 * lane) = make_uint4(0u, 0u, 0u, 0u);
+      occ = (uint32_t)__ballot(o && lane < NT_BUNDLE);
+      n_max = (uint32_t)__builtin_amdgcn_readfirstlane((int)len);  // slot 0 = the longest
     }
+    const int nblk = ((int)n_max + kL - 1) / kL;
+    const int nst = (nblk + kWave - 1) / kWave;
+    const uint64_t g0 = uniform_u64(B.bnd_block[b]) >> 6, g1 = uniform_u64(B.bnd_block[b + 1]) >> 6;  // its stripes
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint32_t*>(B.tplanes) + (c0 >> 6) * (uint64_t)kT * kWave * 4, (short)0,
-        (int)((uint64_t)nst * kT * kWave * 16), 0x00020000);
+        const_cast<uint32_t*>(B.tplanes) + g0 * (uint64_t)kT * kWave * 4, (short)0,
+        (int)((g1 - g0) * (uint64_t)kT * kWave * 16), 0x00020000);
     wave_sync();
-    // this lane's column in the current stripe: bundle, block, holds a block
-    int li = gr.bundle(lane), lw = lane - gr.first(li);
-    bool la = lw < gr.blocks(li);
 #if NT_TS_HALO
     TWalkerH<TP, Pats, Tvrs> wk;
     wk.rs = rs;
-    wk.set_stripe(0, lane, la, nst);
+    wk.set_stripe(0, lane, lane < nblk, nst);
 #else
     TWalker<TP, Pats, Tvrs> wk;
     wk.rs = rs;
-    wk.set_stripe(0, lane, la);
+    wk.set_stripe(0, lane, lane < nblk);
     if (NT_TS_XPRIME) wk.prime();
 #endif
     for (int st = 0; st < nst; ++st) {
+      const int k = st * kWave + lane;  // this lane's block = window
       if (!NT_TS_XPRIME || NT_TS_HALO) wk.prime();
       uint32_t acc[3][8];
 #if NT_TS_DBG_NOWALK  // timing experiments only: results are wrong
 #pragma unroll
       for (int p = 0; p < 3; ++p)
 #pragma unroll
-        for (int b2 = 0; b2 < 8; ++b2) acc[p][b2] = (uint32_t)((st * kWave + lane) * 0x9E3779B9u) >> (p + b2);
+        for (int b = 0; b < 8; ++b) acc[p][b] = (uint32_t)(k * 0x9E3779B9u) >> (p + b);
 #else
-      wk.walk(lw == 0, acc);  // a bundle's first block: nothing before it (out-of-bound starts)
+      wk.walk(k == 0, acc);
 #endif
-      {  // the next stripe's columns (lanes past the group's blocks load nothing)
-        const int x = (st + 1) * kWave + lane;
-        li = gr.bundle(x);
-        lw = x - gr.first(li);
-        la = lw < gr.blocks(li);
 #if NT_TS_HALO
-        wk.set_stripe(st + 1, lane, la, nst);
+      wk.set_stripe(st + 1, lane, k + kWave < nblk, nst);  // lanes past the bundle's last block load nothing
 #else
-        wk.set_stripe(st + 1, lane, la);
+      wk.set_stripe(st + 1, lane, k + kWave < nblk);  // lanes past the bundle's last block load nothing
 #endif
-      }
 #if NT_TS_DBG_NOOUT  // timing experiments only: results are wrong
       {
         uint32_t x = 0;
 #pragma unroll
         for (int p = 0; p < 3; ++p)
 #pragma unroll
-          for (int b2 = 0; b2 < 8; ++b2) x ^= acc[p][b2] * (b2 + 1);
+          for (int b = 0; b < 8; ++b) x ^= acc[p][b] * (b + 1);
         if (x == 0x1234567u) O.flags[0] = 1;
         continue;
       }
 #endif
-      // ---- outputs.  Lane k holds the counts of column k of the stripe for
+      // ---- outputs.  Lane k holds the counts of window k of the stripe for
       // the 32 slots, bit-sliced.  A byte transpose (in registers, then LDS)
-      // gives row s = slot s's 64 counts, and at lane 32 h + s (columns 32 h ..)
-      // the checkpoint sums; the telomeric bits come from a bit-sliced compare
-      // and a bit transpose.  Bitmask words and checkpoints wait in LDS for the
-      // flush.  A bundle alone: the rows go out as whole 128-byte lines every
-      // second stripe.  A packed group: each 16-column piece of a row to its
-      // bundle's read, the bitmask words (a bundle's 64-window words start at
-      // its first column, a multiple of 16) composed at the group's end.
-      const int fs = packed ? st : st % Aux::kF;  // the stripe's place in the flush buffers
-      const int k0 = st * kWave;                  // the stripe's first column
-      // the 16-column pieces q of the stripe (uniform): bundle, first block, first
-      // piece of the bundle, last piece of the bundle
-      int pi[4], pw[4];
-      bool pfirst[4], plast[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int x = k0 + 16 * q;
-        pi[q] = gr.bundle(x);
-        pw[q] = x - gr.first(pi[q]);
-        pfirst[q] = pw[q] == 0;
-        plast[q] = x + 16 == gr.next(pi[q]);
-      }
+      // gives row s = slot s's 64 counts: out as whole 128-byte lines (8 lanes
+      // per slot), and at lane 32 h + s (windows 32 h ..) for the checkpoint
+      // sums; the telomeric bits come from a bit-sliced compare and a bit
+      // transpose.  Bitmask words and checkpoints wait in LDS for the flush.
+      const TSlot& mt = sl[ms];
+      const int m_nw = (int)mt.nw;
+      const int k0 = st * kWave + 32 * mh;  // this lane's first window
+      const int nv = m_nw - k0 < 0 ? 0 : (m_nw - k0 > 32 ? 32 : m_nw - k0);  // its windows in the read
+      const int fs = st % Aux::kF;          // the stripe's place in the flush buffers
 #pragma unroll
       for (int p = 0; p < kNP; ++p) {
         uint32_t* ctp = ct + p * NT_BUNDLE * 32;  // this pass's rows
-        const int half = (st & 1) * 16;  // this stripe's 16 words of a row
+        const int half = (st & 1) * 16;            // this stripe's 16 words of a row
         uint32_t W[8];
 #pragma unroll
         for (int t = 0; t < 8; ++t) W[t] = acc[p][t];
@@ -935,41 +893,32 @@ __device__ __forceinline__ void tscan_bundles(const NtBatch& B, const NtOut& O, 
         for (int j = 0; j < 8; ++j) W[j] = quad_byte_transpose(W[j], sel2, sel1);
 #pragma unroll
         for (int j = 0; j < 8; ++j) ctp[(8 * (lane & 3) + j) * 32 + half + (lane >> 2)] = W[j];
-        uint32_t tbits = half_bit_transpose(ge, lane);
-        if (!packed) {  // a bundle alone: slot ms's windows in the read only
-          const int nv = (int)meta[ms].x - (st * kWave + 32 * mh);
-          tbits &= nv >= 32 ? ~0u : (nv <= 0 ? 0u : ((1u << nv) - 1u));
-        }
-        tmb[((p * NT_BUNDLE + ms) * Aux::kF + fs) * 2 + mh] = tbits;
+        const uint32_t tb = half_bit_transpose(ge, lane) & (nv >= 32 ? ~0u : ((1u << nv) - 1u));
+        tmb[((p * NT_BUNDLE + ms) * Aux::kF + fs) * 2 + mh] = tb;
         wave_sync();
         // window counts (uint8: L <= 170), every second stripe: the rows' 128
-        // columns, store c covers slots 8 c .. 8 c + 7, lane 8 i + q = the 16
-        // bytes (columns 16 q ..) of slot 8 c + i, to the read of the column's
-        // bundle (a bundle alone: whole 128-byte lines; packed: runs of its
-        // pieces)
+        // windows as whole lines, store c covers slots 8 c .. 8 c + 7, lane 8 i +
+        // q = the 16 bytes (windows 16 q ..) of slot 8 c + i
         if ((st & 1) || st == nst - 1) {
-          const int q = lane & 7, x = (st >> 1) * 2 * kWave + 16 * q;
-          const int i = gr.bundle(x), w0 = x - gr.first(i);
 #pragma unroll
           for (int c = 0; c < (NT_TS_DBG_HALFCNT ? 2 : 4); ++c) {  // (HALFCNT: timing only)
-            const int s = 8 * c + (lane >> 3);
-            const uint4 m = meta[i * NT_BUNDLE + s];
-            const uint4 v = *reinterpret_cast<const uint4*>(ctp + s * 32 + 4 * q);
-            if (w0 < (int)m.x && x < gr.end && !NT_TS_DBG_NOCNT) {
-              uint8_t* w = reinterpret_cast<uint8_t*>(O.win_counts) + u64of(m.y, m.z) * kNP +
-                           (uint64_t)p * NT_WIN_ROWS((uint64_t)m.x) + w0;
+            const int s = 8 * c + (lane >> 3), q = lane & 7, kq = (st >> 1) * 2 * kWave + 16 * q;
+            const uint4 m = *reinterpret_cast<const uint4*>(sl + s);  // nw, wb_lo, wb_hi
+            const uint4 x = *reinterpret_cast<const uint4*>(ctp + s * 32 + 4 * q);
+            if (kq < (int)m.x && !NT_TS_DBG_NOCNT) {
+              uint8_t* w = reinterpret_cast<uint8_t*>(O.win_counts) + u64of(m.y, m.z) +
+                           (uint64_t)p * NT_WIN_ROWS((uint64_t)m.x) + kq;
 #if NT_TS_NTSTORE
               typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-              const u32x4 vv = {v.x, v.y, v.z, v.w};
+              const u32x4 vv = {x.x, x.y, x.z, x.w};
               __builtin_nontemporal_store(vv, reinterpret_cast<u32x4*>(w));
 #else
-              *reinterpret_cast<uint4*>(w) = v;
+              *reinterpret_cast<uint4*>(w) = x;
 #endif
             }
           }
         }
-        // checkpoints: covered bases before every 16th window; lane 32 h + s
-        // sums pieces 2 h, 2 h + 1 of slot s's row
+        // checkpoints: covered bases before windows 16 jj, jj = 4 st + g
         const uint4 va = *reinterpret_cast<const uint4*>(ctp + ms * 32 + half + 8 * mh);
         const uint4 vb = *reinterpret_cast<const uint4*>(ctp + ms * 32 + half + 8 * mh + 4);
         uint32_t ga = 0u, gb = 0u;
@@ -981,114 +930,46 @@ __device__ __forceinline__ void tscan_bundles(const NtBatch& B, const NtOut& O, 
         gb = __builtin_amdgcn_udot4(vb.y, 0x01010101u, gb, false);
         gb = __builtin_amdgcn_udot4(vb.z, 0x01010101u, gb, false);
         gb = __builtin_amdgcn_udot4(vb.w, 0x01010101u, gb, false);
-        const uint32_t oa = (uint32_t)__shfl_xor((int)ga, 32, kWave);
-        const uint32_t ob = (uint32_t)__shfl_xor((int)gb, 32, kWave);
-        const uint32_t g0 = mh ? oa : ga, g1 = mh ? ob : gb, g2 = mh ? ga : oa, g3 = mh ? gb : ob;
-        const uint32_t run = runs[ms * 4 + p];
-        // before each piece: the bundle's running count, restarted at a bundle's first piece
-        const uint32_t pre0 = pfirst[0] ? 0u : run;
-        const uint32_t pre1 = pfirst[1] ? 0u : pre0 + g0;
-        const uint32_t pre2 = pfirst[2] ? 0u : pre1 + g1;
-        const uint32_t pre3 = pfirst[3] ? 0u : pre2 + g2;
-        uint32_t* ckr = ckb + (p * NT_BUNDLE + ms) * Aux::kCkStride + 4 * fs + 2 * mh;
-        // (packed: a bundle's first checkpoint, 0, is not kept -- its entry holds
-        // the previous bundle's total, below)
-        if (!packed || !(mh ? pfirst[2] : pfirst[0])) ckr[0] = mh ? pre2 : pre0;
-        if (!packed || !(mh ? pfirst[3] : pfirst[1])) ckr[1] = mh ? pre3 : pre1;
-        wave_sync();  // every lane has read ct and runs, and written its checkpoints
-        if (mh == 0) runs[ms * 4 + p] = pre3 + g3;
-        // the read's total at its bundle's last column: a bundle alone writes it
-        // when its windows fill every column (no later piece holds that
-        // checkpoint); a packed group keeps every bundle's at the column after it
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const bool last = mh ? plast[2 + j] : plast[j];
-          const uint32_t cum = (j ? (mh ? pre3 + g3 : pre1 + g1) : (mh ? pre2 + g2 : pre0 + g0));
-          if (last && !NT_TS_DBG_NOAUX) {
-            if (packed) {
-              ckr[j + 1] = cum;  // the next piece's entry
-            } else {
-              const uint4 m = meta[ms];
-              const int nw = (int)m.x;
-              if (nw > 0 && (mh ? pw[2 + j] : pw[j]) + 16 == nw)
-                reinterpret_cast<uint32_t*>(tmask + aux_base(u64of(m.y, m.z), m.w, kNP) +
-                                            (uint64_t)kNP * aux_nmw(nw))[p * aux_nck(nw) + (nw >> 4)] = cum;
-            }
-          }
-        }
+        const uint32_t mine = ga + gb;
+        const uint32_t other = (uint32_t)__shfl_xor((int)mine, 32, kWave);
+        const uint32_t run = mt.run[p];
+        const uint32_t c0 = run + (mh ? other : 0u);  // before window k0
+        uint32_t* ckr = ckb + (p * NT_BUNDLE + ms) * 4 * Aux::kF + 4 * fs + 2 * mh;
+        ckr[0] = c0;
+        ckr[1] = c0 + ga;
+        // the read's total when its windows end with the bundle's last stripe
+        // (no later stripe holds that checkpoint)
+        if (mh && st == nst - 1 && 16 * ((k0 >> 4) + 2) == m_nw && !NT_TS_DBG_NOAUX)
+          reinterpret_cast<uint32_t*>(tmask + u64of(mt.ab_lo, mt.ab_hi) + (uint64_t)kNP * aux_nmw(m_nw))[
+              p * aux_nck(m_nw) + (m_nw >> 4)] = c0 + mine;
+        wave_sync();  // every lane has read ct and run[p]
+        if (mh == 0) sl[ms].run[p] = run + mine + other;
       }
-      if (!packed) {
-        // ---- flush the bitmask words and checkpoints of stripes st0 .. st
-        if ((fs == Aux::kF - 1 || st == nst - 1) && !NT_TS_DBG_NOAUX) {
-          wave_sync();
-          const int st0 = st - fs;
-#pragma unroll
-          for (int p = 0; p < kNP; ++p) {
-            // bitmask words: lane -> (slot, stripe), kF consecutive u64 per slot
-#pragma unroll
-            for (int i = 0; i < NT_BUNDLE * Aux::kF / kWave; ++i) {
-              const int e = i * kWave + lane, s = e / Aux::kF, w = e % Aux::kF, sw = st0 + w;
-              const uint4 m = meta[s];
-              const int nw = (int)m.x;
-              if (w <= fs && sw * kWave < nw)
-                tmask[aux_base(u64of(m.y, m.z), m.w, kNP) + (uint64_t)p * aux_nmw(nw) + sw] =
-                    *reinterpret_cast<const uint64_t*>(tmb + ((p * NT_BUNDLE + s) * Aux::kF + w) * 2);
-            }
-            // checkpoints: lane -> (slot, jj), 4 kF consecutive u32 per slot
-#pragma unroll
-            for (int i = 0; i < NT_BUNDLE * 4 * Aux::kF / kWave; ++i) {
-              const int e = i * kWave + lane, s = e / (4 * Aux::kF), g = e % (4 * Aux::kF), jj = 4 * st0 + g;
-              const uint4 m = meta[s];
-              const int nw = (int)m.x;
-              if (g < 4 * (fs + 1) && nw > 0 && 16 * jj <= nw)
-                reinterpret_cast<uint32_t*>(tmask + aux_base(u64of(m.y, m.z), m.w, kNP) + (uint64_t)kNP * aux_nmw(nw))[
-                    p * aux_nck(nw) + jj] = ckb[(p * NT_BUNDLE + s) * Aux::kCkStride + g];
-            }
-          }
-          wave_sync();
-        }
-      } else if (st == nst - 1 && !NT_TS_DBG_NOAUX) {
-        // ---- a packed group's end: each read's aux block (its bitmask words,
-        // each from the stripe bits of its 64 windows -- two stripes when its
-        // bundle's first column is not a multiple of 64 -- then its checkpoints)
-        // written whole by a half wave, one read per half wave at a time
+      // ---- flush the bitmask words and checkpoints of stripes st0 .. st
+      if ((fs == Aux::kF - 1 || st == nst - 1) && !NT_TS_DBG_NOAUX) {
         wave_sync();
-        constexpr int kMaxT = (kNP * (2 * Aux::kF + 4 * Aux::kF + 1) + NT_BUNDLE - 1) / NT_BUNDLE;
-        for (int e2 = 0; e2 < G * NT_BUNDLE; e2 += 8) {
+        const int st0 = st - fs;
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {  // 4 reads per half wave in flight
-            const int e = e2 + 2 * u + mh, i = e >> 5, s = e & (NT_BUNDLE - 1);
-            const uint4 m = meta[e];
-            const int nw = (int)m.x;
-            const int si = gr.first(i), c = si & 63;
-            const int nmw = aux_nmw(nw), nck = aux_nck(nw);
-            const int nwd = 2 * kNP * nmw, tot = nw > 0 ? nwd + kNP * nck : 0;
-            uint32_t* blk = reinterpret_cast<uint32_t*>(tmask + aux_base(u64of(m.y, m.z), m.w, kNP));
+        for (int p = 0; p < kNP; ++p) {
+          // bitmask words: lane -> (slot, stripe), kF consecutive u64 per slot
 #pragma unroll
-            for (int r = 0; r < kMaxT; ++r) {
-              const int t = ms + NT_BUNDLE * r;
-              if (t >= tot) break;
-              uint32_t v;
-              if (t < nwd) {  // u32 half of word k of pass p
-                const int p = (t >= 2 * nmw) + (kNP == 3 && t >= 4 * nmw);
-                const int t1 = t - 2 * nmw * p, k = t1 >> 1, f = (si >> 6) + k;
-                const uint32_t* tb = tmb + (p * NT_BUNDLE + s) * Aux::kF * 2;
-                uint64_t wd = u64of(tb[2 * f], tb[2 * f + 1]);
-                if (c) {
-                  const uint64_t hi = f + 1 < nst ? u64of(tb[2 * f + 2], tb[2 * f + 3]) : 0ull;
-                  wd = (wd >> c) | (hi << (64 - c));
-                }
-                const int rem = nw - 64 * k;
-                if (rem < 64) wd &= (1ull << rem) - 1ull;
-                v = (t1 & 1) ? (uint32_t)(wd >> 32) : (uint32_t)wd;
-              } else {  // checkpoint jj of pass p
-                const int t2 = t - nwd;
-                const int p = (t2 >= nck) + (kNP == 3 && t2 >= 2 * nck);
-                const int jj = t2 - nck * p;
-                v = jj == 0 ? 0u : ckb[(p * NT_BUNDLE + s) * Aux::kCkStride + (si >> 4) + jj];
-              }
-              blk[t] = v;
-            }
+          for (int i = 0; i < NT_BUNDLE * Aux::kF / kWave; ++i) {
+            const int e = i * kWave + lane, s = e / Aux::kF, w = e % Aux::kF, sw = st0 + w;
+            const TSlot& t = sl[s];
+            const int nw = (int)t.nw;
+            if (w <= fs && sw * kWave < nw)
+              tmask[u64of(t.ab_lo, t.ab_hi) + (uint64_t)p * aux_nmw(nw) + sw] =
+                  *reinterpret_cast<const uint64_t*>(tmb + ((p * NT_BUNDLE + s) * Aux::kF + w) * 2);
+          }
+          // checkpoints: lane -> (slot, jj), 4 kF consecutive u32 per slot
+#pragma unroll
+          for (int i = 0; i < NT_BUNDLE * 4 * Aux::kF / kWave; ++i) {
+            const int e = i * kWave + lane, s = e / (4 * Aux::kF), g = e % (4 * Aux::kF), jj = 4 * st0 + g;
+            const TSlot& t = sl[s];
+            const int nw = (int)t.nw;
+            if (g < 4 * (fs + 1) && nw > 0 && 16 * jj <= nw)
+              reinterpret_cast<uint32_t*>(tmask + u64of(t.ab_lo, t.ab_hi) + (uint64_t)kNP * aux_nmw(nw))[
+                  p * aux_nck(nw) + jj] = ckb[(p * NT_BUNDLE + s) * 4 * Aux::kF + g];
           }
         }
         wave_sync();

@@ -200,26 +200,13 @@ static void test_packer_and_tlayout(std::mt19937_64& g) {
     std::stable_sort(in.begin(), in.end(), [&](uint32_t a, uint32_t b) { return lens[a] > lens[b]; });
     const uint64_t L = 37, T = (L + 1) / 2, nb = (in.size() + 31) / 32;
     std::vector<uint32_t> bread(nb * 32, 0xFFFFFFFFu);
-    // block columns: bundles in pairs packed at 16-column offsets when the
-    // pair fits 8 stripes, else alone over whole stripes (nt_common.h)
+    // block columns: each bundle over whole stripes
     std::vector<uint64_t> bblock(nb + 1);
     uint64_t col = 0;
-    auto nblk = [&](uint64_t b) { return (lens[in[b * 32]] + L - 1) / L; };
-    for (uint64_t b = 0; b < nb; ++b)
+    for (uint64_t b = 0; b < nb; ++b) {
       for (uint64_t s = 0; s < 32 && b * 32 + s < in.size(); ++s) bread[b * 32 + s] = in[b * 32 + s];
-    for (uint64_t b = 0; b < nb;) {
-      const uint64_t w0 = (nblk(b) + 15) / 16 * 16;
-      if (b + 1 < nb && w0 + (nblk(b + 1) + 15) / 16 * 16 <= 512) {
-        bblock[b] = col;
-        bblock[b + 1] = col + w0;
-        col += w0 + (nblk(b + 1) + 15) / 16 * 16;
-        b += 2;
-      } else {
-        bblock[b] = col;
-        col += (nblk(b) + 63) / 64 * 64;
-        b += 1;
-      }
-      col = (col + 63) / 64 * 64;
+      bblock[b] = col;
+      col += ((lens[in[b * 32]] + L - 1) / L + 63) / 64 * 64;
     }
     bblock[nb] = col;
     const uint64_t gs = col / 64;

@@ -275,12 +275,11 @@ def test_tvr_length_limit():
     assert e.value.name == "NT_E_LIMIT"
 
 
-# Packed bundle groups (nt_common.h): bundles of short reads share stripes at
-# 16-column offsets, their bitmask words are composed across stripes, their
-# checkpoints restart per bundle.  10 kb reads (4 bundles in 7 stripes), reads
-# whose windows fill every column of their bundle (3,200 and 3,160 bases: the
-# checkpoint at window nw lies past the bundle), ragged lengths, 700-base reads.
-def _packed_reads(seed):
+# Short and ragged reads on the bundle path: 10 kb reads (100 windows, a
+# bundle's second stripe part-filled), reads whose windows fill every block of
+# their bundle (3,200 and 3,160 bases: the checkpoint at window nw is the
+# read's total), ragged lengths, 700-base reads.
+def _short_ragged_reads(seed):
     rng = np.random.default_rng(seed)
     lens = ([10000] * 128 + [3200] * 64 + [3160] * 64 + [int(x) for x in rng.integers(1500, 4000, 96)] +
             [700] * 32 + [int(x) for x in rng.integers(5000, 12000, 40)])
@@ -294,12 +293,10 @@ def _packed_reads(seed):
 
 @pytest.mark.parametrize("cfg", [dict(patterns="TTAGGG"), dict(patterns="TTAGGG TCAGGG", tvr_patterns="TGAGGG TTGGGG")],
                          ids=["p2", "p3"])
-def test_packed_bundle_groups(cfg):
-    seqs = _packed_reads(11)
+def test_short_ragged_bundles(cfg):
+    seqs = _short_ragged_reads(11)
     nt = _nt(**cfg)
     assert nt.tscan
-    plan = nt.bundle_plan(np.array([len(x) for x in seqs], np.uint32))
-    assert (plan.bnd_block[:-1] % 64 != 0).sum() >= 5, "expected packed groups"
     res = nt.analyze(seqs, want_windows=True, want_hits=False)
     compare(nt, res, oracle_rows(seqs, cfg["patterns"], tvr=cfg.get("tvr_patterns")), check_hits=False)
 
@@ -637,7 +634,7 @@ FULL_CONFIGS = {  # patterns, TVRs, reads, variant rate, bundle path, read lengt
     "c3": ("YYAGGG", None, 10_000_000, 0.05, True, 50_000),
     "c4": ("TTAGGG TCAGGG", "TGAGGG TTGGGG", 10_000_000, 0.05, True, 50_000),
     "c5_shard": ("TTAGGG", None, 12_500_000, 0.0, False, 50_000),
-    "c10k": ("TTAGGG", None, 1_000_000, 0.0, True, 10_000),  # packed bundle groups
+    "c10k": ("TTAGGG", None, 1_000_000, 0.0, True, 10_000),
 }
 
 

@@ -36,37 +36,19 @@ def pack(seqs, L=100):
     return planes, blk, ln
 
 
-def plan_of(lengths, L, n_pass=2):
+def plan_of(lengths, L):
     """nt_bundle_plan's grouping (restated): longest first, ties in input
-    order, 32 to a bundle; a bundle alone spans ceil(ceil(n_max / L) / 64)
-    stripes, or up to 4 bundles are packed at multiples of 16 columns into at
-    most NT_TS_FLUSH(np) stripes when that leaves a smaller idle fraction."""
+    order, 32 to a bundle; a bundle spans ceil(ceil(n_max / L) / 64) stripes,
+    its first block column = 64 x its first stripe."""
     order = sorted(range(len(lengths)), key=lambda r: -int(lengths[r]))
     nb = (len(order) + 31) // 32
     bread = np.full(nb * 32, 0xFFFFFFFF, np.uint32)
     bread[:len(order)] = order
-    nblk = [(int(lengths[order[32 * b]]) + L - 1) // L for b in range(nb)]
-    fmax = 4 if n_pass == 3 else 8
     bblock = np.zeros(nb + 1, np.uint64)
-    col, b = 0, 0
-    while b < nb:
-        best, best_idle, used, w = 1, 2.0, 0, 0
-        for n in range(1, 5):
-            if b + n > nb:
-                break
-            used += nblk[b + n - 1]
-            w += -(-nblk[b + n - 1] // 16) * 16
-            st = -(-w // 64)
-            if n > 1 and st > fmax:
-                break
-            idle = (st * 64 - used) / (st * 64)
-            if idle < best_idle - 1e-12:
-                best, best_idle = n, idle
-        for i in range(best):
-            bblock[b + i] = col
-            col += -(-nblk[b] // 64) * 64 if best == 1 else -(-nblk[b + i] // 16) * 16
-        col = -(-col // 64) * 64
-        b += best
+    col = 0
+    for b in range(nb):
+        bblock[b] = col
+        col += -(-((int(lengths[order[32 * b]]) + L - 1) // L) // 64) * 64
     bblock[nb] = col
     return BundlePlan(bread, bblock, np.zeros(0, np.uint32), col // 64 * ((L + 1) // 2) * 64 * 16)
 
@@ -105,22 +87,6 @@ def test_host_tlayout_matches_definition(L):
     check_layout(planes, blk, ln, plan, L)
 
 
-@pytest.mark.parametrize("n_pass", [2, 3])
-def test_host_tlayout_packed_groups(n_pass):
-    # equal short reads (10 kb at L = 100: 100 columns a bundle, 4 bundles
-    # packed in 7 stripes for 2 passes) and a mix of lengths: bundles share
-    # stripes, each at its 16-column offset
-    rng = np.random.default_rng(n_pass)
-    alpha = np.frombuffer(b"ACGT", np.uint8)
-    lens = [10000] * 256 + [int(rng.integers(1500, 4000)) for _ in range(200)] + [700] * 64
-    seqs = [alpha[rng.integers(0, 4, n)].tobytes() for n in lens]
-    planes, blk, ln = pack(seqs, 100)
-    plan = plan_of(ln, 100, n_pass)
-    starts = plan.bnd_block[:-1].astype(np.int64)
-    assert (starts % 64 != 0).sum() >= 6, "expected packed groups"
-    check_layout(planes, blk, ln, plan, 100)
-
-
 def check_layout(planes, blk, ln, plan, L):
     got = bundle_layout_host(planes, blk, ln, plan, L)
     want = tlayout_numpy(planes, blk, ln, plan, L)
@@ -137,3 +103,6 @@ def test_host_tlayout_argument_checks():
         bundle_layout_host(planes, blk, ln, small, 100)
     with pytest.raises(Exception):
         bundle_layout_host(planes, blk, ln, plan, 171)
+    off = BundlePlan(plan.bnd_read, plan.bnd_block + np.uint64(16), plan.list, plan.tplane_bytes * 2)
+    with pytest.raises(Exception):  # a bundle that does not start on a stripe
+        bundle_layout_host(planes, blk, ln, off, 100)
