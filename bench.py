@@ -249,12 +249,12 @@ def main():
         import numpy as np
         scan_path = "bundle" if len(plan.list) == 0 else f"bundle + per-read ({len(plan.list)} reads)"
         bread = torch.from_numpy(plan.bnd_read.view(np.int32)).to(dev)
-        bblock = torch.from_numpy(plan.bnd_block.view(np.int64)).to(dev)
+        bstripe = torch.from_numpy(plan.bnd_stripe.view(np.int64)).to(dev)
         tpl = torch.empty(max(1, plan.tplane_bytes // 4), dtype=torch.int32, device=dev)
         # reads the plan leaves outside the bundles go to the per-read scan
         blist = torch.from_numpy(plan.list.view(np.int32)).to(dev) if len(plan.list) else None
-        keep = [bread, bblock, tpl, blist]
-        bundles = DeviceBundles(tpl.data_ptr(), bread.data_ptr(), bblock.data_ptr(), plan.n_bundles,
+        keep = [bread, bstripe, tpl, blist]
+        bundles = DeviceBundles(tpl.data_ptr(), bread.data_ptr(), bstripe.data_ptr(), plan.n_bundles,
                                 blist.data_ptr() if blist is not None else 0, len(plan.list), plan.tplane_bytes)
         nt.bundle_layout_device(planes.data_ptr(), blk_off.data_ptr(), lens.data_ptr(), win_off.data_ptr(),
                                 n, n * rows, bundles)

@@ -98,7 +98,7 @@ typedef struct {
    * in list[0 .. n_list) the per-read scan (list may be NULL when n_list == 0). */
   const uint32_t* tplanes;
   const uint32_t* bnd_read;   /* [n_bundles * 32] read of each slot, ~0u = empty */
-  const uint64_t* bnd_block;  /* [n_bundles + 1] first block column of each bundle (nt_bundle_plan) */
+  const uint64_t* bnd_stripe; /* [n_bundles + 1] first stripe of each bundle */
   uint64_t n_bundles;
   const uint32_t* list;       /* reads outside the bundles */
   uint64_t n_list;
@@ -161,12 +161,10 @@ int nt_pack_reads(const char* const* seqs, const uint64_t* lens, uint64_t n_read
  * program fixes the block size L).  has_exc (NULL = none) marks reads with
  * non-ACGT letters, which stay outside the bundles, as do reads of any
  * program the bundle scan does not cover (then *n_bundles = 0).  Outputs:
- * bnd_read [ceil(n/32)*32], bnd_block [ceil(n/32)+1] (each bundle's first
- * block column, a multiple of 64: every bundle starts on a stripe), list [n]
- * (the reads left out, in order), and the bytes of the T-layout buffer
- * (bnd_block[n_bundles] / 64 stripes). */
+ * bnd_read [ceil(n/32)*32], bnd_stripe [ceil(n/32)+1], list [n] (the reads
+ * left out, in order), and the bytes of the T-layout buffer. */
 int nt_bundle_plan(nt_ctx* ctx, const uint32_t* len, const uint8_t* has_exc, uint64_t n_reads,
-                   uint32_t* bnd_read, uint64_t* bnd_block, uint64_t* n_bundles, uint32_t* list,
+                   uint32_t* bnd_read, uint64_t* bnd_stripe, uint64_t* n_bundles, uint32_t* list,
                    uint64_t* n_list, uint64_t* tplane_bytes);
 /* Host (ingest): write the T-layout of the planned bundles into the host
  * buffer tplanes (tplane_bytes from the plan; every byte written) from host
@@ -174,7 +172,7 @@ int nt_bundle_plan(nt_ctx* ctx, const uint32_t* len, const uint8_t* has_exc, uin
  * (AVX2), all host threads.  nt_analyze_host builds its batches' T-layout this
  * way and uploads it beside the planes (no device transposer per batch). */
 int nt_bundle_layout_host(const uint32_t* planes, const uint64_t* blk_off, const uint32_t* len,
-                          const uint32_t* bnd_read, const uint64_t* bnd_block, uint64_t n_bundles,
+                          const uint32_t* bnd_read, const uint64_t* bnd_stripe, uint64_t n_bundles,
                           int32_t subseq_length, uint32_t* tplanes, uint64_t tplane_bytes);
 /* Device: the same T-layout (bit for bit) from the batch's device planes, for
  * callers whose reads are already resident.  Asynchronous on the context stream. */

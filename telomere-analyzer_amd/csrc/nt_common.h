@@ -90,14 +90,10 @@ struct NtProgram {
 // T-layout ("bundles", the bundle scan's copy of the reads, nt_tscan.h):
 //   reads grouped NT_BUNDLE to a bundle, slots sorted by length (non-increasing;
 //   read index ~0u = empty slot).  Bundle b's positions are cut into blocks of
-//   L = subseq_length positions; the bundles' blocks follow each other in one
-//   sequence of block COLUMNS, 64 to a STRIPE: stripe g holds T*64 16-byte
-//   words (T = ceil(L/2)), word t*64 + l = {lo, hi of position q, lo, hi of
-//   position q+1} of column 64 g + l, q = its block's start + 2t, bit s = slot s.
-//   Bundle b owns columns [bnd_block[b], bnd_block[b+1]) -- its block k is
-//   column bnd_block[b] + k, the columns past its last block hold zeros -- and
-//   starts on a stripe (bnd_block[b] a multiple of 64; the column form leaves
-//   room for bundles that share stripes).
+//   L = subseq_length positions, 64 blocks to a STRIPE; stripe g holds T*64
+//   16-byte words (T = ceil(L/2)): word t*64 + l = {lo, hi of position q,
+//   lo, hi of position q+1} of block l, q = block start + 2t, bit s = slot s.
+//   Bundle b owns stripes [bnd_stripe[b], bnd_stripe[b+1]).
 #define NT_BUNDLE 32
 
 struct NtBatch {
@@ -115,7 +111,7 @@ struct NtBatch {
   // bundle scan (nt_tscan.h); tplanes == nullptr: no bundles
   const uint32_t* tplanes;     // 16-byte words, see above
   const uint32_t* bnd_read;    // [n_bundles * NT_BUNDLE]
-  const uint64_t* bnd_block;   // [n_bundles + 1] first column of each bundle
+  const uint64_t* bnd_stripe;  // [n_bundles + 1]
   uint64_t n_bundles;
 };
 

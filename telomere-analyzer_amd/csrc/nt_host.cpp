@@ -183,7 +183,7 @@ struct nt_ctx {
   int cu_count = 256;
   DevBuf planes, blk_off, len, win_off, exc_off, exc_pos, exc_code;
   DevBuf wc, start, end, dens, flags, hits, scratch, tmask, thr, queue;
-  DevBuf tplanes, bnd_read, bnd_block, list;  // upload_reads' bundle layout
+  DevBuf tplanes, bnd_read, bnd_stripe, list;  // upload_reads' bundle layout
   HostBuf h_planes, h_meta, h_tplanes;  // upload_reads staging
   // host-path phase times (s, cumulative; nt_host_times): layout, pack,
   // T-layout, uploads, the device work and downloads, the row checks
@@ -423,7 +423,7 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
   NtBatch B{batch->planes, batch->blk_off, batch->len, batch->win_off,
             batch->exc_off, batch->exc_pos, batch->exc_code, batch->n_reads,
             tscan ? batch->list : nullptr, tscan ? batch->n_list : 0,
-            tscan ? batch->tplanes : nullptr, batch->bnd_read, batch->bnd_block, tscan ? batch->n_bundles : 0};
+            tscan ? batch->tplanes : nullptr, batch->bnd_read, batch->bnd_stripe, tscan ? batch->n_bundles : 0};
   if (tscan && batch->n_list && !batch->list) return fail(ctx, NT_E_ARG, "n_list > 0 without a list");
   const uint64_t n_scan = tscan ? batch->n_list : batch->n_reads;  // reads of the per-read scan
   NtOut O{out->win_counts, out->start, out->end, out->density, out->flags, out->hits};
@@ -547,9 +547,9 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
     for (uint64_t k = 0; k < tsub; ++k) {
       const uint64_t b0 = bb[k], b1 = bb[k + 1];
       if (b1 == b0) continue;
-      NtBatch Bt = B;  // bundles [b0, b1): bnd_block stays absolute
+      NtBatch Bt = B;  // bundles [b0, b1): bnd_stripe stays absolute
       Bt.bnd_read += NT_BUNDLE * b0;
-      Bt.bnd_block += b0;
+      Bt.bnd_stripe += b0;
       Bt.n_bundles = b1 - b0;
       const uint64_t tgrid = std::max<uint64_t>(1, std::min<uint64_t>((Bt.n_bundles + 3) / 4, (uint64_t)ctx->cu_count * tbpc));
       const int pe = ev ? ctx->ev_nt[ctx->n_ev - 1] : 0;  // event pair of this launch
@@ -691,9 +691,9 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
 // 64) stripes of ceil(L/2) * 64 16-byte words, and must stay below 2^31 bytes
 // (the scan's buffer offsets): reads longer than that stay out.
 int nt_bundle_plan(nt_ctx* ctx, const uint32_t* len, const uint8_t* has_exc, uint64_t n_reads,
-                   uint32_t* bnd_read, uint64_t* bnd_block, uint64_t* n_bundles, uint32_t* list,
+                   uint32_t* bnd_read, uint64_t* bnd_stripe, uint64_t* n_bundles, uint32_t* list,
                    uint64_t* n_list, uint64_t* tplane_bytes) {
-  if (!ctx || !n_bundles || !n_list || !tplane_bytes || (n_reads && (!len || !bnd_read || !bnd_block || !list)))
+  if (!ctx || !n_bundles || !n_list || !tplane_bytes || (n_reads && (!len || !bnd_read || !bnd_stripe || !list)))
     return NT_E_ARG;
   if (!ctx->compiled) return fail(ctx, NT_E_STATE, "nt_compile() not called");
   const uint64_t L = (uint64_t)ctx->prog.L, T = (L + 1) / 2;
@@ -710,17 +710,20 @@ int nt_bundle_plan(nt_ctx* ctx, const uint32_t* len, const uint8_t* has_exc, uin
   }
   std::stable_sort(in.begin(), in.end(), [&](uint32_t a, uint32_t b) { return len[a] > len[b]; });
   const uint64_t nb = (in.size() + NT_BUNDLE - 1) / NT_BUNDLE;
-  for (uint64_t i = 0; i < nb * NT_BUNDLE; ++i) bnd_read[i] = i < in.size() ? in[i] : 0xFFFFFFFFu;
-  auto nblk = [&](uint64_t b) { return ((uint64_t)len[in[b * NT_BUNDLE]] + L - 1) / L; };  // slot 0: the longest
-  uint64_t col = 0;  // each bundle over whole stripes
+  uint64_t g = 0;
   for (uint64_t b = 0; b < nb; ++b) {
-    bnd_block[b] = col;
-    col += (nblk(b) + 63) / 64 * 64;
+    bnd_stripe[b] = g;
+    for (uint64_t s = 0; s < NT_BUNDLE; ++s) {
+      const uint64_t i = b * NT_BUNDLE + s;
+      bnd_read[i] = i < in.size() ? in[i] : 0xFFFFFFFFu;
+    }
+    const uint64_t nmax = len[in[b * NT_BUNDLE]];
+    g += ((nmax + L - 1) / L + 63) / 64;
   }
-  bnd_block[nb] = col;
+  bnd_stripe[nb] = g;
   *n_bundles = nb;
   *n_list = nl;
-  *tplane_bytes = col / 64 * stripe_bytes;
+  *tplane_bytes = g * stripe_bytes;
   return NT_OK;
 }
 
@@ -734,7 +737,7 @@ int nt_bundle_layout(nt_ctx* ctx, const nt_batch* batch, uint32_t* tplanes, uint
   const uint64_t stripe_bytes = (uint64_t)((ctx->prog.L + 1) / 2) * 64 * 16;
   if (tplane_bytes % stripe_bytes) return fail(ctx, NT_E_ARG, "tplane_bytes is not a whole number of stripes");
   NtBatch B{batch->planes, batch->blk_off, batch->len, batch->win_off, nullptr, nullptr, nullptr, batch->n_reads,
-            nullptr, 0, tplanes, batch->bnd_read, batch->bnd_block, batch->n_bundles};
+            nullptr, 0, tplanes, batch->bnd_read, batch->bnd_stripe, batch->n_bundles};
   hipError_t e = nt_dev_launch_bundle(&B, tplane_bytes / stripe_bytes, tplanes, ctx->prog.L, ctx->prog.div32_m,
                                       ctx->prog.div32_s, ctx->stream, ctx->cu_count);
   return e == hipSuccess ? NT_OK : hip_fail(ctx, e, "launch nt_bundle_kernel");
@@ -897,30 +900,30 @@ static int upload_reads(nt_ctx* ctx, const char* const* seqs, const uint64_t* le
   // packed planes (ingest) and uploaded beside them
   uint64_t nb = 0, nl = 0, tpb = 0;
   std::vector<uint32_t> h_bread, h_list;
-  std::vector<uint64_t> h_bblock;
+  std::vector<uint64_t> h_bstripe;
   if (ctx->tjit_fn && want_bundles) {
     std::vector<uint8_t> hx(n_reads);
     for (uint64_t r = 0; r < n_reads; ++r) hx[r] = cnt[r] > 0;
     h_bread.resize((n_reads + NT_BUNDLE - 1) / NT_BUNDLE * NT_BUNDLE + NT_BUNDLE);
-    h_bblock.resize((n_reads + NT_BUNDLE - 1) / NT_BUNDLE + 2);
+    h_bstripe.resize((n_reads + NT_BUNDLE - 1) / NT_BUNDLE + 2);
     h_list.resize(n_reads + 1);
-    int rc = nt_bundle_plan(ctx, h_len, hx.data(), n_reads, h_bread.data(), h_bblock.data(), &nb, h_list.data(),
+    int rc = nt_bundle_plan(ctx, h_len, hx.data(), n_reads, h_bread.data(), h_bstripe.data(), &nb, h_list.data(),
                             &nl, &tpb);
     if (rc) return rc;
     h_bread.resize(nb * NT_BUNDLE);
-    h_bblock.resize(nb + 1);
+    h_bstripe.resize(nb + 1);
     h_list.resize(nl);
   }
   if (nb) {
     lap(3);
     if ((e = ctx->h_tplanes.ensure(tpb)) != hipSuccess) return hip_fail(ctx, e, "hipHostMalloc(tplanes)");
-    int rc = nt_bundle_layout_host(hp, h_blk, h_len, h_bread.data(), h_bblock.data(), nb, L,
+    int rc = nt_bundle_layout_host(hp, h_blk, h_len, h_bread.data(), h_bstripe.data(), nb, L,
                                    (uint32_t*)ctx->h_tplanes.p, tpb);
     if (rc) return fail(ctx, rc, "nt_bundle_layout_host");
     lap(2);
     NT_UP_PTR(tplanes, ctx->h_tplanes.p, tpb);
     NT_UP(bnd_read, h_bread);
-    NT_UP(bnd_block, h_bblock);
+    NT_UP(bnd_stripe, h_bstripe);
     if (nl) { NT_UP(list, h_list); }
     // the vectors are pageable: finish their copies before they go
     if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess) return hip_fail(ctx, e, "hipStreamSynchronize");
@@ -934,7 +937,7 @@ static int upload_reads(nt_ctx* ctx, const char* const* seqs, const uint64_t* le
                 te ? (const uint8_t*)ctx->exc_code.p : nullptr, n_reads, tw,
                 nb ? (const uint32_t*)ctx->tplanes.p : nullptr,
                 nb ? (const uint32_t*)ctx->bnd_read.p : nullptr,
-                nb ? (const uint64_t*)ctx->bnd_block.p : nullptr, nb,
+                nb ? (const uint64_t*)ctx->bnd_stripe.p : nullptr, nb,
                 nl && nb ? (const uint32_t*)ctx->list.p : nullptr, nb ? nl : 0};
   lap(3);
   *max_len = ml;

@@ -164,7 +164,7 @@ nt_bundle_kernel(NtBatch B, uint32_t* __restrict__ tp, int L, uint32_t div_m, ui
   for (uint64_t b = blockIdx.x; b < B.n_bundles; b += gridDim.x) {
     const uint32_t r = B.bnd_read[b * NT_BUNDLE + s];
     const int64_t len = r != 0xFFFFFFFFu ? (int64_t)B.len[r] : 0;
-    const uint64_t c0 = uniform_u64(B.bnd_block[b]), c1 = uniform_u64(B.bnd_block[b + 1]);  // its columns
+    const uint64_t g0 = uniform_u64(B.bnd_stripe[b]), g1 = uniform_u64(B.bnd_stripe[b + 1]);
     if (threadIdx.x < NT_BUNDLE) {
       const uint64_t bo = r != 0xFFFFFFFFu ? B.blk_off[r] : 0ull;
       *reinterpret_cast<uint4*>(meta + 4 * s) = make_uint4((uint32_t)len, (uint32_t)bo, (uint32_t)(bo >> 32), 0u);
@@ -189,10 +189,12 @@ nt_bundle_kernel(NtBatch B, uint32_t* __restrict__ tp, int L, uint32_t div_m, ui
         }
       }
     };
-    const uint64_t nu = (c1 - c0 + 31) / 32;  // 32-column units of the bundle
+    const uint64_t nu = 2 * (g1 - g0);  // half stripes of the bundle
     fetch(0);
     for (uint64_t u = 0; u < nu; ++u) {
-      const uint64_t w0 = (uint64_t)L * u;  // first plane word of the unit
+      const uint64_t G = g0 + (u >> 1);
+      const int h = (int)(u & 1);
+      const uint64_t w0 = (uint64_t)L * u;  // first plane word of the half stripe
 #pragma unroll
       for (int k = 0; k < kMaxE; ++k) {
         const uint32_t e = threadIdx.x + 256u * k;
@@ -226,14 +228,10 @@ nt_bundle_kernel(NtBatch B, uint32_t* __restrict__ tp, int L, uint32_t div_m, ui
         }
       }
       __syncthreads();
-      // 3. rows t: column c = c0 + 32 u + l (l < 32, inside the bundle) at word
-      // (c / 64 T + t) 64 + c % 64
-      const uint64_t col = c0 + 32 * u + s;
-      if (col < c1) {
-        uint4* out = reinterpret_cast<uint4*>(tp) + (col >> 6) * (uint64_t)T * kWave + (col & 63);
-        for (int t = threadIdx.x >> 5; t < T; t += 8)
-          out[(uint64_t)t * kWave] = *reinterpret_cast<const uint4*>(rows + t * kBndRowWords + 4 * s);
-      }
+      // 3. rows t: 32 words of 16 bytes at word (G T + t) 64 + 32 h + l
+      uint4* out = reinterpret_cast<uint4*>(tp) + G * (uint64_t)T * kWave + 32 * h;
+      for (int t = threadIdx.x >> 5; t < T; t += 8)
+        out[(uint64_t)t * kWave + s] = *reinterpret_cast<const uint4*>(rows + t * kBndRowWords + 4 * s);
       __syncthreads();
     }
     __syncthreads();  // meta is rewritten for the next bundle

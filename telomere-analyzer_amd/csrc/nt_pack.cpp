@@ -376,15 +376,10 @@ int64_t pack_one(const unsigned char* s, uint64_t n, int rc, uint32_t* out, uint
 // -> 32 positions; position p = block k = p / L (stripe k / 64, lane k % 64),
 // offset o = p % L (row o / 2, half o % 2).
 static void tlayout_bundle(const uint32_t* planes, const uint64_t* blk_off, const uint32_t* len,
-                           const uint32_t* slots, uint64_t c0, uint64_t c1, uint32_t L, uint32_t* tp) {
-  // bundle columns [c0, c1): word (col / 64 * T + t) * 64 + col % 64
+                           const uint32_t* slots, uint64_t g0, uint64_t nst, uint32_t L, uint32_t* tp) {
   const uint64_t T = (L + 1) / 2;
-  auto word = [&](uint64_t col, uint64_t t) { return tp + (((col >> 6) * T + t) * 64 + (col & 63)) * 4; };
-  for (uint64_t c = c0; c < c1;) {  // zero the bundle's columns, a run of one stripe's lanes per t
-    const uint64_t e = std::min<uint64_t>(c1, (c | 63) + 1);
-    for (uint64_t t = 0; t < T; ++t) std::memset(word(c, t), 0, (e - c) * 16);
-    c = e;
-  }
+  uint32_t* base = tp + g0 * T * 64 * 4;
+  std::memset(base, 0, nst * T * 64 * 16);
   uint64_t n_max = 0;
   const uint32_t* pl[NT_BUNDLE];
   uint64_t ln[NT_BUNDLE];
@@ -394,7 +389,7 @@ static void tlayout_bundle(const uint32_t* planes, const uint64_t* blk_off, cons
     pl[s] = r != 0xFFFFFFFFu ? planes + 2 * blk_off[r] : nullptr;
     n_max = std::max(n_max, ln[s]);
   }
-  n_max = std::min<uint64_t>(n_max, (c1 - c0) * L);
+  n_max = std::min<uint64_t>(n_max, nst * 64 * L);
   alignas(32) uint32_t xl[32], xh[32], yl[32], yh[32];
   uint64_t k = 0, o = 0;  // block and offset of position 32 w
   for (uint64_t w = 0; 32 * w < n_max; ++w) {
@@ -414,7 +409,7 @@ static void tlayout_bundle(const uint32_t* planes, const uint64_t* blk_off, cons
     const int np = (int)std::min<uint64_t>(32, n_max - 32 * w);
     uint64_t kk = k, oo = o;
     for (int i = 0; i < np; ++i) {
-      uint32_t* q = word(c0 + kk, oo >> 1) + 2 * (oo & 1);
+      uint32_t* q = base + (((kk >> 6) * T + (oo >> 1)) * 64 + (kk & 63)) * 4 + 2 * (oo & 1);
       q[0] = yl[i];
       q[1] = yh[i];
       if (++oo == L) {
@@ -644,21 +639,18 @@ int nt_pack_reads(const char* const* seqs, const uint64_t* lens, uint64_t n_read
 
 
 int nt_bundle_layout_host(const uint32_t* planes, const uint64_t* blk_off, const uint32_t* len,
-                          const uint32_t* bnd_read, const uint64_t* bnd_block, uint64_t n_bundles,
+                          const uint32_t* bnd_read, const uint64_t* bnd_stripe, uint64_t n_bundles,
                           int32_t subseq_length, uint32_t* tplanes, uint64_t tplane_bytes) {
   if (n_bundles == 0) return NT_OK;
-  if (!planes || !blk_off || !len || !bnd_read || !bnd_block || !tplanes) return NT_E_ARG;
+  if (!planes || !blk_off || !len || !bnd_read || !bnd_stripe || !tplanes) return NT_E_ARG;
   if (subseq_length < 1 || subseq_length > 170) return NT_E_ARG;
   const uint64_t L = (uint64_t)subseq_length, T = (L + 1) / 2;
-  if (bnd_block[n_bundles] % 64 || bnd_block[n_bundles] / 64 * T * 64 * 16 > tplane_bytes) return NT_E_ARG;
-  for (uint64_t b = 0; b < n_bundles; ++b) {
-    if (bnd_block[b + 1] < bnd_block[b] || bnd_block[b] % 64) return NT_E_ARG;  // bundles start on stripes
-    const uint32_t r0 = bnd_read[NT_BUNDLE * b];
-    if (r0 != 0xFFFFFFFFu && (len[r0] + L - 1) / L > bnd_block[b + 1] - bnd_block[b]) return NT_E_ARG;
-  }
+  if (bnd_stripe[n_bundles] * T * 64 * 16 > tplane_bytes) return NT_E_ARG;
+  for (uint64_t b = 0; b < n_bundles; ++b)
+    if (bnd_stripe[b + 1] < bnd_stripe[b]) return NT_E_ARG;
   parallel_for(n_bundles, [&](uint64_t b) {
-    tlayout_bundle(planes, blk_off, len, bnd_read + NT_BUNDLE * b, bnd_block[b], bnd_block[b + 1], (uint32_t)L,
-                   tplanes);
+    tlayout_bundle(planes, blk_off, len, bnd_read + NT_BUNDLE * b, bnd_stripe[b], bnd_stripe[b + 1] - bnd_stripe[b],
+                   (uint32_t)L, tplanes);
   });
   return NT_OK;
 }

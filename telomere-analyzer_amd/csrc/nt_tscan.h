@@ -818,7 +818,7 @@ __device__ __forceinline__ void tscan_bundles(const NtBatch& B, const NtOut& O, 
     }
     const int nblk = ((int)n_max + kL - 1) / kL;
     const int nst = (nblk + kWave - 1) / kWave;
-    const uint64_t g0 = uniform_u64(B.bnd_block[b]) >> 6, g1 = uniform_u64(B.bnd_block[b + 1]) >> 6;  // its stripes
+    const uint64_t g0 = uniform_u64(B.bnd_stripe[b]), g1 = uniform_u64(B.bnd_stripe[b + 1]);
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint32_t*>(B.tplanes) + g0 * (uint64_t)kT * kWave * 4, (short)0,
         (int)((g1 - g0) * (uint64_t)kT * kWave * 16), 0x00020000);

@@ -56,7 +56,7 @@ class NtBatch(ctypes.Structure):
         ("win_off", ctypes.c_void_p), ("exc_off", ctypes.c_void_p), ("exc_pos", ctypes.c_void_p),
         ("exc_code", ctypes.c_void_p), ("n_reads", ctypes.c_uint64), ("n_windows", ctypes.c_uint64),
         # bundle scan (optional): the T-layout and its bundles, the reads left to the per-read scan
-        ("tplanes", ctypes.c_void_p), ("bnd_read", ctypes.c_void_p), ("bnd_block", ctypes.c_void_p),
+        ("tplanes", ctypes.c_void_p), ("bnd_read", ctypes.c_void_p), ("bnd_stripe", ctypes.c_void_p),
         ("n_bundles", ctypes.c_uint64), ("list", ctypes.c_void_p), ("n_list", ctypes.c_uint64),
     ]
 

@@ -238,7 +238,7 @@ class NanoTel:
         b = bundles
         return NtBatch(planes, blk_off, lengths, win_off, exc_off or None, exc_pos or None,
                        exc_code or None, int(n_reads), int(n_windows),
-                       b.tplanes if b else None, b.bnd_read if b else None, b.bnd_block if b else None,
+                       b.tplanes if b else None, b.bnd_read if b else None, b.bnd_stripe if b else None,
                        b.n_bundles if b else 0, (b.list or None) if b else None, b.n_list if b else 0)
 
     def bundle_plan(self, lengths, has_exc=None):
@@ -276,19 +276,19 @@ class NanoTel:
 
 
 class BundlePlan:
-    """Host result of nt_bundle_plan: bnd_read (n_bundles*32 u32), bnd_block
+    """Host result of nt_bundle_plan: bnd_read (n_bundles*32 u32), bnd_stripe
     (n_bundles+1 u64), list (the reads left to the per-read scan), tplane_bytes."""
 
-    def __init__(self, bnd_read, bnd_block, lst, tplane_bytes):
-        self.bnd_read, self.bnd_block, self.list, self.tplane_bytes = bnd_read, bnd_block, lst, tplane_bytes
-        self.n_bundles = len(bnd_block) - 1 if len(bnd_block) else 0
+    def __init__(self, bnd_read, bnd_stripe, lst, tplane_bytes):
+        self.bnd_read, self.bnd_stripe, self.list, self.tplane_bytes = bnd_read, bnd_stripe, lst, tplane_bytes
+        self.n_bundles = len(bnd_stripe) - 1 if len(bnd_stripe) else 0
 
 
 class DeviceBundles:
     """Device pointers (ints) of a bundle layout for scan_call_device."""
 
-    def __init__(self, tplanes, bnd_read, bnd_block, n_bundles, lst, n_list, tplane_bytes):
-        self.tplanes, self.bnd_read, self.bnd_block, self.n_bundles = tplanes, bnd_read, bnd_block, n_bundles
+    def __init__(self, tplanes, bnd_read, bnd_stripe, n_bundles, lst, n_list, tplane_bytes):
+        self.tplanes, self.bnd_read, self.bnd_stripe, self.n_bundles = tplanes, bnd_read, bnd_stripe, n_bundles
         self.list, self.n_list, self.tplane_bytes = lst, n_list, tplane_bytes
 
 
@@ -298,7 +298,7 @@ def bundle_layout_host(planes, blk_off, lengths, plan, subseq_length):
     bo = np.ascontiguousarray(blk_off, np.uint64)
     ln = np.ascontiguousarray(lengths, np.uint32)
     br = np.ascontiguousarray(plan.bnd_read, np.uint32)
-    bs = np.ascontiguousarray(plan.bnd_block, np.uint64)
+    bs = np.ascontiguousarray(plan.bnd_stripe, np.uint64)
     out = np.empty(max(1, plan.tplane_bytes // 4), np.uint32)
     _check(lib().nt_bundle_layout_host(pl.ctypes.data, bo.ctypes.data, ln.ctypes.data, br.ctypes.data,
                                        bs.ctypes.data, plan.n_bundles, int(subseq_length), out.ctypes.data,

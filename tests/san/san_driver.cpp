@@ -200,18 +200,16 @@ static void test_packer_and_tlayout(std::mt19937_64& g) {
     std::stable_sort(in.begin(), in.end(), [&](uint32_t a, uint32_t b) { return lens[a] > lens[b]; });
     const uint64_t L = 37, T = (L + 1) / 2, nb = (in.size() + 31) / 32;
     std::vector<uint32_t> bread(nb * 32, 0xFFFFFFFFu);
-    // block columns: each bundle over whole stripes
-    std::vector<uint64_t> bblock(nb + 1);
-    uint64_t col = 0;
+    std::vector<uint64_t> bstripe(nb + 1);
+    uint64_t gs = 0;
     for (uint64_t b = 0; b < nb; ++b) {
+      bstripe[b] = gs;
       for (uint64_t s = 0; s < 32 && b * 32 + s < in.size(); ++s) bread[b * 32 + s] = in[b * 32 + s];
-      bblock[b] = col;
-      col += ((lens[in[b * 32]] + L - 1) / L + 63) / 64 * 64;
+      gs += ((lens[in[b * 32]] + L - 1) / L + 63) / 64;
     }
-    bblock[nb] = col;
-    const uint64_t gs = col / 64;
+    bstripe[nb] = gs;
     std::vector<uint32_t> tp(gs * T * 64 * 4 + 4, 0xDEADBEEFu);
-    CHECK(nt_bundle_layout_host(planes.data(), blk.data(), len.data(), bread.data(), bblock.data(), nb, (int)L,
+    CHECK(nt_bundle_layout_host(planes.data(), blk.data(), len.data(), bread.data(), bstripe.data(), nb, (int)L,
                                 tp.data(), gs * T * 64 * 16) == 0);
     CHECK(tp[gs * T * 64 * 4] == 0xDEADBEEFu);  // nothing past the buffer
     for (uint64_t b = 0; b < nb; ++b)
@@ -220,8 +218,7 @@ static void test_packer_and_tlayout(std::mt19937_64& g) {
         if (r == 0xFFFFFFFFu) continue;
         for (uint64_t p = 0; p < lens[r]; p += 1 + g() % 7) {
           const uint64_t k = p / L, o = p % L;
-          const uint64_t c = bblock[b] + k;  // the block's column
-          const uint64_t idx = ((c / 64) * T + o / 2) * 64 + c % 64;
+          const uint64_t idx = ((bstripe[b] + k / 64) * T + o / 2) * 64 + k % 64;
           const int got = (int)((tp[4 * idx + 2 * (o & 1)] >> s) & 1u) | (int)(((tp[4 * idx + 2 * (o & 1) + 1] >> s) & 1u) << 1);
           CHECK(got == code2(seqs[r][p]));
         }

@@ -468,9 +468,9 @@ def _device_bundles(nt, t, n, read_len):
     from nanotel_amd.api import DeviceBundles
     plan = nt.bundle_plan(np.full(n, read_len, np.uint32))
     d = dict(bnd_read=torch.from_numpy(plan.bnd_read.view(np.int32)).cuda(),
-             bnd_block=torch.from_numpy(plan.bnd_block.view(np.int64)).cuda(),
+             bnd_stripe=torch.from_numpy(plan.bnd_stripe.view(np.int64)).cuda(),
              tplanes=torch.empty(max(1, plan.tplane_bytes // 4), dtype=torch.int32, device="cuda"))
-    b = DeviceBundles(d["tplanes"].data_ptr(), d["bnd_read"].data_ptr(), d["bnd_block"].data_ptr(),
+    b = DeviceBundles(d["tplanes"].data_ptr(), d["bnd_read"].data_ptr(), d["bnd_stripe"].data_ptr(),
                       plan.n_bundles, 0, 0, plan.tplane_bytes)
     nt.bundle_layout_device(t["planes"].data_ptr(), t["blk_off"].data_ptr(), t["lens"].data_ptr(),
                             t["win_off"].data_ptr(), n, n * t["rows"], b)
@@ -614,7 +614,7 @@ def test_host_tlayout_matches_device_mixed_lengths():
     dln = torch.from_numpy(ln.view(np.int32)).cuda()
     dwo = torch.from_numpy(wo.view(np.int64)).cuda()
     br = torch.from_numpy(plan.bnd_read.view(np.int32)).cuda()
-    bs = torch.from_numpy(plan.bnd_block.view(np.int64)).cuda()
+    bs = torch.from_numpy(plan.bnd_stripe.view(np.int64)).cuda()
     tp = torch.full((plan.tplane_bytes // 4,), -1, dtype=torch.int32, device="cuda")
     bb = DeviceBundles(tp.data_ptr(), br.data_ptr(), bs.data_ptr(), plan.n_bundles, 0, 0, plan.tplane_bytes)
     nt.bundle_layout_device(dp.data_ptr(), dblk.data_ptr(), dln.data_ptr(), dwo.data_ptr(), n, int(tw.value), bb)
@@ -697,7 +697,7 @@ def test_offsets_beyond_32_bits(path):
     # and their T-layout word offsets pass 2^32.  Reproduced without
     # allocating them: the planes / window-count / T-layout base pointers are
     # shifted down by exactly the offsets added to blk_off / win_off /
-    # bnd_block.  Bundle path: the bundle scan reads the shifted T-layout, the
+    # bnd_stripe.  Bundle path: the bundle scan reads the shifted T-layout, the
     # calling kernel the shifted planes.
     import torch
     from nanotel_amd import synth_params
@@ -717,7 +717,7 @@ def test_offsets_beyond_32_bits(path):
         b, keep = _device_bundles(nt, t, n, read_len)
         stripe_bytes = 50 * 64 * 16
         soff = (1 << 35) // stripe_bytes + 1  # stripes: T-layout offsets past 2^35 bytes (2^33 words)
-        bs = keep["bnd_block"] + 64 * soff  # (block columns, 64 a stripe)
+        bs = keep["bnd_stripe"] + soff
         bundles = DeviceBundles(b.tplanes - soff * stripe_bytes, b.bnd_read, bs.data_ptr(), b.n_bundles, 0, 0,
                                 b.tplane_bytes)
         keep["bs_shift"] = bs

@@ -38,19 +38,19 @@ def pack(seqs, L=100):
 
 def plan_of(lengths, L):
     """nt_bundle_plan's grouping (restated): longest first, ties in input
-    order, 32 to a bundle; a bundle spans ceil(ceil(n_max / L) / 64) stripes,
-    its first block column = 64 x its first stripe."""
+    order, 32 to a bundle; a bundle spans ceil(ceil(n_max / L) / 64) stripes."""
     order = sorted(range(len(lengths)), key=lambda r: -int(lengths[r]))
     nb = (len(order) + 31) // 32
     bread = np.full(nb * 32, 0xFFFFFFFF, np.uint32)
     bread[:len(order)] = order
-    bblock = np.zeros(nb + 1, np.uint64)
-    col = 0
+    bstripe = np.zeros(nb + 1, np.uint64)
+    g = 0
     for b in range(nb):
-        bblock[b] = col
-        col += -(-((int(lengths[order[32 * b]]) + L - 1) // L) // 64) * 64
-    bblock[nb] = col
-    return BundlePlan(bread, bblock, np.zeros(0, np.uint32), col // 64 * ((L + 1) // 2) * 64 * 16)
+        bstripe[b] = g
+        nmax = int(lengths[order[32 * b]])
+        g += ((nmax + L - 1) // L + 63) // 64
+    bstripe[nb] = g
+    return BundlePlan(bread, bstripe, np.zeros(0, np.uint32), g * ((L + 1) // 2) * 64 * 16)
 
 
 def tlayout_numpy(planes, blk, ln, plan, L):
@@ -68,8 +68,7 @@ def tlayout_numpy(planes, blk, ln, plan, L):
             lo = (w >> (p % 32).astype(np.uint32)) & 1
             hi = (x >> (p % 32).astype(np.uint32)) & 1
             k, o = p // L, p % L
-            c = int(plan.bnd_block[b]) + k  # the block's column
-            idx = ((c // 64) * T + o // 2) * 64 + c % 64
+            idx = ((int(plan.bnd_stripe[b]) + k // 64) * T + o // 2) * 64 + k % 64
             d = 4 * idx + 2 * (o % 2)
             np.bitwise_or.at(out, d, (lo << s).astype(np.uint32))
             np.bitwise_or.at(out, d + 1, (hi << s).astype(np.uint32))
@@ -84,10 +83,6 @@ def test_host_tlayout_matches_definition(L):
     seqs = [alpha[rng.integers(0, 4, n)].tobytes() for n in lens]
     planes, blk, ln = pack(seqs, L)
     plan = plan_of(ln, L)
-    check_layout(planes, blk, ln, plan, L)
-
-
-def check_layout(planes, blk, ln, plan, L):
     got = bundle_layout_host(planes, blk, ln, plan, L)
     want = tlayout_numpy(planes, blk, ln, plan, L)
     assert got.shape == want.shape
@@ -98,11 +93,8 @@ def check_layout(planes, blk, ln, plan, L):
 def test_host_tlayout_argument_checks():
     planes, blk, ln = pack([b"ACGT" * 100], 100)
     plan = plan_of(ln, 100)
-    small = BundlePlan(plan.bnd_read, plan.bnd_block, plan.list, plan.tplane_bytes - 16)
+    small = BundlePlan(plan.bnd_read, plan.bnd_stripe, plan.list, plan.tplane_bytes - 16)
     with pytest.raises(Exception):
         bundle_layout_host(planes, blk, ln, small, 100)
     with pytest.raises(Exception):
         bundle_layout_host(planes, blk, ln, plan, 171)
-    off = BundlePlan(plan.bnd_read, plan.bnd_block + np.uint64(16), plan.list, plan.tplane_bytes * 2)
-    with pytest.raises(Exception):  # a bundle that does not start on a stripe
-        bundle_layout_host(planes, blk, ln, off, 100)

@@ -19,7 +19,7 @@ for f in glob.glob(f"{out}/sq/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"]
         if "nt_" not in k: continue
-        k = "scan" if "scan" in k else ("call" if "call" in k else k[:40])
+        k = k.split("(")[0].split(" ")[-1][:40]  # the kernel's name (a split calling kernel per pass)
         acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, d in acc.items():
     print(k, {c: sum(v) / len(v) for c, v in sorted(d.items())})
