@@ -195,7 +195,10 @@ def main():
         print(f"bench.py: {world} ranks over RCCL need {world} GPUs, {torch.cuda.device_count()} visible "
               f"(NT_BENCH_BACKEND=gloo rehearses N ranks on fewer GPUs)", file=sys.stderr)
         sys.exit(2)
-    if world > 1:
+    # NT_DIST_FORCE=1: join the process group and run the collectives even
+    # with one rank (exercises the RCCL path on a one-GPU box)
+    grouped = world > 1 or os.environ.get("NT_DIST_FORCE") == "1"
+    if grouped:
         torch.cuda.set_device(local)
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -269,7 +272,7 @@ def main():
         step()
     torch.cuda.synchronize(dev)
     nt.set_profiling(True)  # HIP events around each kernel, on the launch stream
-    if world > 1:
+    if grouped:
         dist.barrier()
     torch.cuda.synchronize(dev)
     evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
@@ -279,7 +282,7 @@ def main():
         step()
         evs[i + 1].record(stream)
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if grouped:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()
@@ -288,7 +291,7 @@ def main():
     n_calls, scan_ms, call_ms = nt.kernel_times()
     assert n_calls == args.steps
     launches = nt.kernel_launches()  # the bundle scan runs in ranges: per-LAUNCH figures below
-    if world > 1:
+    if grouped:
         t = torch.tensor([wall], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wall = float(t.item())
@@ -347,7 +350,7 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(cfg)
         print(json.dumps(out))
-    if world > 1:
+    if grouped:
         dist.destroy_process_group()
 
 

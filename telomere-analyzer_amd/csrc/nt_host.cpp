@@ -524,7 +524,9 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
     // the bundle scan first: one wave per bundle, exactly the resident blocks
     // (one per CU while a calling kernel runs beside it: room for its waves)
     const uint32_t thr_full = ctx->thr_h[std::min<size_t>((size_t)L, ctx->thr_h.size() - 1)];
-    const int tbpc = tsub > 1 ? 1 : ctx->tscan_bpc;
+    int tbpc = tsub > 1 ? 1 : ctx->tscan_bpc;
+    if (const char* v = std::getenv("NT_TSCAN_RANGE_BPC"))  // tuning: blocks per CU beside the calling
+      if (tsub > 1) tbpc = std::max(1, std::min(ctx->tscan_bpc, std::atoi(v)));
     // range sizes: geometric with NT_TRATIO (default 1 = equal).  Smaller later
     // ranges leave less calling exposed at the end but measured no better: the
     // calling beside a range's scan slows that scan (contention), 3.34-3.61 ms

@@ -736,16 +736,26 @@ constexpr int kTsSlotWords = 12;
 // read-modify-write in the memory system).  22.5 KB at most: one workgroup
 // per CU (the scan runs at one wave per SIMD) leaves room for two of the
 // calling kernel's beside it.
+#ifndef NT_TS_KF2  // stripes per flush of a 2-pass program (even)
+#define NT_TS_KF2 8
+#endif
+#ifndef NT_TS_KF3  // ... of a 3-pass program
+#define NT_TS_KF3 4
+#endif
 template <int kNP>
 struct TsAux {
-  static constexpr int kF = kNP == 3 ? 4 : 8;                 // stripes per flush (even)
+  static constexpr int kF = kNP == 3 ? NT_TS_KF3 : NT_TS_KF2;  // stripes per flush (even)
+  static_assert(kF >= 2 && kF % 2 == 0, "flush depth");
   static constexpr int kCtWords = kNP * NT_BUNDLE * 32;       // [p][s][2 stripes x 16 words]
   static constexpr int kTmWords = kNP * NT_BUNDLE * kF * 2;   // [p][s][stripe] u64
   static constexpr int kCkWords = kNP * NT_BUNDLE * 4 * kF;   // [p][s][4 stripe + g] u32
   static constexpr int kWords = kCtWords + kTmWords + kCkWords;
 };
-constexpr int kTsLdsWords = NT_BUNDLE * kTsSlotWords + 5376;
-static_assert(TsAux<2>::kWords <= 5376 && TsAux<3>::kWords <= 5376, "LDS");
+// per-wave LDS words of a kNP-pass program's bundle scan
+template <int kNP>
+constexpr int ts_lds_words() {
+  return NT_BUNDLE * kTsSlotWords + TsAux<kNP>::kWords;
+}
 
 // 4x4 byte transpose inside every quad of lanes: lane i of the quad gets byte
 // i of the quad's four words (byte i' from lane i') -- two DPP exchanges

@@ -11,8 +11,10 @@ NanoTel.R:2434-2508), host side.
 written as <barcode>_filtered_sorted_summary.csv (write_csv, the summary's
 number formatting) and <barcode>_results.txt (n, median telomere length with
 mismatch, % shorter than 2 kb).  NA comparisons drop the row, as dplyr's
-filter does.  The ggplot2 figure (<barcode>_telomere_plot.png) is not drawn:
-`plot_rows` returns its data (read_index and the three plotted columns).
+filter does.  The ggplot2 figure (<barcode>_telomere_plot.png, NanoTel.R:
+2486-2506) is drawn with matplotlib in ggplot2's layout with theme_prism's
+look (12 x 6 in at 150 dpi, three lines over read_index, legend at the
+bottom); it is not pixel-identical to R's (no ggplot2 rasteriser here).
 """
 import heapq
 import math
@@ -97,9 +99,51 @@ def results_lines(barcode, filtered):
             f"% of telomeres shorter than 2kb            : {pct_s}%"]
 
 
-def write_analysis(save_path, barcode, rows, columns, format_row, sci_threshold=None):
-    """Writes <barcode>_filtered_sorted_summary.csv and <barcode>_results.txt;
-    returns the plot rows."""
+# scale_color_manual of NanoTel.R:2491-2495, in the legend's (alphabetical) order
+PLOT_SERIES = (("Read Length", 1, "#E8735A"),
+               ("Running Median Telomere Length", 3, "#4169E1"),
+               ("Telomere Length (mismatch)", 2, "#228B22"))
+
+
+def write_telomere_plot(path, plot):
+    """<barcode>_telomere_plot.png: ggplot(df_for_plot, aes(x = read_index)) +
+    three geom_line()s (NanoTel.R:2486-2506), title "Telomere Analysis", axis
+    labels and the legend at the bottom as there; theme_prism's look: no grid,
+    black axis lines with outward ticks, bold titles.  plot: analyze()'s plot
+    rows.  An empty plot (no read kept) draws the empty panel, as ggplot2."""
+    import matplotlib
+    matplotlib.use("Agg")
+    import matplotlib.pyplot as plt
+    fig = plt.figure(figsize=(12, 6), dpi=150)
+    try:
+        ax = fig.add_subplot(1, 1, 1)
+        x = [r[0] for r in plot]
+        # ggplot2 geom_line: linewidth 0.5 mm = 1.42 pt; draw order = the layers
+        for name, col, colour in (PLOT_SERIES[0], PLOT_SERIES[2], PLOT_SERIES[1]):
+            ax.plot(x, [r[col] for r in plot], color=colour, linewidth=1.42, label=name)
+        ax.set_title("Telomere Analysis", fontsize=14, fontweight="bold")
+        ax.set_xlabel("Read (sorted by length, longest to shortest)", fontsize=14, fontweight="bold")
+        ax.set_ylabel("Length (bp)", fontsize=14, fontweight="bold")
+        for side in ("top", "right"):
+            ax.spines[side].set_visible(False)
+        for side in ("left", "bottom"):
+            ax.spines[side].set_linewidth(1.0)
+        ax.tick_params(direction="out", length=5, width=1.0, labelsize=12)
+        ax.grid(False)
+        handles, labels = ax.get_legend_handles_labels()
+        order = [labels.index(n) for n, _, _ in PLOT_SERIES if n in labels]
+        if order:
+            ax.legend([handles[i] for i in order], [labels[i] for i in order], loc="upper center",
+                      bbox_to_anchor=(0.5, -0.14), ncol=3, frameon=False, fontsize=12)
+        fig.tight_layout()
+        fig.savefig(path, dpi=150, format="png")
+    finally:
+        plt.close(fig)
+
+
+def write_analysis(save_path, barcode, rows, columns, format_row, sci_threshold=None, plot_png=True):
+    """Writes <barcode>_filtered_sorted_summary.csv, <barcode>_results.txt and
+    (plot_png) <barcode>_telomere_plot.png; returns the plot rows."""
     filtered, plot = analyze(rows)
     with open(os.path.join(save_path, f"{barcode}_filtered_sorted_summary.csv"), "w", newline="") as f:
         f.write(",".join(list(columns) + ["TelLenMM_RunningMed", "SeqLen_minus_RunMed"]) + "\n")
@@ -109,4 +153,6 @@ def write_analysis(save_path, barcode, rows, columns, format_row, sci_threshold=
     with open(os.path.join(save_path, f"{barcode}_results.txt"), "w") as f:
         for line in results_lines(barcode, filtered):
             f.write(line + "\n")
+    if plot_png:
+        write_telomere_plot(os.path.join(save_path, f"{barcode}_telomere_plot.png"), plot)
     return plot

@@ -64,7 +64,10 @@ def main(argv=None):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dev = a.device if a.device is not None else local
-    if world > 1:
+    # NT_DIST_FORCE=1 (with a launcher): join the process group and run the
+    # collectives even with one rank -- the RCCL path on a one-GPU box
+    grouped = world > 1 or (os.environ.get("NT_DIST_FORCE") == "1" and "WORLD_SIZE" in os.environ)
+    if grouped:
         import torch
         import torch.distributed as dist
         torch.cuda.set_device(dev)
@@ -81,7 +84,7 @@ def main(argv=None):
             sci_threshold=a.readr_sci_threshold, use_filter=a.use_filter,
             analysis=a.analysis, plot=not a.no_plots, plot_jpeg=not a.no_jpeg)
     finally:
-        if world > 1:
+        if grouped:
             import torch.distributed as dist
             dist.destroy_process_group()
     return 0

@@ -344,7 +344,7 @@ def run(input_path, save_path, patterns, fmt="fastq", nrec=10000, rc=False, min_
     world = dist.get_world_size() if dist_on else 1
     # RCCL (backend "nccl") reduces device tensors, gloo host ones: every
     # collective below runs on coll_dev
-    coll_dev = shard.collective_device() if dist_on and world > 1 else None
+    coll_dev = shard.collective_device() if dist_on else None
     os.makedirs(save_path, exist_ok=True)
     reads_dir = os.path.join(save_path, "reads")
     os.makedirs(reads_dir, exist_ok=True)

@@ -18,6 +18,8 @@ So each rank publishes, per chunk it owns, the chunk's largest relative serial
 them, and the serial_starts follow from a sequential scan that reproduces the
 reference's fp64 arithmetic exactly.  Rows then go to rank 0 in chunk order.
 """
+import os
+
 import numpy as np
 
 from .api import assign_serials
@@ -73,6 +75,15 @@ def serial_starts(rel_max):
     return starts
 
 
+def _collective(group=None):
+    """Whether the collectives run: a process group of more than one rank, or
+    of one rank with NT_DIST_FORCE=1 (exercises the RCCL path on one GPU)."""
+    import torch.distributed as dist
+    if not dist.is_initialized():
+        return False
+    return dist.get_world_size(group) > 1 or os.environ.get("NT_DIST_FORCE") == "1"
+
+
 def exchange_rel_max(local, n_chunks, group=None, device=None, failed=False):
     """All ranks' per-chunk relative maxima: local = {chunk: rel_max} for the
     chunks this rank owns.  One all_reduce(MAX) over an n_chunks float64
@@ -86,7 +97,7 @@ def exchange_rel_max(local, n_chunks, group=None, device=None, failed=False):
     for k, v in local.items():
         t[k] = v
     t[n_chunks] = 1.0 if failed else 0.0
-    if dist.is_initialized() and dist.get_world_size(group) > 1:
+    if _collective(group):
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
     a = t.cpu().numpy()
     return a[:n_chunks], bool(a[n_chunks] > 0.0)
@@ -107,7 +118,7 @@ def max_over_ranks(x, group=None, device=None):
     RCCL, see collective_device)."""
     import torch
     import torch.distributed as dist
-    if not (dist.is_initialized() and dist.get_world_size(group) > 1):
+    if not _collective(group):
         return int(x)
     t = torch.tensor([int(x)], dtype=torch.int64, device=device if device is not None else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
@@ -128,7 +139,7 @@ def gather_rows(local_rows, group=None, dst=0):
     """Gather {chunk: rows} from every rank to dst; returns the rows
     concatenated in chunk order on dst (None elsewhere)."""
     import torch.distributed as dist
-    if not (dist.is_initialized() and dist.get_world_size(group) > 1):
+    if not _collective(group):
         return [r for _, rows in sorted(local_rows.items()) for r in rows]
     world = dist.get_world_size(group)
     out = [None] * world if dist.get_rank(group) == dst else None
@@ -145,7 +156,7 @@ def gather_chunks(local, group=None, dst=0):
     """Gather {chunk: value} from every rank to dst; returns the values in
     chunk order on dst (None elsewhere)."""
     import torch.distributed as dist
-    if not (dist.is_initialized() and dist.get_world_size(group) > 1):
+    if not _collective(group):
         return [v for _, v in sorted(local.items())]
     world = dist.get_world_size(group)
     out = [None] * world if dist.get_rank(group) == dst else None

@@ -101,3 +101,22 @@ def test_median_text_types():
     assert analysis.median_text([100000, 100000]) == "1e+05"  # a double: as.character
     assert analysis.median_text([100000]) == "100000"           # an integer
     assert analysis.median_text([]) == "NA"
+
+
+def test_telomere_plot_png(tmp_path):
+    """<barcode>_telomere_plot.png (NanoTel.R:2486-2506): 12 x 6 in at 150 dpi,
+    the three series in their scale_color_manual colours.  Not pixel-identical
+    to ggplot2 (parity unpinned: no R here)."""
+    from PIL import Image
+    rows = [row(i, 20000 - 37 * i, 0.9, 1, 1000 + 13 * (i % 50)) for i in range(1, 200)]
+    plot = analysis.write_analysis(str(tmp_path), "bc", rows, driver.columns(False), driver.format_row)
+    assert len(plot) == 199 and [p[0] for p in plot] == list(range(1, 200))
+    im = Image.open(tmp_path / "bc_telomere_plot.png").convert("RGB")
+    assert im.size == (1800, 900)
+    colours = {c for _, c in im.getcolors(1 << 20)}
+    for _, _, hexc in analysis.PLOT_SERIES:
+        rgb = tuple(int(hexc[i:i + 2], 16) for i in (1, 3, 5))
+        assert rgb in colours, hexc
+    # no rows kept: the empty panel is still written
+    analysis.write_analysis(str(tmp_path), "empty", [], driver.columns(False), driver.format_row)
+    assert Image.open(tmp_path / "empty_telomere_plot.png").size == (1800, 900)

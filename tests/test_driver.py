@@ -131,6 +131,39 @@ def _outputs(out):
     return files
 
 
+def _forced_one_rank(rank, port, inp, out):
+    # a one-rank process group whose collectives run anyway (NT_DIST_FORCE=1):
+    # the path RCCL takes on a one-GPU box (test_gpu_e2e's nccl cases)
+    import torch.distributed as dist
+    from nanotel_amd import driver, shard
+    os.environ["NT_DIST_FORCE"] = "1"
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    calls = []
+    real = dist.all_reduce
+    dist.all_reduce = lambda *a, **k: (calls.append(1), real(*a, **k))[1]
+    try:
+        driver.NanoTel = OracleNanoTel
+        driver.run(inp, out, "TTAGGG", fmt="fasta", nrec=3, log=lambda *a: None)
+    finally:
+        dist.all_reduce = real
+    assert shard._collective() and len(calls) >= 2  # the per-round exchange and the end-of-run flags
+    dist.destroy_process_group()
+
+
+def test_forced_collectives_on_one_rank():
+    import torch.multiprocessing as mp
+    with tempfile.TemporaryDirectory() as d:
+        inp = _make_input(d, False)
+        _rank_main(0, 1, 0, inp, os.path.join(d, "plain"), False)
+        mp.spawn(_forced_one_rank, args=(_free_port(), inp, os.path.join(d, "forced")), nprocs=1, join=True)
+        a, b = _outputs(os.path.join(d, "plain")), _outputs(os.path.join(d, "forced"))
+        for k in ("in_filtered_sorted_summary.csv", "in_results.txt", "in_telomere_plot.png"):
+            a.pop(k, None)
+        assert a == b and len(a["in_summary.csv"].splitlines()) > 5
+
+
 @pytest.mark.parametrize("rc", [False, True])
 def test_sharded_driver_matches_single_process(rc):
     import torch.multiprocessing as mp

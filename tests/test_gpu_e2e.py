@@ -156,3 +156,57 @@ def test_bench_two_ranks(launcher):
     # value = bases of both ranks / the slower rank's time
     assert abs(d["value"] - 2 * 20000 * 10000 * 3 / (d["ms_per_step"] * 3 / 1e3) / 1e9) < 0.01 * d["value"]
 
+
+
+def _port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_cli_rccl_one_rank_matches_plain(tmp_path):
+    """The driver's RCCL path (NT_DIST_BACKEND=nccl: the per-round all_reduce,
+    the held-chunk max and the failure flags on device tensors, the rows by
+    gather_object) on the one GPU of this box: a one-rank RCCL group whose
+    collectives run anyway (NT_DIST_FORCE=1) writes the files of a plain run."""
+    import subprocess
+    import sys
+    inp = _make_input(str(tmp_path), False)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONPATH=os.path.join(root, "telomere-analyzer_amd"), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    args = ["-i", inp, "--format", "fasta", "--patterns", "TTAGGG", "-n", "4", "--device", "0"]
+    one = str(tmp_path / "one")
+    subprocess.run([sys.executable, "-m", "nanotel_amd", "--save_path", one] + args, env=env, check=True,
+                   timeout=120)
+    rccl = str(tmp_path / "rccl")
+    env.update(NT_DIST_BACKEND="nccl", NT_DIST_FORCE="1")
+    subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+                    "--master-addr", "127.0.0.1", "--master-port", str(_port()), "-m", "nanotel_amd",
+                    "--save_path", rccl] + args, env=env, check=True, timeout=180)
+    a, b = _outputs(one), _outputs(rccl)
+    assert a == b and len(a["in_summary.csv"].splitlines()) > 5
+
+
+def test_bench_rccl_one_rank():
+    """bench.py under torch.distributed.run over RCCL (the driver's 1..8-GPU
+    scaling command) with one rank: barrier, max-over-ranks all_reduce on a
+    device tensor, one JSON line."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, NT_BENCH_BACKEND="nccl", NT_DIST_FORCE="1", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(root, "bench.py"),
+           "--gpus", "1", "--steps", "3", "--warmup", "1", "--config", "c10k", "--reads", "20000",
+           "--no-cpu-baseline"]
+    r = subprocess.run(cmd, env=env, check=True, timeout=240, capture_output=True, text=True)
+    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 1 and d["value"] > 0
