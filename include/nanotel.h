@@ -182,6 +182,20 @@ int nt_bundle_layout(nt_ctx* ctx, const nt_batch* batch, uint32_t* tplanes, uint
 /* Asynchronous on the context stream.  max_len = longest read of the batch. */
 int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t max_len);
 
+/* Pipelined batches (device-resident callers streaming batch after batch):
+ * with on != 0 an nt_scan_call that runs the bundle scan in ranges returns
+ * with its last range's calling still running on the library's calling
+ * stream, beside the NEXT nt_scan_call's first scan range (the bundle scan is
+ * bandwidth-bound, the calling latency-bound), instead of making the context
+ * stream wait for it.  A batch's outputs are complete once nt_join (the
+ * context stream waits for every calling launched so far) or nt_synchronize
+ * has run.  Two consecutive calls must not share output buffers (the
+ * library's own aux buffers alternate).  Turning it off joins.  The
+ * reference processes its chunks one after another (NanoTel.R:2171-2268);
+ * this only overlaps the device work of consecutive ones. */
+int nt_set_pipelined(nt_ctx* ctx, int on);
+int nt_join(nt_ctx* ctx);
+
 /* Measurement: with profiling on, every nt_scan_call records HIP events on
  * the context stream around its scan kernel(s) and its calling kernel.
  * nt_kernel_times waits for them and returns the summed spans of the calls

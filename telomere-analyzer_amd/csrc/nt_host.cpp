@@ -155,6 +155,13 @@ struct nt_ctx {
   bool lds_limit_set = false;
   hipStream_t call_stream = nullptr;  // sub-batched calling kernels (NT_SUBBATCH > 1)
   hipEvent_t ev_scan = nullptr, ev_call = nullptr;
+  // pipelined batches (nt_set_pipelined): a call leaves its last range's
+  // calling on call_stream, beside the next call's first scan range; calls
+  // alternate between two aux buffers (tmask / tmask_alt), and call i waits
+  // for the calling of call i - 2 (ev_done[i % 2]) before its scan writes
+  bool pipelined = false;
+  uint64_t pipe_i = 0;
+  hipEvent_t ev_done[2] = {nullptr, nullptr};
   bool profile = false;  // HIP events around the scan and call kernels of every call
   // per recorded call: [0] start, [1] end of the scans (serial calling), [2]
   // end, [3 + 2k], [4 + 2k] around bundle-scan range k (overlapped calling)
@@ -183,6 +190,7 @@ struct nt_ctx {
   int cu_count = 256;
   DevBuf planes, blk_off, len, win_off, exc_off, exc_pos, exc_code;
   DevBuf wc, start, end, dens, flags, hits, scratch, tmask, thr, queue;
+  DevBuf tmask_alt;  // the odd calls' aux buffer in pipelined mode
   DevBuf tplanes, bnd_read, bnd_stripe, list;  // upload_reads' bundle layout
   HostBuf h_planes, h_meta, h_tplanes;  // upload_reads staging
   // host-path phase times (s, cumulative; nt_host_times): layout, pack,
@@ -315,6 +323,8 @@ void nt_destroy(nt_ctx* ctx) {
   if (ctx->prog_dev) (void)hipFree(ctx->prog_dev);
   if (ctx->ev_scan) (void)hipEventDestroy(ctx->ev_scan);
   if (ctx->ev_call) (void)hipEventDestroy(ctx->ev_call);
+  for (hipEvent_t x : ctx->ev_done)
+    if (x) (void)hipEventDestroy(x);
   if (ctx->call_stream) (void)hipStreamDestroy(ctx->call_stream);
   for (auto& a : ctx->ev)
     for (hipEvent_t ev : a) (void)hipEventDestroy(ev);
@@ -330,8 +340,33 @@ int nt_set_stream(nt_ctx* ctx, void* hip_stream) {
   return NT_OK;
 }
 
+// the context stream waits for everything on the calling stream (pipelined
+// batches' last callings)
+int nt_join(nt_ctx* ctx) {
+  if (!ctx) return NT_E_ARG;
+  if (!ctx->call_stream) return NT_OK;
+  (void)hipSetDevice(ctx->device);
+  hipError_t e;
+  if ((e = hipEventRecord(ctx->ev_call, ctx->call_stream)) != hipSuccess ||
+      (e = hipStreamWaitEvent(ctx->stream, ctx->ev_call, 0)) != hipSuccess)
+    return hip_fail(ctx, e, "nt_join");
+  return NT_OK;
+}
+
+int nt_set_pipelined(nt_ctx* ctx, int on) {
+  if (!ctx) return NT_E_ARG;
+  if (ctx->pipelined && !on) {
+    const int rc = nt_join(ctx);
+    if (rc) return rc;
+  }
+  ctx->pipelined = on != 0;
+  return NT_OK;
+}
+
 int nt_synchronize(nt_ctx* ctx) {
   if (!ctx) return NT_E_ARG;
+  const int rc = nt_join(ctx);
+  if (rc) return rc;
   hipError_t e = hipStreamSynchronize(ctx->stream);
   return e == hipSuccess ? NT_OK : hip_fail(ctx, e, "hipStreamSynchronize");
 }
@@ -433,8 +468,11 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
     ctx->lds_limit_set = true;
   }
   const uint64_t tmw = nt_dev_tmask_words(batch->n_windows, batch->n_reads, np);
-  if ((e = ctx->tmask.ensure(tmw * 8)) != hipSuccess) return hip_fail(ctx, e, "hipMalloc(tmask)");
-  uint64_t* tmask = (uint64_t*)ctx->tmask.p;
+  // pipelined: the odd calls use the second aux buffer (the previous call's
+  // calling may still read the other one)
+  DevBuf& tmb = (ctx->pipelined && (ctx->pipe_i & 1)) ? ctx->tmask_alt : ctx->tmask;
+  if ((e = tmb.ensure(tmw * 8)) != hipSuccess) return hip_fail(ctx, e, "hipMalloc(tmask)");
+  uint64_t* tmask = (uint64_t*)tmb.p;
   // debugging: NT_DBG_POISON_AUX=<byte> fills the aux buffer first (every word read must be written)
   if (const char* v = std::getenv("NT_DBG_POISON_AUX"))
     (void)hipMemsetAsync(tmask, std::atoi(v) & 255, tmw * 8, ctx->stream);
@@ -495,7 +533,18 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
     if ((e = hipEventCreateWithFlags(&ctx->ev_scan, hipEventDisableTiming)) != hipSuccess ||
         (e = hipEventCreateWithFlags(&ctx->ev_call, hipEventDisableTiming)) != hipSuccess)
       return hip_fail(ctx, e, "hipEventCreate");
+    for (hipEvent_t& x : ctx->ev_done) {
+      if ((e = hipEventCreateWithFlags(&x, hipEventDisableTiming)) != hipSuccess ||
+          (e = hipEventRecord(x, ctx->call_stream)) != hipSuccess)
+        return hip_fail(ctx, e, "hipEventCreate");
+    }
   }
+  // pipelined: this call's scans overwrite the aux buffer that the calling of
+  // call pipe_i - 2 read
+  const bool piped = ctx->pipelined && (nsub > 1 || tsub > 1);
+  if (ctx->pipelined && ctx->ev_done[0] &&
+      (e = hipStreamWaitEvent(ctx->stream, ctx->ev_done[ctx->pipe_i & 1], 0)) != hipSuccess)
+    return hip_fail(ctx, e, "stream dependency");
   // read queues: two per sub-batch (LDS and global-scratch launches) and one
   // per bundle range, zeroed on the stream
   const uint64_t nqueue = 2 * nsub + tsub;
@@ -679,10 +728,15 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
   }
   if (nsub > 1 || tsub > 1) {
     if (ev) (void)hipEventRecord(ev[1], ctx->stream);  // end of the last scan
-    if ((e = hipEventRecord(ctx->ev_call, ctx->call_stream)) != hipSuccess ||
-        (e = hipStreamWaitEvent(ctx->stream, ctx->ev_call, 0)) != hipSuccess)
+    if (piped) {  // the last calling stays in flight (nt_join)
+      if ((e = hipEventRecord(ctx->ev_done[ctx->pipe_i & 1], ctx->call_stream)) != hipSuccess)
+        return hip_fail(ctx, e, "hipEventRecord");
+    } else if ((e = hipEventRecord(ctx->ev_call, ctx->call_stream)) != hipSuccess ||
+               (e = hipStreamWaitEvent(ctx->stream, ctx->ev_call, 0)) != hipSuccess) {
       return hip_fail(ctx, e, "stream join");
+    }
   }
+  if (ctx->pipelined) ++ctx->pipe_i;
   if (ev) (void)hipEventRecord(ev[2], ctx->stream);
   return NT_OK;
 }
@@ -1016,6 +1070,7 @@ int nt_analyze_host(nt_ctx* ctx, const char* const* seqs, const uint64_t* lens, 
   double t0 = now_s();
   rc = nt_scan_call(ctx, &B, &O, ml);
   if (rc) return rc;
+  if (ctx->pipelined && (rc = nt_join(ctx)) != NT_OK) return rc;  // the rows are read back below
   std::vector<uint8_t> h_flags(n_reads);
 #define NT_DOWN(dst, buf, bytes)                                                              \
   e = hipMemcpyAsync(dst, ctx->buf.p, bytes, hipMemcpyDeviceToHost, ctx->stream);            \

@@ -86,6 +86,8 @@ SIGNATURES = {
     "nt_last_error": (ctypes.c_char_p, [_P]),
     "nt_set_stream": (ctypes.c_int, [_P, _P]),
     "nt_synchronize": (ctypes.c_int, [_P]),
+    "nt_set_pipelined": (ctypes.c_int, [_P, ctypes.c_int]),
+    "nt_join": (ctypes.c_int, [_P]),
     "nt_compile": (ctypes.c_int, [_P, ctypes.POINTER(NtParams), ctypes.POINTER(NtProgramInfo)]),
     "nt_window_count": (ctypes.c_int64, [ctypes.c_int64, ctypes.c_int32]),
     "nt_window_rows": (ctypes.c_uint64, [ctypes.c_int64]),

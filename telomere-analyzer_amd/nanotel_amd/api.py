@@ -130,6 +130,17 @@ class NanoTel:
     def synchronize(self):
         _check(lib().nt_synchronize(self._h), self._h)
 
+    def set_pipelined(self, on=True):
+        """nt_set_pipelined: a scan_call() returns with its last bundle range's
+        calling still running beside the next call's scan; outputs are
+        complete after join() / synchronize().  Consecutive calls need their
+        own output buffers."""
+        _check(lib().nt_set_pipelined(self._h, int(bool(on))), self._h)
+
+    def join(self):
+        """nt_join: the launch stream waits for every calling launched so far."""
+        _check(lib().nt_join(self._h), self._h)
+
     # ------------------------------------------------------------------
     def analyze(self, seqs, want_windows=False, want_hits=False):
         """Scan + call every read of a chunk (host buffers in, host arrays out).

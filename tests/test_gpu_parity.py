@@ -512,6 +512,55 @@ def test_device_bundle_scan_matches_per_read_scan(read_len):
     compare(nt, res, oracle_rows(seqs, "TTAGGG"), check_windows=False, check_hits=False)
 
 
+def test_pipelined_batches_match_serial():
+    """nt_set_pipelined: each call's last bundle range's calling runs beside the
+    next call's scan (the bench's stream of batches).  Four calls over three
+    different device batches, each with its own outputs, equal the serial
+    calls' outputs bit for bit (the library's aux buffers alternate; a shared
+    one would be overwritten under the running calling)."""
+    import torch
+    from nanotel_amd import synth_params
+    n, read_len = 8192, 10000  # 256 bundles: two bundle ranges
+    nt = _nt(patterns="TTAGGG")
+    assert nt.tscan
+    batches = []
+    for first in (0, 70000, 140000):
+        t = _device_batch(nt, synth_params(read_len=read_len, first_read=first), n, read_len, hits=False)
+        b, keep = _device_bundles(nt, t, n, read_len)
+        batches.append((t, b, keep))
+    keys = ("start", "end", "dens", "flags", "wc")
+
+    def run(t, b, o):
+        nt.scan_call_device(t["planes"].data_ptr(), t["blk_off"].data_ptr(), t["lens"].data_ptr(),
+                            t["win_off"].data_ptr(), n, n * t["rows"], read_len, o["start"].data_ptr(),
+                            o["end"].data_ptr(), o["dens"].data_ptr(), o["flags"].data_ptr(), o["wc"].data_ptr(),
+                            bundles=b)
+
+    refs = []
+    for t, b, _ in batches:
+        o = {k: torch.full_like(t[k], 0x55) for k in keys}
+        run(t, b, o)
+        nt.synchronize()
+        refs.append(o)
+    order = [0, 1, 2, 0]
+    outs = [{k: torch.full_like(batches[i][0][k], 0x55) for k in keys} for i in order]
+    nt.set_pipelined(True)
+    for i, o in zip(order, outs):
+        run(batches[i][0], batches[i][1], o)
+    nt.join()
+    nt.synchronize()
+    nt.set_pipelined(False)
+    for i, o in zip(order, outs):
+        t, r = batches[i][0], refs[i]
+        for k in keys:
+            if k == "wc":
+                assert torch.equal(_valid_counts(t, n, nt.n_pass, o[k]), _valid_counts(t, n, nt.n_pass, r[k])), (i, k)
+            else:
+                assert torch.equal(o[k], r[k]), (i, k)
+    assert int((refs[0]["flags"] & 1).sum()) > 1000  # telomeric reads: the calling did work
+    nt.close()
+
+
 @pytest.mark.parametrize("tvr", [None, "TGAGGG TTGGGG"], ids=["p2", "p3"])
 def test_bundle_ranges_with_mixed_lengths_and_exceptions(tvr):
     # enough bundles for the two bundle-scan ranges (calling beside the scan),

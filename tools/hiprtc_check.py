@@ -30,8 +30,9 @@ def tscan_source(pats, tvrs="", L="100"):
 extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
 nt_tscan_jit(NtBatch B, NtOut O, uint64_t* __restrict__ tmask, unsigned long long* __restrict__ queue,
              uint32_t thr_full) {
-  __shared__ uint32_t tsl[4 * nt::kTsLdsWords];
-  nt::tscan_bundles<TJit, TPats, TTvrs>(B, O, tmask, queue, thr_full, tsl + (threadIdx.x >> 6) * nt::kTsLdsWords);
+  constexpr int kW = nt::ts_lds_words<TJit::kNP>();
+  __shared__ uint32_t tsl[4 * kW];
+  nt::tscan_bundles<TJit, TPats, TTvrs>(B, O, tmask, queue, thr_full, tsl + (threadIdx.x >> 6) * kW);
 }
 """
     return src

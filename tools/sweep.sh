@@ -1,10 +1,15 @@
 #!/bin/bash
 # Bench sweep over environment knobs: [BENCH_ARGS=..] tools/sweep.sh "ENV=.. ENV=.." ...
+# one log per spec (gpurun_out/sw_<i>.log), a summary line per spec on stdout
 set -u
+mkdir -p gpurun_out
+i=0
 for spec in "$@"; do
-  echo "=== $spec"
-  env $spec timeout -k 10 300 python bench.py --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/sweep.log 2>&1
+  i=$((i + 1))
+  log=gpurun_out/sw_$i.log
+  echo "=== [$i] $spec"
+  env $spec timeout -k 10 300 python bench.py --no-cpu-baseline ${BENCH_ARGS:-} > $log 2>&1
   st=$?
-  python3 -c "import json; d=json.loads(open('gpurun_out/sweep.log').read().strip().splitlines()[-1]); r=d['roofline']; print('value', d['value'], 'ms', d['ms_per_step'], 'scan', r['kernel_avg_ms'], 'call', r['call_kernel_avg_ms'])" || tail -3 gpurun_out/sweep.log
-  if [ $st -eq 124 ] || [ $st -gt 128 ]; then break; fi
+  python3 -c "import json; d=json.loads(open('$log').read().strip().splitlines()[-1]); r=d['roofline']; print('value', d['value'], 'ms', d['ms_per_step'], 'scan', r['kernel_avg_ms'], 'call', r['call_kernel_avg_ms'])" || tail -3 $log
+  if [ $st -eq 124 ] || [ $st -gt 128 ]; then echo "status $st: stopping"; break; fi
 done

@@ -11,11 +11,12 @@ cat > "$out/t.hip" <<EOT
 using PatL = nt::CtList<$pats>;
 using TvrL = nt::CtList<$tvrs>;
 using JitT = nt::TProg<PatL, TvrL, $L>;
-extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(${WAVES:-4})))
+extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(${WAVES:-2})))
 nt_tscan_jit(NtBatch B, NtOut O, uint64_t* __restrict__ tmask,
              unsigned long long* __restrict__ queue, uint32_t thr_full) {
-  __shared__ uint32_t tsl[4 * nt::kTsLdsWords];
-  nt::tscan_bundles<JitT, PatL, TvrL>(B, O, tmask, queue, thr_full, tsl + (threadIdx.x >> 6) * nt::kTsLdsWords);
+  constexpr int kW = nt::ts_lds_words<JitT::kNP>();
+  __shared__ uint32_t tsl[4 * kW];
+  nt::tscan_bundles<JitT, PatL, TvrL>(B, O, tmask, queue, thr_full, tsl + (threadIdx.x >> 6) * kW);
 }
 EOT
 cd "$out"
