@@ -238,21 +238,45 @@ def main():
     bundles, keep = None, []
     scan_path = "per-read"
     plan = None
+    cap_note = None
+    # device memory: the planes, outputs and the library's aux buffer (8 np
+    # (rows/64 + 2) u64 a read, allocated at the first call) are resident; the
+    # bundle layout is a second copy of the reads (the calling kernel reads the
+    # per-read planes).  When both copies do not fit, the bundle scan takes the
+    # reads whose layout fits and the rest stay with the per-read scan (marked
+    # for it in the plan, as reads with non-ACGT letters are); pipelining needs
+    # a second output set and aux buffer.
+    margin = 4 << 30
+    aux_bytes = 64 * npass * (rows // 64 + 2) * n
+    out_bytes = sum(x.numel() * x.element_size() for x in (start, end, dens, flags, wc))
+    want_pipe = not args.no_pipeline
     if nt.tscan and not args.per_read:
         import numpy as np
-        plan = nt.bundle_plan(np.full(n, L, np.uint32))
-        # the bundle layout is a second copy of the reads (the calling kernel
-        # reads the per-read planes): when both do not fit, the per-read scan
+        lens_h = np.full(n, L, np.uint32)
+        plan = nt.bundle_plan(lens_h)
         free, _ = torch.cuda.mem_get_info(dev)
-        if plan.tplane_bytes + (4 << 30) > free:
-            plan = None
-            scan_path = "per-read (bundle layout does not fit beside the planes)"
+        if plan.tplane_bytes + aux_bytes + margin > free:
+            per = plan.tplane_bytes / max(1, n)
+            k = int((free - aux_bytes - margin) / per) // 32 * 32 if free > aux_bytes + margin else 0
+            if k >= 32 * 128:  # at least two bundle ranges' worth
+                has_exc = np.zeros(n, np.uint8)
+                has_exc[k:] = 1
+                plan = nt.bundle_plan(lens_h, has_exc)
+                cap_note = (f"bundle layout for {k} of {n} reads (planes + layout beside the outputs fill "
+                            f"the GPU); the other {n - k} on the per-read scan")
+            else:
+                plan = None
+                scan_path = "per-read (bundle layout does not fit beside the planes)"
+        if plan is not None:
+            want_pipe = want_pipe and plan.tplane_bytes + 2 * aux_bytes + out_bytes + margin <= free
     if plan is not None and plan.n_bundles == 0:
         plan = None
     if plan is not None:
         from nanotel_amd.api import DeviceBundles
         import numpy as np
         scan_path = "bundle" if len(plan.list) == 0 else f"bundle + per-read ({len(plan.list)} reads)"
+        if cap_note:
+            scan_path += "; " + cap_note
         bread = torch.from_numpy(plan.bnd_read.view(np.int32)).to(dev)
         bstripe = torch.from_numpy(plan.bnd_stripe.view(np.int64)).to(dev)
         tpl = torch.empty(max(1, plan.tplane_bytes // 4), dtype=torch.int32, device=dev)
@@ -270,7 +294,7 @@ def main():
     # a stream of resident batches runs; consecutive steps write alternate
     # output sets, and the timed region ends after nt_join (every step's rows
     # complete).  --no-pipeline: each step waits for its own calling.
-    pipelined = bundles is not None and not args.no_pipeline
+    pipelined = bundles is not None and want_pipe
     outs = [(start, end, dens, flags, wc)]
     if pipelined:
         outs.append(tuple(torch.empty_like(x) for x in outs[0]))

@@ -158,9 +158,12 @@ int nt_pack_reads(const char* const* seqs, const uint64_t* lens, uint64_t n_read
 
 /* --- bundle layout (the bundle scan's copy of the reads) ------------------- */
 /* Host: group the reads of a batch 32 to a bundle (longest first; the compiled
- * program fixes the block size L).  has_exc (NULL = none) marks reads with
- * non-ACGT letters, which stay outside the bundles, as do reads of any
- * program the bundle scan does not cover (then *n_bundles = 0).  Outputs:
+ * program fixes the block size L).  has_exc (NULL = none) marks reads that
+ * stay outside the bundles and go to the per-read scan: reads with non-ACGT
+ * letters (nt_pack_reads' exception lists), or any the caller leaves there
+ * (e.g. to bound the T-layout's memory when a batch's planes and its layout
+ * do not both fit); so do the reads of any program the bundle scan does not
+ * cover (then *n_bundles = 0).  Outputs:
  * bnd_read [ceil(n/32)*32], bnd_stripe [ceil(n/32)+1], list [n] (the reads
  * left out, in order), and the bytes of the T-layout buffer. */
 int nt_bundle_plan(nt_ctx* ctx, const uint32_t* len, const uint8_t* has_exc, uint64_t n_reads,
