@@ -462,16 +462,20 @@ def test_device_resident_path_matches_host_path(jit):
     compare(nt, res, oracle_rows(seqs[:6], "TTAGGG"))
 
 
-def _device_bundles(nt, t, n, read_len):
-    """The bench's bundle layout of a device batch (host plan, device transpose)."""
+def _device_bundles(nt, t, n, read_len, has_exc=None):
+    """The bench's bundle layout of a device batch (host plan, device transpose);
+    has_exc: reads left to the per-read scan (their list goes with the bundles)."""
     import torch
     from nanotel_amd.api import DeviceBundles
-    plan = nt.bundle_plan(np.full(n, read_len, np.uint32))
+    plan = nt.bundle_plan(np.full(n, read_len, np.uint32), has_exc)
     d = dict(bnd_read=torch.from_numpy(plan.bnd_read.view(np.int32)).cuda(),
              bnd_stripe=torch.from_numpy(plan.bnd_stripe.view(np.int64)).cuda(),
              tplanes=torch.empty(max(1, plan.tplane_bytes // 4), dtype=torch.int32, device="cuda"))
+    nl = len(plan.list)
+    if nl:
+        d["list"] = torch.from_numpy(plan.list.view(np.int32)).cuda()
     b = DeviceBundles(d["tplanes"].data_ptr(), d["bnd_read"].data_ptr(), d["bnd_stripe"].data_ptr(),
-                      plan.n_bundles, 0, 0, plan.tplane_bytes)
+                      plan.n_bundles, d["list"].data_ptr() if nl else 0, nl, plan.tplane_bytes)
     nt.bundle_layout_device(t["planes"].data_ptr(), t["blk_off"].data_ptr(), t["lens"].data_ptr(),
                             t["win_off"].data_ptr(), n, n * t["rows"], b)
     nt.synchronize()
@@ -683,6 +687,9 @@ FULL_CONFIGS = {  # patterns, TVRs, reads, variant rate, bundle path, read lengt
     "c3": ("YYAGGG", None, 10_000_000, 0.05, True, 50_000),
     "c4": ("TTAGGG TCAGGG", "TGAGGG TTGGGG", 10_000_000, 0.05, True, 50_000),
     "c5_shard": ("TTAGGG", None, 12_500_000, 0.0, False, 50_000),
+    # the shard as bench.py runs it: the bundle copy for the reads whose copy fits
+    # beside the planes, the rest marked for the per-read scan (has_exc)
+    "c5_capped": ("TTAGGG", None, 12_500_000, 0.0, "capped", 50_000),
     "c10k": ("TTAGGG", None, 1_000_000, 0.0, True, 10_000),
 }
 
@@ -697,7 +704,19 @@ def test_full_size_config_sampled_vs_oracle(name):
     sp = synth_params(read_len=read_len, first_read=0, variant_rate=var)
     t = _device_batch(nt, sp, n, read_len, hits=False)
     b = keep = None
-    if bundle:
+    extra = np.zeros(0, np.int64)
+    if bundle == "capped":
+        torch.cuda.empty_cache()
+        free = torch.cuda.mem_get_info()[0]
+        aux = 64 * nt.n_pass * (t["rows"] // 64 + 2) * n
+        per = nt.bundle_plan(np.full(n, read_len, np.uint32)).tplane_bytes / n
+        k = int((free - aux - (4 << 30)) / per) // 32 * 32
+        assert 32 * 128 <= k < n, k
+        has_exc = np.zeros(n, np.uint8)
+        has_exc[k:] = 1
+        b, keep = _device_bundles(nt, t, n, read_len, has_exc)
+        extra = np.arange(k - 64, k + 64)  # both sides of the bundled / per-read boundary
+    elif bundle:
         b, keep = _device_bundles(nt, t, n, read_len)
     nt.scan_call_device(t["planes"].data_ptr(), t["blk_off"].data_ptr(), t["lens"].data_ptr(),
                         t["win_off"].data_ptr(), n, n * t["rows"], read_len, t["start"].data_ptr(),
@@ -709,7 +728,7 @@ def test_full_size_config_sampled_vs_oracle(name):
     n_telo = int(((flags & 1) != 0).sum())
     # the sample: 256 first, 384 last (12 bundles), 1400 spread over the batch
     idx = np.unique(np.concatenate([np.arange(256), np.arange(n - 384, n),
-                                    np.linspace(256, n - 385, 1400).astype(np.int64)]))
+                                    np.linspace(256, n - 385, 1400).astype(np.int64), extra]))
     it = torch.from_numpy(idx).cuda()
     res = {"start": t["start"].view(n, 3)[it].cpu().numpy(), "end": t["end"].view(n, 3)[it].cpu().numpy(),
            "density": t["dens"].view(n, 3)[it].cpu().numpy(), "flags": flags[it].cpu().numpy()}
