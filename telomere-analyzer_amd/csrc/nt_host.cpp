@@ -521,7 +521,8 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
   }
   int bpc_cap = 0;
   if (const char* v = std::getenv("NT_SCAN_WAVES")) bpc_cap = std::atoi(v);
-  if ((nsub > 1 || tsub > 1) && !ctx->call_stream) {
+  const bool piped = ctx->pipelined && (nsub > 1 || tsub > 1 || tscan);
+  if ((nsub > 1 || tsub > 1 || piped) && !ctx->call_stream) {
     int prio = 0;  // NT_CALL_PRIO (tuning): the calling stream's priority, clamped to the device's range
     if (const char* v = std::getenv("NT_CALL_PRIO")) {
       int lo = 0, hi = 0;
@@ -541,7 +542,6 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
   }
   // pipelined: this call's scans overwrite the aux buffer that the calling of
   // call pipe_i - 2 read
-  const bool piped = ctx->pipelined && (nsub > 1 || tsub > 1);
   if (ctx->pipelined && ctx->ev_done[0] &&
       (e = hipStreamWaitEvent(ctx->stream, ctx->ev_done[ctx->pipe_i & 1], 0)) != hipSuccess)
     return hip_fail(ctx, e, "stream dependency");
@@ -617,7 +617,7 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
       Bc.list = Bt.bnd_read;
       Bc.n_list = NT_BUNDLE * Bt.n_bundles;
       hipStream_t cs = ctx->stream;
-      if (tsub > 1) {
+      if (tsub > 1 || piped) {
         if ((e = hipEventRecord(ctx->ev_scan, ctx->stream)) != hipSuccess ||
             (e = hipStreamWaitEvent(ctx->call_stream, ctx->ev_scan, 0)) != hipSuccess)
           return hip_fail(ctx, e, "stream dependency");
@@ -726,7 +726,7 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
     }
     if (e != hipSuccess) return hip_fail(ctx, e, "launch nt_call_kernel");
   }
-  if (nsub > 1 || tsub > 1) {
+  if (nsub > 1 || tsub > 1 || piped) {
     if (ev) (void)hipEventRecord(ev[1], ctx->stream);  // end of the last scan
     if (piped) {  // the last calling stays in flight (nt_join)
       if ((e = hipEventRecord(ctx->ev_done[ctx->pipe_i & 1], ctx->call_stream)) != hipSuccess)
