@@ -513,7 +513,10 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
   uint64_t tsub = 1;
   if (tscan) {
     nsub = 1;
-    uint64_t per = 16384;
+    // pipelined, the last range's calling is hidden behind the next batch's
+    // scan anyway: fewer, larger ranges (fewer range tails; same box, c10k
+    // +1.4 %, c4 +1.5 %, c3 10 M +0.6 %)
+    uint64_t per = ctx->pipelined ? 32768 : 16384;
     if (const char* v = std::getenv("NT_TSUB_BUNDLES")) per = std::max<uint64_t>(1, std::strtoull(v, nullptr, 10));
     tsub = std::max<uint64_t>(2, (batch->n_bundles + per - 1) / per);
     if (const char* v = std::getenv("NT_TSUB")) tsub = std::max<uint64_t>(1, std::strtoull(v, nullptr, 10));
