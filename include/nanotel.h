@@ -325,6 +325,35 @@ int64_t nt_reader_skip(nt_reader* r, uint64_t nrec, const uint64_t** seq_lens);
  * call holds them all.  Only grows. */
 int nt_reader_keep(nt_reader* r, uint32_t chunks);
 
+/* --- sharded ingest (one process per GPU; replaces every R worker reading the
+ * whole chunk stream, NanoTel.R:2207-2254): each rank finds the chunk starts
+ * from 1/N of the input and reads only its own chunks.  Chunk k is still
+ * records [k nrec, (k+1) nrec) of the whole stream (A15 unchanged).
+ * nt_reader_layout: file sizes and offsets in the concatenated stream;
+ *   *all_plain = no file is gzip (then byte ranges shard it).
+ * nt_reader_shard_range: the records that START in bytes [a, b) of the
+ *   concatenated plain files (resynchronised at a FASTA '>' line / a FASTQ '@'
+ *   line whose second next line starts with '+'); returns their count, with
+ *   *first = the first record start parsed (>= a) and *next = the first start
+ *   >= b (the total size at the end).  A caller checks first(rank r) ==
+ *   next(rank r - 1): a mismatch means a false resynchronisation.
+ * nt_reader_shard_positions: their global byte offsets (valid until the next call).
+ * nt_reader_count_files: the record count of each listed file (whole files,
+ *   on host threads; gzip parts of a run directory).
+ * nt_reader_plan: before the first read -- the files this reader will visit,
+ *   ascending (the inflate-ahead workers take only these).
+ * nt_reader_seek: mode 0 = to byte a of the concatenated plain files (a record
+ *   start); mode 1 = to record b of file a.  Seeks go forward in the plan.
+ * nt_reader_stats: out[0] = bytes parsed (records read or skipped, index
+ *   passes included), out[1] = bytes inflated. */
+int nt_reader_layout(nt_reader* r, int* all_plain, uint64_t* total_bytes);
+int64_t nt_reader_shard_range(nt_reader* r, uint64_t a, uint64_t b, uint64_t* first, uint64_t* next);
+int64_t nt_reader_shard_positions(const nt_reader* r, const uint64_t** pos);
+int nt_reader_count_files(nt_reader* r, const uint64_t* files, uint64_t n, uint64_t* counts);
+int nt_reader_plan(nt_reader* r, const uint64_t* files, uint64_t n);
+int nt_reader_seek(nt_reader* r, int mode, uint64_t a, uint64_t b);
+int nt_reader_stats(const nt_reader* r, uint64_t* out2);
+
 /* --- synthetic long reads (bench / tests) --------------------------------- */
 int nt_synth_device(nt_ctx* ctx, const nt_synth_params* sp, uint64_t n_reads, uint32_t* planes_dev);
 int nt_uniform_layout_device(nt_ctx* ctx, uint64_t n_reads, uint64_t read_len, int32_t subseq_length,

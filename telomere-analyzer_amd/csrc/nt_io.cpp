@@ -56,17 +56,19 @@ struct Prefetcher {
     std::string err;
     std::vector<char> data;
   };
+  std::vector<std::string> files_;  // the files in the order the parser takes them (the reader's plan)
   const std::vector<std::string>* files = nullptr;
   std::vector<Slot> slots;
-  size_t next = 0, consumed = 0, window = 1;
+  size_t next = 0, consumed = 0, window = 1, freed = 0;
   bool stop = false;
   std::mutex mu;
   std::condition_variable cv;
   std::vector<std::thread> workers;
 
-  void start(const std::vector<std::string>& f, unsigned n_threads) {
-    files = &f;
-    slots.resize(f.size());
+  void start(std::vector<std::string> f, unsigned n_threads) {
+    files_ = std::move(f);
+    files = &files_;
+    slots.resize(files_.size());
     window = n_threads;
     for (unsigned t = 0; t < n_threads; ++t) workers.emplace_back([this] { run(); });
   }
@@ -117,6 +119,7 @@ struct Prefetcher {
   bool take(size_t i, std::vector<char>& out, bool& plain, std::string& err) {
     std::unique_lock<std::mutex> lk(mu);
     consumed = i + 1;
+    for (; freed < i; ++freed) std::vector<char>().swap(slots[freed].data);  // passed over by a seek
     cv.notify_all();
     cv.wait(lk, [&] { return slots[i].done; });
     if (!slots[i].err.empty()) {
@@ -156,8 +159,22 @@ struct RBuf {
 
 struct nt_reader {
   std::vector<std::string> files;
-  size_t file_idx = 0;  // next file to open
+  // the files in the order they are read: all of them, or the plan of a rank
+  // of a sharded run (nt_reader_plan: only the files its chunks touch)
+  std::vector<uint64_t> order;
+  size_t file_idx = 0;  // next position in `order` to open
+  uint64_t cur_file = ~0ull;  // the open file (index into files)
+  uint64_t rec_in_file = 0;   // records parsed in it so far
   int format = 0;       // 0 fasta, 1 fastq
+  unsigned pf_threads = 0;  // gzip parts inflated ahead (multi-file input), started at the first open
+  bool started = false;
+  // sharded ingest: plain files' sizes and offsets in the concatenated stream,
+  // the record starts of this rank's byte range (nt_reader_shard_range)
+  std::vector<uint64_t> fsize, fbase;
+  std::vector<uint64_t> shard_pos;
+  // bytes the parser walked over (records, kept or skipped) and bytes inflated
+  uint64_t bytes_parsed = 0, bytes_inflated = 0;
+  size_t rec_at = 0;  // header offset (in the window) of the last record parsed
   // the current file's bytes: a mapping of the whole plain file, a whole gzip
   // part inflated ahead (Prefetcher), or windows of a gzip stream (serial inflate)
   gzFile gz = nullptr;
@@ -301,7 +318,7 @@ bool more(nt_reader* r) {
   while (got < cap) {
     const int n = gzread(r->gz, nb->own.data() + got, (unsigned)std::min<size_t>(cap - got, 1u << 30));
     if (n < 0 || (n == 0 && gz_failed(r->gz))) {  // corrupt or truncated gzip stream
-      r->err = "read error in " + r->files[r->file_idx - 1];
+      r->err = "read error in " + r->files[r->cur_file];
       r->src_eof = true;
       return false;
     }
@@ -311,6 +328,7 @@ bool more(nt_reader* r) {
     }
     got += (size_t)n;
   }
+  r->bytes_inflated += got - keep;
   nb->data = nb->own.data();
   nb->size = got;
   for (size_t i = r->nl_i; i < r->nl.size(); ++i) r->nl[i] -= r->pos;
@@ -321,19 +339,37 @@ bool more(nt_reader* r) {
   return got > keep;
 }
 
+// The reader's first open: the inflate-ahead workers of a multi-file input
+// start on the files of the plan (all files unless nt_reader_plan named some).
+void start(nt_reader* r) {
+  if (r->started) return;
+  r->started = true;
+  if (r->pf_threads > 0 && r->order.size() > 1) {
+    std::vector<std::string> paths;
+    for (uint64_t f : r->order) paths.push_back(r->files[f]);
+    r->pf.reset(new Prefetcher());
+    r->pf->start(std::move(paths), r->pf_threads);
+  }
+}
+
 bool open_next(nt_reader* r) {
   close_source(r);
   r->win.reset();
   r->pos = r->end = r->scan = 0;
   r->nl.clear();
   r->nl_i = 0;
-  if (!r->err.empty() || r->file_idx >= r->files.size()) return false;
-  const std::string& path = r->files[r->file_idx++];
+  r->cur_file = ~0ull;
+  r->rec_in_file = 0;
+  start(r);
+  if (!r->err.empty() || r->file_idx >= r->order.size()) return false;
+  r->cur_file = r->order[r->file_idx++];
+  const std::string& path = r->files[r->cur_file];
   auto b = std::make_shared<RBuf>();
   if (r->pf) {  // a gzip part inflated ahead by the workers: parse straight from memory
     bool plain = false;
     if (!r->pf->take(r->file_idx - 1, b->own, plain, r->err)) return false;
     if (!plain) {
+      r->bytes_inflated += b->own.size();
       b->data = b->own.data();
       b->size = b->own.size();
       r->win = b;
@@ -416,6 +452,16 @@ bool next_line(const nt_reader* r, Cur& c, size_t& ls, size_t& le, bool& need) {
   return true;
 }
 
+// A record was parsed: the cursor moves past it (rec_at = its header line's
+// offset in the window; the bytes walked over count as parsed).
+void commit(nt_reader* r, const Cur& c, size_t hdr) {
+  r->bytes_parsed += c.p - r->pos;
+  r->pos = c.p;
+  r->nl_i = c.i;
+  r->rec_at = hdr;
+  ++r->rec_in_file;
+}
+
 // One record from the window at the committed cursor, appended to the chunk
 // store (or, when lens_only, its sequence length only).  Returns 1 = a
 // record, 0 = end of this file, -1 = error, 2 = incomplete (more() and retry).
@@ -430,7 +476,7 @@ int parse_record(nt_reader* r, bool lens_only, std::vector<uint64_t>* skip_lens)
       if (!next_line(r, c, ls, le, need)) return need ? 2 : 0;
       if (le > ls && b[ls] == '>') break;
     }
-    const size_t name_at = ls + 1, name_len = le - ls - 1;
+    const size_t hdr = ls, name_at = ls + 1, name_len = le - ls - 1;
     r->pieces.clear();
     uint64_t len = 0;
     for (;;) {  // sequence lines up to the next header or the end of the file
@@ -447,8 +493,7 @@ int parse_record(nt_reader* r, bool lens_only, std::vector<uint64_t>* skip_lens)
       len += le - ls;
       r->pieces.emplace_back(ls, le - ls);
     }
-    r->pos = c.p;
-    r->nl_i = c.i;
+    commit(r, c, hdr);
     if (lens_only) {
       skip_lens->push_back(len);
       return 1;
@@ -478,7 +523,7 @@ int parse_record(nt_reader* r, bool lens_only, std::vector<uint64_t>* skip_lens)
     }
     break;
   }
-  const size_t name_at = ls + 1, name_len = le - ls - 1;
+  const size_t hdr = ls, name_at = ls + 1, name_len = le - ls - 1;
   auto malformed = [&] {
     r->err = "malformed FASTQ record '" + std::string(b + name_at, name_len) + "'";
     return -1;
@@ -495,8 +540,7 @@ int parse_record(nt_reader* r, bool lens_only, std::vector<uint64_t>* skip_lens)
     }
     ql += le - ls;
   }
-  r->pos = c.p;
-  r->nl_i = c.i;
+  commit(r, c, hdr);
   if (lens_only) {
     skip_lens->push_back(sl);
     return 1;
@@ -568,14 +612,13 @@ int nt_reader_open(const char* path, int format, nt_reader** out) {
     r->files.push_back(path);
   }
   r->format = format;
+  r->order.resize(r->files.size());
+  for (size_t i = 0; i < r->files.size(); ++i) r->order[i] = i;
   if (r->files.size() > 1) {  // a run directory: inflate gzip parts ahead on worker threads
     unsigned nt = std::thread::hardware_concurrency();
     nt = std::max(1u, std::min(nt == 0 ? 1u : nt, 16u));
     if (const char* v = std::getenv("NT_READER_THREADS")) nt = (unsigned)std::max(0, atoi(v));
-    if (nt > 0) {
-      r->pf.reset(new Prefetcher());
-      r->pf->start(r->files, nt);
-    }
+    r->pf_threads = nt;
   }
   *out = r;
   return NT_OK;
@@ -650,6 +693,278 @@ int64_t nt_reader_skip(nt_reader* r, uint64_t nrec, const uint64_t** seq_lens) {
   *seq_lens = L.data();
   r->records_total += (uint64_t)n;
   return n;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------ sharded ingest
+//
+// One process per GPU reads its share of the input instead of the whole
+// stream: every rank finds where the nrec-record chunks start
+// from 1/N of the bytes, then reads only the chunks it scans.
+//  * plain files (all of them): rank r indexes bytes [S r / N, S (r+1) / N) of
+//    the concatenated files -- it resynchronises at the first record start in
+//    its range (FASTA: a '>' line; FASTQ: an '@' line whose second next line
+//    starts with '+') and counts the records starting there; the ranks' counts
+//    give every record its global index, so the chunk starts are known;
+//  * gzip parts (a run directory): a gzip stream can only be inflated from its
+//    start, so rank r counts the records of whole files f = r (mod N);
+//  * then each rank seeks to its chunks' starts (nt_reader_seek) and reads
+//    them with nt_reader_next, visiting only the files its plan names
+//    (nt_reader_plan: the inflate-ahead workers take only those).
+// A resynchronisation that is not a true record start (a FASTQ quality line
+// shaped like a header) shows as a mismatch between rank r's first record and
+// the record at which rank r - 1's parse crossed into rank r's range: the
+// caller checks first(r) == next(r - 1) and otherwise reads unsharded.
+namespace {
+
+size_t nl_at(const char* d, size_t n, size_t p) {  // offset of the '\n' ending the line at p (or n)
+  const void* q = p < n ? memchr(d + p, '\n', n - p) : nullptr;
+  return q ? (size_t)((const char*)q - d) : n;
+}
+
+// first record-start candidate at or after byte o (> 0) of a plain file
+size_t resync(const char* d, size_t n, size_t o, int format) {
+  size_t p = o;
+  if (p > 0 && p < n && d[p - 1] != '\n') {
+    const size_t e = nl_at(d, n, p);
+    if (e >= n) return n;
+    p = e + 1;
+  }
+  while (p < n) {
+    const size_t e1 = nl_at(d, n, p);
+    if (format == 0) {
+      if (d[p] == '>') return p;
+    } else if (d[p] == '@' && e1 + 1 < n) {
+      const size_t e2 = nl_at(d, n, e1 + 1);
+      if (e2 + 1 < n && d[e2 + 1] == '+') return p;
+    }
+    if (e1 >= n) return n;
+    p = e1 + 1;
+  }
+  return n;
+}
+
+// a temporary reader over some of r's files (no inflate-ahead workers)
+void init_like(nt_reader& t, const nt_reader* r) {
+  t.files = r->files;
+  t.format = r->format;
+  t.pf_threads = 0;
+  t.order.clear();
+}
+
+// first file holding byte x of the concatenated plain files (n if none)
+size_t file_at(const nt_reader* r, uint64_t x) {
+  for (size_t f = 0; f < r->fsize.size(); ++f)
+    if (r->fbase[f] + r->fsize[f] > x) return f;
+  return r->fsize.size();
+}
+
+}  // namespace
+
+extern "C" {
+
+int nt_reader_layout(nt_reader* r, int* all_plain, uint64_t* total_bytes) {
+  if (!r || !all_plain || !total_bytes) return NT_E_ARG;
+  r->fsize.assign(r->files.size(), 0);
+  r->fbase.assign(r->files.size(), 0);
+  int plain = 1;
+  uint64_t tot = 0;
+  for (size_t f = 0; f < r->files.size(); ++f) {
+    struct stat st;
+    if (stat(r->files[f].c_str(), &st) != 0) {
+      r->err = "cannot open " + r->files[f];
+      return NT_E_ARG;
+    }
+    if (is_gzip(r->files[f])) plain = 0;
+    r->fsize[f] = (uint64_t)st.st_size;
+    r->fbase[f] = tot;
+    tot += (uint64_t)st.st_size;
+  }
+  *all_plain = plain;
+  *total_bytes = tot;
+  return NT_OK;
+}
+
+int64_t nt_reader_shard_range(nt_reader* r, uint64_t a, uint64_t b, uint64_t* first, uint64_t* next) {
+  if (!r || !first || !next || b < a || r->fbase.size() != r->files.size()) return NT_E_ARG;
+  const uint64_t S = r->fbase.empty() ? 0 : r->fbase.back() + r->fsize.back();
+  r->shard_pos.clear();
+  *first = *next = S;
+  const size_t f = file_at(r, a);
+  if (a >= S || f >= r->files.size()) return 0;
+  nt_reader t;
+  init_like(t, r);
+  for (size_t g = f; g < r->files.size(); ++g) t.order.push_back(g);
+  if (!open_next(&t)) {
+    r->err = t.err;
+    return NT_E_ARG;
+  }
+  // a range that starts inside a file resynchronises; one that starts at a
+  // file's first byte parses it as the unsharded reader does (errors included)
+  const uint64_t o = a - r->fbase[f];
+  const size_t p = o == 0 ? 0 : resync(t.win->data, t.end, (size_t)o, t.format);
+  t.pos = t.scan = p;
+  std::vector<uint64_t> lens;
+  bool have_first = false;
+  for (;;) {
+    const int k = parse_record(&t, true, &lens);
+    if (k == 1) {
+      const uint64_t x = r->fbase[t.cur_file] + t.rec_at;
+      if (!have_first) {
+        *first = x;
+        have_first = true;
+      }
+      if (x >= b) {
+        *next = x;
+        break;
+      }
+      r->shard_pos.push_back(x);
+      if (lens.size() > 4096) lens.clear();
+      continue;
+    }
+    if (k < 0) {
+      r->err = t.err;
+      return NT_E_ARG;
+    }
+    if (k == 2) {
+      if (!more(&t) && !t.err.empty()) {
+        r->err = t.err;
+        return NT_E_ARG;
+      }
+      continue;
+    }
+    if (!t.err.empty()) {
+      r->err = t.err;
+      return NT_E_ARG;
+    }
+    if (!open_next(&t)) {  // end of the stream
+      if (!t.err.empty()) {
+        r->err = t.err;
+        return NT_E_ARG;
+      }
+      break;
+    }
+  }
+  r->bytes_parsed += t.bytes_parsed;
+  return (int64_t)r->shard_pos.size();
+}
+
+int64_t nt_reader_shard_positions(const nt_reader* r, const uint64_t** pos) {
+  if (!r || !pos) return NT_E_ARG;
+  *pos = r->shard_pos.data();
+  return (int64_t)r->shard_pos.size();
+}
+
+int nt_reader_count_files(nt_reader* r, const uint64_t* files, uint64_t n, uint64_t* counts) {
+  if (!r || (n && (!files || !counts))) return NT_E_ARG;
+  for (uint64_t i = 0; i < n; ++i)
+    if (files[i] >= r->files.size()) return NT_E_ARG;
+  std::atomic<uint64_t> next{0}, parsed{0}, inflated{0};
+  std::mutex mu;
+  std::string err;
+  const unsigned nt = (unsigned)std::min<uint64_t>(host_threads(), n);
+  par(nt, [&](unsigned) {
+    for (uint64_t i = next++; i < n; i = next++) {
+      nt_reader t;
+      init_like(t, r);
+      t.order.push_back(files[i]);
+      std::vector<uint64_t> lens;
+      uint64_t c = 0;
+      for (;;) {
+        lens.clear();
+        const int64_t k = read_records(&t, 1u << 16, true, &lens);
+        if (k < 0) {
+          std::lock_guard<std::mutex> lk(mu);
+          if (err.empty()) err = t.err;
+          return;
+        }
+        if (k == 0) break;
+        c += (uint64_t)k;
+      }
+      counts[i] = c;
+      parsed += t.bytes_parsed;
+      inflated += t.bytes_inflated;
+    }
+  });
+  r->bytes_parsed += parsed;
+  r->bytes_inflated += inflated;
+  if (!err.empty()) {
+    r->err = err;
+    return NT_E_ARG;
+  }
+  return NT_OK;
+}
+
+int nt_reader_plan(nt_reader* r, const uint64_t* files, uint64_t n) {
+  if (!r || (n && !files)) return NT_E_ARG;
+  if (r->started) return NT_E_STATE;
+  for (uint64_t i = 0; i < n; ++i)
+    if (files[i] >= r->files.size() || (i && files[i] <= files[i - 1])) return NT_E_ARG;
+  r->order.assign(files, files + n);
+  return NT_OK;
+}
+
+int nt_reader_seek(nt_reader* r, int mode, uint64_t a, uint64_t b) {
+  if (!r || (mode != 0 && mode != 1)) return NT_E_ARG;
+  start(r);
+  uint64_t f = 0, off = 0, skip = 0;
+  if (mode == 0) {  // byte a of the concatenated plain files
+    if (r->fbase.size() != r->files.size()) return NT_E_ARG;
+    f = file_at(r, a);
+    if (f >= r->files.size()) {  // the end of the stream
+      close_source(r);
+      r->win.reset();
+      r->pos = r->end = r->scan = 0;
+      r->file_idx = r->order.size();
+      return NT_OK;
+    }
+    off = a - r->fbase[f];
+  } else {  // record b of file a
+    f = a;
+    skip = b;
+    if (f >= r->files.size()) return NT_E_ARG;
+  }
+  const bool here = r->active && r->cur_file == f;
+  if (mode == 0 && here && r->win && r->win->map && off <= r->end) {
+    // the mapped file is open: move within it
+  } else if (mode == 1 && here && r->rec_in_file <= skip) {
+    skip -= r->rec_in_file;  // forward in the open file
+  } else {
+    size_t at = r->file_idx;
+    while (at < r->order.size() && r->order[at] != f) ++at;
+    if (at >= r->order.size()) {
+      r->err = "seek to a file outside the reader's plan: " + r->files[f];
+      return NT_E_ARG;
+    }
+    r->file_idx = at;
+    if (!open_next(r)) return NT_E_ARG;
+  }
+  if (mode == 0) {
+    if (off > r->end) return NT_E_ARG;
+    r->pos = r->scan = off;
+    r->nl.clear();
+    r->nl_i = 0;
+    return NT_OK;
+  }
+  std::vector<uint64_t> lens;
+  while (skip > 0) {
+    lens.clear();
+    const int64_t k = read_records(r, std::min<uint64_t>(skip, 1u << 16), true, &lens);
+    if (k <= 0 || r->cur_file != f) {
+      if (r->err.empty()) r->err = "seek past the end of " + r->files[f];
+      return NT_E_ARG;
+    }
+    skip -= (uint64_t)k;
+  }
+  return NT_OK;
+}
+
+int nt_reader_stats(const nt_reader* r, uint64_t* out2) {
+  if (!r || !out2) return NT_E_ARG;
+  out2[0] = r->bytes_parsed;
+  out2[1] = r->bytes_inflated;
+  return NT_OK;
 }
 
 }  // extern "C"

@@ -128,6 +128,13 @@ SIGNATURES = {
                                         ctypes.POINTER(ctypes.c_void_p)]),
     "nt_reader_keep": (ctypes.c_int, [_P, ctypes.c_uint32]),
     "nt_reader_skip": (ctypes.c_int64, [_P, ctypes.c_uint64, ctypes.POINTER(ctypes.c_void_p)]),
+    "nt_reader_layout": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int), _U64P]),
+    "nt_reader_shard_range": (ctypes.c_int64, [_P, ctypes.c_uint64, ctypes.c_uint64, _U64P, _U64P]),
+    "nt_reader_shard_positions": (ctypes.c_int64, [_P, ctypes.POINTER(ctypes.c_void_p)]),
+    "nt_reader_count_files": (ctypes.c_int, [_P, _P, ctypes.c_uint64, _P]),
+    "nt_reader_plan": (ctypes.c_int, [_P, _P, ctypes.c_uint64]),
+    "nt_reader_seek": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64]),
+    "nt_reader_stats": (ctypes.c_int, [_P, _U64P]),
     "nt_synth_device": (ctypes.c_int, [_P, ctypes.POINTER(NtSynthParams), ctypes.c_uint64, _P]),
     "nt_uniform_layout_device": (ctypes.c_int, [_P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int32,
                                                 _P, _P, _P]),

@@ -3,9 +3,10 @@ block (NanoTel.R:30-93) and its argument checks (NanoTel.R:104-137).
 
     python -m nanotel_amd -i reads.fastq.gz --save_path out --patterns "TTAGGG"
 
-Multi-GPU: launch one process per GPU with torch.distributed.run; chunks are
-dealt round-robin to the ranks (driver.py / shard.py), rank 0 writes the
-summary.  --use_filter runs the edge pre-filter on the GPU.  --analysis writes
+Multi-GPU: launch one process per GPU with torch.distributed.run; the ranks
+index 1/N of the input each, read only their own blocks of chunks and scan
+them (driver.py / shard.py); the collectives run over RCCL when every rank has
+its own GPU; rank 0 writes the summary.  --use_filter runs the edge pre-filter on the GPU.  --analysis writes
 <barcode>_filtered_sorted_summary.csv and <barcode>_results.txt (analysis.py;
 not its ggplot2 PNG).  The single-read plots are written as in the reference
 (plots.py) unless --no_plots.
@@ -48,6 +49,19 @@ def parser():
     return ap
 
 
+def dist_backend(world, local_world, device_arg, n_gpus, env=os.environ):
+    """The process group's backend: NT_DIST_BACKEND when set; otherwise RCCL
+    ("nccl") when every local rank has a GPU of its own (the summary-row
+    gather and the per-group serial all_reduce then go over xGMI, north_star's
+    layout), gloo when ranks share a GPU (an explicit --device, or more local
+    ranks than GPUs) or there is one rank."""
+    if env.get("NT_DIST_BACKEND"):
+        return env["NT_DIST_BACKEND"]
+    if world > 1 and device_arg is None and n_gpus >= local_world:
+        return "nccl"
+    return "gloo"
+
+
 def main(argv=None):
     a = parser().parse_args(argv)
     if a.version:
@@ -71,11 +85,10 @@ def main(argv=None):
         import torch
         import torch.distributed as dist
         torch.cuda.set_device(dev)
-        # The driver's collectives are tiny and host-side (8 bytes per chunk,
-        # an error flag, the pickled summary rows): gloo by default.
-        # NT_DIST_BACKEND=nccl runs the per-round all_reduce over RCCL on a
-        # device tensor instead (opt-in).
-        dist.init_process_group(os.environ.get("NT_DIST_BACKEND", "gloo"))
+        # RCCL when each rank has its own GPU (device tensors for every
+        # collective, shard.collective_device), gloo when they share one
+        local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+        dist.init_process_group(dist_backend(world, local_world, a.device, torch.cuda.device_count()))
     try:
         run(a.input_path, a.save_path, a.patterns, fmt=a.format, nrec=a.nrec, rc=a.rc,
             min_density=a.min_density, subseq_length=a.subseq_length,

@@ -214,15 +214,19 @@ def _plot_jobs(nt, res, order, lens, ser, save_path):
 
 # One device call covers several of the reference's nrec-record chunks (they
 # stay the units of serials and rows): the calling kernel specialised for the
-# patterns runs on batches of >= 65,536 reads (nt_host.cpp), so a call takes
-# ceil(65536 / nrec) rounds of chunks, at most kGroupRounds and at most
-# kGroupBases bases per rank.
+# patterns runs on batches of >= 65,536 reads (nt_host.cpp), so a rank's block
+# of a group is ceil(65536 / nrec) chunks, at most kGroupRounds, scanned in
+# calls of at most kGroupBases bases.
 kCallReads = 65536
 kGroupRounds = 16
 kGroupBases = 4_000_000_000
 
 
 def _group_rounds(nrec):
+    """Chunks per block (NT_GROUP_CHUNKS overrides: small blocks spread small
+    test inputs over the ranks)."""
+    if os.environ.get("NT_GROUP_CHUNKS"):
+        return max(1, int(os.environ["NT_GROUP_CHUNKS"]))
     return max(1, min(kGroupRounds, -(-kCallReads // max(1, nrec))))
 
 
@@ -243,11 +247,11 @@ class _LazyNames(dict):
 
 
 def _scan_group(nt, chunks, use_filter, write_reads, log, want_windows=False):
-    """Scan + call the reads of several chunks in ONE device call (after
-    --use_filter, per chunk, when on).  Returns per chunk (rel_serials,
-    row_order, rel_max, result view, name_of(j), lengths, {read: seq}) over
-    the reads that were scanned; rel_max is shard.SKIPPED for a chunk that
-    --use_filter emptied."""
+    """Scan + call the reads of several chunks in as few device calls as
+    possible -- one per kGroupBases bases (after --use_filter, per chunk, when
+    on).  Returns per chunk (rel_serials, row_order, rel_max, result view,
+    name_of(j), lengths, {read: seq}) over the reads that were scanned;
+    rel_max is shard.SKIPPED for a chunk that --use_filter emptied."""
     parts = []
     for ch in chunks:
         idx = np.arange(ch.n)
@@ -256,42 +260,86 @@ def _scan_group(nt, chunks, use_filter, write_reads, log, want_windows=False):
             if idx.size == 0:
                 log("No read have passed the filteration at run_with_rc_and_filter!")
         parts.append((ch, idx))
-    ptrs = np.concatenate([ch.pointers()[idx] for ch, idx in parts]) if parts else np.zeros(0, np.uint64)
-    lens = np.concatenate([ch.lengths[idx] for ch, idx in parts]) if parts else np.zeros(0, np.uint64)
-    res = nt.analyze_pointers(ptrs, lens, want_windows=want_windows) if ptrs.size else None
-    out, a = [], 0
+    calls, cur, bases = [], [], 0  # consecutive chunks, at most kGroupBases bases a call (at least one chunk)
     for ch, idx in parts:
-        b = a + idx.size
-        if idx.size == 0:
-            out.append((None, np.zeros(0, np.int64), shard.SKIPPED, None, None, lens[:0], {}))
-            continue
-        v = _View({k: res[k][a:b] for k in ("start", "end", "density", "flags", "width", "telomeric") if k in res})
-        if want_windows:
-            v["win_off"], v["n_windows"], v["win_counts"] = res["win_off"][a:b], res["n_windows"][a:b], \
-                res["win_counts"]
-        np_, nl_ = ch.name_pointers()
-        v["name_ptrs"], v["name_lens"] = np_[idx], nl_[idx]
-        rel, order, rmax = shard.chunk_relative(v["telomeric"])
-        name_of = (lambda c, ix: (lambda j: c.name(int(ix[j]))))(ch, idx)
-        seqs = {int(j): ch.seq(int(idx[int(j)])) for j in order} if write_reads else {}
-        out.append((rel, order, rmax, v, name_of, lens[a:b], seqs))
-        a = b
+        b = int(ch.lengths[idx].sum()) if idx.size else 0
+        if cur and bases + b > kGroupBases:
+            calls.append(cur)
+            cur, bases = [], 0
+        cur.append((ch, idx))
+        bases += b
+    if cur:
+        calls.append(cur)
+    out = []
+    for call in calls:
+        ptrs = np.concatenate([ch.pointers()[idx] for ch, idx in call])
+        lens = np.concatenate([ch.lengths[idx] for ch, idx in call])
+        res = nt.analyze_pointers(ptrs, lens, want_windows=want_windows) if ptrs.size else None
+        a = 0
+        for ch, idx in call:
+            b = a + idx.size
+            if idx.size == 0:
+                out.append((None, np.zeros(0, np.int64), shard.SKIPPED, None, None, lens[:0], {}))
+                continue
+            v = _View({k: res[k][a:b] for k in ("start", "end", "density", "flags", "width", "telomeric")
+                       if k in res})
+            if want_windows:
+                v["win_off"], v["n_windows"], v["win_counts"] = res["win_off"][a:b], res["n_windows"][a:b], \
+                    res["win_counts"]
+            np_, nl_ = ch.name_pointers()
+            v["name_ptrs"], v["name_lens"] = np_[idx], nl_[idx]
+            rel, order, rmax = shard.chunk_relative(v["telomeric"])
+            name_of = (lambda c, ix: (lambda j: c.name(int(ix[j]))))(ch, idx)
+            seqs = {int(j): ch.seq(int(idx[int(j)])) for j in order} if write_reads else {}
+            out.append((rel, order, rmax, v, name_of, lens[a:b], seqs))
+            a = b
     return out
 
 
 class _Prefetch:
-    """Chunk k+1 is read on a worker thread while chunk k is scanned (the C++
-    reader keeps the last chunks valid, nt_reader_keep, and ctypes drops the
-    GIL).  Chunks this rank does not scan (own(k) false) are passed over with
-    the reader's count-only skip path: record boundaries and lengths, no copies."""
+    """The next chunk is read on a worker thread while the current ones are
+    scanned (the C++ reader keeps the last chunks valid, nt_reader_keep, and
+    ctypes drops the GIL).
 
-    def __init__(self, rdr, nrec, own=lambda k: True):
+    Sharded ingest (plan.sharded): only this rank's chunks are read, in order,
+    with one seek at the start of each of its blocks.  Otherwise the whole
+    stream is read and the chunks this rank does not scan are passed over with
+    the reader's count-only skip path (record boundaries and lengths, no copies)."""
+
+    def __init__(self, rdr, nrec, own=lambda k: True, plan=None, g=1, world=1, rank=0):
         self._rdr, self._nrec, self._own = rdr, nrec, own
+        self._plan = plan if plan is not None and plan.sharded else None
         self._k = 0
+        if self._plan is not None:
+            n = self._plan.n_chunks
+            G = g * world
+            self._seq = [k for t0 in range(0, n, G) for k in range(t0 + rank * g, min(t0 + (rank + 1) * g, n))]
+            self._i = 0
+            self._g = g
+            blocks = [(k, min(k + g, n)) for k in self._seq[::g]]
+            files = sorted({f for k0, k1 in blocks for f in range(*self._span(k0, k1))})
+            rdr.plan(files)
         self._ex = ThreadPoolExecutor(1)
         self._f = self._ex.submit(self._read)
 
+    def _span(self, k0, k1):
+        f0, f1 = self._plan.files_of(k0, k1, self._nrec)
+        return f0, f1 + 1
+
     def _read(self):
+        if self._plan is not None:
+            if self._i >= len(self._seq):
+                return None
+            k = self._seq[self._i]
+            self._i += 1
+            if k % self._g == 0:  # a block's first chunk
+                self._plan.seek(self._rdr, k)
+            ch = self._rdr.next_chunk(self._nrec)
+            want = self._plan.chunk_len(k, self._nrec)
+            if ch is None or ch.n != want:
+                raise RuntimeError(f"NanoTel: sharded ingest read {0 if ch is None else ch.n} records "
+                                   f"of chunk {k + 1}, expected {want}")
+            return ch
         k = self._k
         self._k += 1
         return self._rdr.next_chunk(self._nrec) if self._own(k) else self._rdr.skip_chunk(self._nrec)
@@ -357,49 +405,69 @@ def run(input_path, save_path, patterns, fmt="fastq", nrec=10000, rc=False, min_
     tvr = tvr_patterns is not None
     rdr = Reader(input_path, fmt)
     files = rdr.files()
-    g = _group_rounds(nrec)  # rounds of chunks per device call
+    g = _group_rounds(nrec)  # chunks per block: a rank's chunks of one group
+    G = g * world            # chunks per group (one collective per group)
     rdr.keep(g + 2)          # this rank's chunks of a group stay valid, plus the one read ahead
-    # chunk k of the stream is scanned by rank k % world (rounds of `world`
-    # chunks); the other ranks pass over it with the reader's skip path
-    src = _Prefetch(rdr, nrec, own=lambda k: k % world == rank)
+    t0 = time.time()
+    tm = {"setup": 0.0, "index": 0.0, "read_wait": 0.0, "scan": 0.0, "rows_files": 0.0, "collectives": 0.0}
+    # sharded ingest: the ranks find the chunk starts together (each indexes
+    # 1/N of the input) and each reads only its own chunks; otherwise every
+    # rank reads the stream and passes over the others' chunks
+    ti = time.perf_counter()
+    try:
+        plan = shard.ingest_plan(rdr, nrec, rank, world, device=coll_dev, log=log) if dist_on \
+            else shard.IngestPlan(reason="one rank")
+    except Exception:  # every rank raises here (the plan's exchange carries the error flag)
+        rdr.close()
+        nt.close()
+        raise
+    tm["index"] = time.perf_counter() - ti
+    # chunk k of the stream is scanned by rank (k // g) % world: groups of
+    # `world` blocks of g chunks
+    src = _Prefetch(rdr, nrec, own=lambda c: shard.block_owner(c, g, world) == rank, plan=plan, g=g,
+                    world=world, rank=rank)
     writers = ThreadPoolExecutor(min(16, os.cpu_count() or 1)) if (write_reads or plot) else None
     plotters = None  # worker processes for the plots of large chunks (Python drawing holds the GIL)
     pending = []
-    lengths_all = []
+    lengths_own = {}  # chunk -> read lengths (uint32), gathered to rank 0 for run.log
     local_rows = {}
     held = None  # (chunk, read args, plot job) of this rank's last -Inf row (see _targets)
-    k = 0  # global chunk index
+    k = 0  # global chunk index of the group's first chunk
     s_next, m_run = 1.0, shard.NEG_INF  # serial_start of the next chunk, running max(Serial)
-    t0 = time.time()
     failure = None
-    # groups of up to g rounds of `world` chunks: rank r scans chunk r of each
-    # round, the group's in one device call; one all_reduce per group fixes the
+    # groups of G chunks: rank r scans block r of each group (its device calls,
+    # split at kGroupBases bases); one all_reduce per group fixes the
     # serial_starts (and carries an error flag, so that a rank that fails stops
     # every rank at the same group instead of leaving them blocked in the next
-    # collective).  Every rank reads the same stream, so the groups' extents
-    # (the rounds, the bases cap) agree.
-    tm = {"setup": time.time() - t0, "read_wait": 0.0, "scan": 0.0, "rows_files": 0.0, "collectives": 0.0}
+    # collective).  The ranks agree on the groups: the plan's chunk count, or
+    # (unsharded) the same stream read by every rank.
+    tm["setup"] = time.time() - t0 - tm["index"]
     while True:
         own = []  # (chunk's place in the group, chunk)
         n_grp, ended = 0, False
         try:
-            bases = 0
-            for _ in range(g):
-                for r in range(world):
+            if plan.sharded:
+                n_grp = min(G, plan.n_chunks - k)
+                ended = k + G >= plan.n_chunks
+                for c in range(k + rank * g, min(k + (rank + 1) * g, plan.n_chunks)):
+                    tr = time.perf_counter()
+                    ch = src.next_chunk()
+                    tm["read_wait"] += time.perf_counter() - tr
+                    own.append((c - k, ch))
+            else:
+                for pos in range(G):
                     tr = time.perf_counter()
                     ch = src.next_chunk()
                     tm["read_wait"] += time.perf_counter() - tr
                     if ch is None:
                         ended = True
                         break
-                    lengths_all.append(ch.lengths.copy())
-                    bases += int(ch.lengths.sum())
-                    if r == rank:
-                        log(f"processing chunk {k + n_grp + 1} ...")
-                        own.append((n_grp, ch))
+                    if shard.block_owner(k + pos, g, world) == rank:
+                        own.append((pos, ch))
                     n_grp += 1
-                if ended or bases >= kGroupBases * world:
-                    break
+            for pos, ch in own:
+                log(f"processing chunk {k + pos + 1} ...")
+                lengths_own[k + pos] = ch.lengths.astype(np.uint32)
             ts = time.perf_counter()
             scanned = _scan_group(nt, [ch for _, ch in own], use_filter, write_reads, log, want_windows=plot)
             tm["scan"] += time.perf_counter() - ts
@@ -407,7 +475,7 @@ def run(input_path, save_path, patterns, fmt="fastq", nrec=10000, rc=False, min_
             failure, scanned = ex, []
         local = {own[i][0]: scanned[i][2] for i in range(len(scanned))}
         tc = time.perf_counter()
-        maxima, failed = shard.exchange_rel_max(local, g * world, device=coll_dev, failed=failure is not None)
+        maxima, failed = shard.exchange_rel_max(local, G, device=coll_dev, failed=failure is not None)
         tm["collectives"] += time.perf_counter() - tc
         if failed:
             break
@@ -477,8 +545,12 @@ def run(input_path, save_path, patterns, fmt="fastq", nrec=10000, rc=False, min_
         raise RuntimeError("NanoTel: another rank failed (see its error)")
     t_end = time.time()
     rows = SummaryRows(shard.gather_chunks(local_rows) or [], nt.n_pass)
+    lengths_all = shard.gather_chunks(lengths_own)
     if stats is not None:
         stats.update(tm)
+        stats["ingest"] = plan.mode or "unsharded"
+        stats["ingest_reason"] = plan.reason
+        stats["bytes_parsed"], stats["bytes_inflated"] = rdr.stats()
         stats.update({"host_" + k: v for k, v in nt.host_times().items()} if hasattr(nt, "host_times") else {})
         stats["groups_rounds"] = g
     rdr.close()

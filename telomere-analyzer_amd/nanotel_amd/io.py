@@ -115,6 +115,55 @@ class Reader:
             return None
         return SkippedChunk(n, d)
 
+    # ---- sharded ingest (nt_reader_layout / shard_range / count_files / plan / seek)
+
+    def _check(self, rc, what):
+        if rc < 0:
+            raise NanoTelError(int(rc), f"{what}: {lib().nt_reader_error(self._h).decode()}")
+        return rc
+
+    def layout(self):
+        """(all files plain, total bytes of the concatenated files)."""
+        plain, tot = ctypes.c_int(), ctypes.c_uint64()
+        self._check(lib().nt_reader_layout(self._h, ctypes.byref(plain), ctypes.byref(tot)), "layout")
+        return bool(plain.value), int(tot.value)
+
+    def shard_range(self, a, b):
+        """Records starting in bytes [a, b) of the concatenated plain files:
+        (their global byte offsets (uint64 array), first record start >= a,
+        first record start >= b)."""
+        first, nxt = ctypes.c_uint64(), ctypes.c_uint64()
+        n = self._check(lib().nt_reader_shard_range(self._h, int(a), int(b), ctypes.byref(first),
+                                                    ctypes.byref(nxt)), "shard_range")
+        p = ctypes.c_void_p()
+        lib().nt_reader_shard_positions(self._h, ctypes.byref(p))
+        pos = np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(ctypes.c_uint64)), shape=(n,)).copy() \
+            if n else np.zeros(0, np.uint64)
+        return pos, int(first.value), int(nxt.value)
+
+    def count_files(self, files):
+        """Record counts of whole files (indices into files())."""
+        f = np.ascontiguousarray(files, np.uint64)
+        out = np.zeros(f.size, np.uint64)
+        self._check(lib().nt_reader_count_files(self._h, f.ctypes.data, f.size, out.ctypes.data), "count_files")
+        return out
+
+    def plan(self, files):
+        f = np.ascontiguousarray(files, np.uint64)
+        self._check(lib().nt_reader_plan(self._h, f.ctypes.data, f.size), "plan")
+
+    def seek_byte(self, pos):
+        self._check(lib().nt_reader_seek(self._h, 0, int(pos), 0), "seek")
+
+    def seek_record(self, file, skip):
+        self._check(lib().nt_reader_seek(self._h, 1, int(file), int(skip)), "seek")
+
+    def stats(self):
+        """(bytes parsed, bytes inflated) by this reader so far."""
+        out = (ctypes.c_uint64 * 2)()
+        lib().nt_reader_stats(self._h, out)
+        return int(out[0]), int(out[1])
+
     def close(self):
         if getattr(self, "_h", None) is not None and self._h.value:
             lib().nt_reader_close(self._h)

@@ -169,6 +169,137 @@ def gather_chunks(local, group=None, dst=0):
     return [v for _, v in sorted(merged.items())]
 
 
+def block_owner(chunk, g, world):
+    """Rank that scans chunk `chunk`: blocks of g consecutive chunks dealt
+    round-robin (group t = chunks [t g world, (t+1) g world); rank r owns the
+    r-th block of every group), so a rank's chunks of a group are one
+    contiguous run of records and a sharded reader seeks once per group."""
+    return (chunk // g) % world
+
+
+class IngestPlan:
+    """Where every nrec-record chunk of the input starts, found by the ranks
+    together from 1/N of the input each (nt_reader_shard_range /
+    nt_reader_count_files), so that each rank reads only the chunks it scans
+    (DESIGN.md §7).  Chunk k is still records [k nrec, (k+1) nrec) of the
+    whole stream (run_future_worker_chuncks, NanoTel.R:2207-2254), so the
+    serials (A15) do not change.
+
+    mode "range": all files plain -- chunk starts are byte offsets of the
+    concatenated files; "files": gzip parts -- chunk starts are (file, record
+    within the file); None: unsharded (one rank, a single gzip stream, or a
+    failed resynchronisation): every rank reads the whole stream and passes
+    over the chunks it does not scan (nt_reader_skip)."""
+
+    def __init__(self, mode=None, n_chunks=None, total=None, starts=None, file_first=None, reason=""):
+        self.mode, self.n_chunks, self.total = mode, n_chunks, total
+        self.starts = starts          # range: (n_chunks,) byte offsets; files: (n_chunks, 2) (file, skip)
+        self.file_first = file_first  # range: files' first byte offsets; files: files' first record index
+        self.reason = reason
+        self.index_s = 0.0
+
+    @property
+    def sharded(self):
+        return self.mode is not None
+
+    def chunk_len(self, k, nrec):
+        return min(nrec, self.total - k * nrec)
+
+    def seek(self, rdr, k):
+        """Move the reader to chunk k's first record."""
+        if self.mode == "range":
+            rdr.seek_byte(int(self.starts[k]))
+        else:
+            rdr.seek_record(int(self.starts[k, 0]), int(self.starts[k, 1]))
+
+    def files_of(self, k0, k1, nrec):
+        """The files holding records of chunks [k0, k1) (an inclusive index range)."""
+        if self.mode == "range":
+            a = int(self.starts[k0])
+            b = int(self.starts[k1]) - 1 if k1 < self.n_chunks else int(self.file_first[-1]) - 1
+            f0 = int(np.searchsorted(self.file_first, a, side="right")) - 1
+            f1 = int(np.searchsorted(self.file_first, max(a, b), side="right")) - 1
+        else:
+            r0, r1 = k0 * nrec, min(k1 * nrec, self.total) - 1
+            f0 = int(np.searchsorted(self.file_first, r0, side="right")) - 1
+            f1 = int(np.searchsorted(self.file_first, r1, side="right")) - 1
+            f1 = max(f0, f1)
+        return f0, f1
+
+
+def _all_sum(vec, device):
+    """Elementwise sum over the ranks of an int64 vector (one all_reduce)."""
+    import torch
+    import torch.distributed as dist
+    t = torch.as_tensor(np.ascontiguousarray(vec, np.int64), device=device if device is not None else "cpu")
+    if _collective():
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return t.cpu().numpy()
+
+
+def ingest_plan(rdr, nrec, rank, world, device=None, log=None):
+    """The ranks' chunk starts (collective: every rank calls it).  See IngestPlan."""
+    import time
+    t0 = time.perf_counter()
+    if world <= 1 or os.environ.get("NT_SHARD_INGEST", "1") == "0":
+        return IngestPlan(reason="one rank" if world <= 1 else "NT_SHARD_INGEST=0")
+    from ._lib import NanoTelError
+    files = rdr.files()
+    plain, total_bytes = rdr.layout()
+    if plain:
+        a, b = total_bytes * rank // world, total_bytes * (rank + 1) // world
+        row, err = np.zeros((world, 4), np.int64), None
+        try:
+            pos, first, nxt = rdr.shard_range(a, b)
+            row[rank] = (pos.size, first, nxt, 0)
+        except NanoTelError as ex:
+            pos, err = np.zeros(0, np.uint64), ex
+            row[rank] = (0, 0, 0, 1)
+        row = _all_sum(row.ravel(), device).reshape(world, 4)
+        if row[:, 3].any():
+            raise err if err is not None else RuntimeError("NanoTel: another rank failed to read the input")
+        if any(row[r, 1] != row[r - 1, 2] for r in range(1, world)):
+            plan = IngestPlan(reason="resynchronisation mismatch (a FASTQ quality line shaped like a header)")
+        else:
+            counts = row[:, 0]
+            total = int(counts.sum())
+            n_chunks = -(-total // nrec)
+            g0 = int(counts[:rank].sum())
+            first_local = (-g0) % nrec
+            idx = np.arange(first_local, pos.size, nrec)
+            starts = np.zeros(n_chunks, np.int64)
+            if idx.size:
+                starts[(g0 + idx) // nrec] = pos[idx].astype(np.int64)
+            starts = _all_sum(starts, device)
+            sizes = np.array([os.path.getsize(f) for f in files], np.int64)
+            ff = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+            plan = IngestPlan("range", n_chunks, total, starts, ff)
+    elif len(files) < 2:
+        plan = IngestPlan(reason="a single gzip stream (inflated from its start by every rank)")
+    else:
+        own = np.arange(rank, len(files), world, dtype=np.uint64)
+        vec, err = np.zeros(len(files) + 1, np.int64), None
+        try:
+            vec[own.astype(np.int64)] = rdr.count_files(own).astype(np.int64)
+        except NanoTelError as ex:
+            err = ex
+            vec[-1] = 1
+        vec = _all_sum(vec, device)
+        if vec[-1]:
+            raise err if err is not None else RuntimeError("NanoTel: another rank failed to read the input")
+        counts = vec[:-1]
+        total = int(counts.sum())
+        n_chunks = -(-total // nrec)
+        ff = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)  # files' first record index
+        first = np.arange(n_chunks, dtype=np.int64) * nrec
+        f = np.searchsorted(ff, first, side="right") - 1
+        plan = IngestPlan("files", n_chunks, total, np.stack([f, first - ff[f]], axis=1), ff)
+    plan.index_s = time.perf_counter() - t0
+    if log is not None and not plan.sharded:
+        log(f"ingest not sharded: {plan.reason}")
+    return plan
+
+
 def sequential_serials(flags_per_chunk):
     """Reference recurrence run chunk by chunk in one process (the oracle for
     the sharded path): list of per-chunk absolute serial arrays."""

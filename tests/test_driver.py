@@ -104,16 +104,25 @@ def _free_port():
     return p
 
 
-def _rank_main(rank, world, port, inp, out, rc, use_filter=False):
+def _rank_main(rank, world, port, inp, out, rc, use_filter=False, g=1, fmt="fasta", nrec=3, stats_dir=None):
+    """One rank of a driver run (g: chunks per block, NT_GROUP_CHUNKS -- 1 deals
+    the few chunks of these small inputs over every rank)."""
+    import json
     import torch.distributed as dist
     from nanotel_amd import driver
     driver.NanoTel = OracleNanoTel
+    if g is not None:
+        os.environ["NT_GROUP_CHUNKS"] = str(g)
     if world > 1:
         os.environ["MASTER_ADDR"] = "127.0.0.1"
         os.environ["MASTER_PORT"] = str(port)
         dist.init_process_group("gloo", rank=rank, world_size=world)
-    driver.run(inp, out, "TTAGGG", fmt="fasta", nrec=3, rc=rc, use_filter=use_filter, analysis=True,
-               log=lambda *a: None)
+    st = {}
+    driver.run(inp, out, "TTAGGG", fmt=fmt, nrec=nrec, rc=rc, use_filter=use_filter, analysis=True,
+               log=lambda *a: None, stats=st)
+    if stats_dir is not None:
+        with open(os.path.join(stats_dir, f"stats_{world}_{rank}.json"), "w") as f:
+            json.dump({k: v for k, v in st.items() if isinstance(v, (int, float, str))}, f)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
@@ -336,6 +345,7 @@ def _failing_rank(rank, world, port, inp, out, q):
     driver.NanoTel = FailingNanoTel
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
+    os.environ["NT_GROUP_CHUNKS"] = "1"
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         driver.run(inp, out, "TTAGGG", fmt="fasta", nrec=3, log=lambda *a: None, plot=False)
@@ -369,3 +379,130 @@ def test_rank_failure_stops_every_rank():
         got = dict(q.get(timeout=5) for _ in range(2))
         assert got[1] == "injected scan failure"
         assert "another rank failed" in got[0]
+
+
+def _shard_records(n=61, seed=31):
+    rng = np.random.default_rng(seed)
+    recs = []
+    for i in range(n):
+        m = int(rng.integers(150, 3000))
+        s = list(rng.choice(list("ACGT"), m))
+        if i % 3 != 2:
+            t = int(rng.integers(150, min(m, 1500)))
+            s[:t] = list(("TTAGGG" * (t // 6 + 1))[:t])
+        recs.append((f"rd{i} ch={i % 7}", "".join(s)))
+    return recs, rng
+
+
+def _write_shard_inputs(d):
+    """The three input shapes of a sharded run: one plain FASTQ (CRLF, quality
+    lines that start with '@' or '+', a blank line between records), one
+    wrapped FASTA, and a run directory of 16 fastq.gz parts (two empty)."""
+    recs, rng = _shard_records()
+    qual = lambda s: "".join(rng.choice(list("@+I#5"), len(s)))  # noqa: E731
+    fq = os.path.join(d, "reads.fastq")
+    with open(fq, "w", newline="") as f:
+        for i, (n, s) in enumerate(recs):
+            f.write(f"@{n}\r\n{s}\r\n+\r\n{qual(s)}\r\n" + ("\n" if i % 5 == 4 else ""))
+    fa = os.path.join(d, "reads.fasta")
+    with open(fa, "w") as f:
+        for n, s in recs:
+            f.write(f">{n}\n" + "\n".join(s[i:i + 70] for i in range(0, len(s), 70)) + "\n")
+    run = os.path.join(d, "run")
+    os.makedirs(run)
+    cuts = np.sort(np.concatenate([[0, 0, len(recs), len(recs)], rng.integers(0, len(recs), 13)]))
+    for p in range(16):
+        with gzip.open(os.path.join(run, f"part_{p:02d}.fastq.gz"), "wt") as f:
+            for n, s in recs[cuts[p]:cuts[p + 1]]:
+                f.write(f"@{n}\n{s}\n+\n{qual(s)}\n")
+    return {"fastq": (fq, "fastq", "range"), "fasta": (fa, "fasta", "range"), "run": (run, "fastq", "files")}
+
+
+def _expected_inflate(run, world, g, nrec):
+    """Bytes each rank of a sharded run over a directory of fastq.gz parts
+    inflates: its count-pass parts (p = rank mod world) and every part that
+    holds a record of its blocks (blocks of g chunks dealt round-robin)."""
+    parts = sorted(os.listdir(run))
+    data = [gzip.open(os.path.join(run, p), "rb").read() for p in parts]
+    counts = [x.count(b"\n") // 4 for x in data]
+    first = np.concatenate([[0], np.cumsum(counts)])
+    total = int(first[-1])
+    n_chunks = -(-total // nrec)
+    out = []
+    for r in range(world):
+        b = sum(len(data[p]) for p in range(r, len(parts), world))
+        need = set()
+        for k0 in range(r * g, n_chunks, g * world):
+            r0, r1 = k0 * nrec, min((k0 + g) * nrec, total) - 1
+            f0 = int(np.searchsorted(first, r0, side="right")) - 1
+            f1 = int(np.searchsorted(first, r1, side="right")) - 1
+            need.update(range(f0, max(f0, f1) + 1))
+        out.append(b + sum(len(data[p]) for p in need))
+    return out
+
+
+@pytest.mark.timeout(600)
+def test_sharded_ingest_outputs_identical_across_world_sizes():
+    """Every rank reads only its own chunks: for a plain FASTQ,
+    a wrapped FASTA and a 16-part fastq.gz run directory, world 1/2/3/8 write
+    byte-identical outputs, the plan is sharded ("range" / "files"), and each
+    rank parses about 2/N of the input bytes (its index share plus its chunks),
+    not the whole stream."""
+    import json
+    import torch.multiprocessing as mp
+    with tempfile.TemporaryDirectory() as d:
+        for key, (inp, fmt, mode) in _write_shard_inputs(d).items():
+            res = {}
+            g = 1 if mode == "range" else 2  # a block of the run directory spans about 2 parts
+            for world in (1, 2, 3, 8):
+                out = os.path.join(d, f"{key}_out{world}")
+                sd = os.path.join(d, f"{key}_stats")
+                os.makedirs(sd, exist_ok=True)
+                if world == 1:
+                    _rank_main(0, 1, 0, inp, out, False, False, g, fmt, 4, sd)
+                else:
+                    mp.spawn(_rank_main, args=(world, _free_port(), inp, out, False, False, g, fmt, 4, sd),
+                             nprocs=world, join=True)
+                res[world] = _outputs(out)
+                st = [json.load(open(os.path.join(sd, f"stats_{world}_{r}.json"))) for r in range(world)]
+                if world > 1:
+                    assert all(s["ingest"] == mode for s in st), (key, world, st[0])
+                    size = sum(os.path.getsize(os.path.join(r, f)) for r, _, fs in os.walk(inp) for f in fs) \
+                        if os.path.isdir(inp) else os.path.getsize(inp)
+                    if mode == "range":
+                        # every rank's parse: its 1/N index share + its chunks
+                        assert max(s["bytes_parsed"] for s in st) < size * (2.0 / world + 0.25), (key, world, st)
+                        assert sum(s["bytes_parsed"] for s in st) < 2.2 * size
+                    else:
+                        # gzip parts: the count pass inflates parts p = r (mod N),
+                        # the chunk reads exactly the parts the rank's blocks touch
+                        assert [s["bytes_inflated"] for s in st] == _expected_inflate(inp, world, g, 4), (key, world)
+            assert res[1] == res[2] == res[3] == res[8], key
+            summary = res[1][f"{os.path.basename(inp)}_summary.csv"].decode().splitlines()
+            assert len(summary) > 20
+
+
+@pytest.mark.parametrize("g", [1, 2, None])
+def test_block_ownership_world2(g):
+    """Blocks of g chunks (None: the default, ceil(65536 / nrec) capped at 16)
+    give the files of a single process."""
+    import torch.multiprocessing as mp
+    with tempfile.TemporaryDirectory() as d:
+        inp = _make_input(d, False)
+        _rank_main(0, 1, 0, inp, os.path.join(d, "one"), False)
+        mp.spawn(_rank_main, args=(2, _free_port(), inp, os.path.join(d, "two"), False, False, g),
+                 nprocs=2, join=True)
+        assert _outputs(os.path.join(d, "one")) == _outputs(os.path.join(d, "two"))
+
+
+def test_dist_backend_choice():
+    """RCCL by default when every local rank has its own GPU; gloo when ranks
+    share one (explicit --device, more local ranks than GPUs) or run alone;
+    NT_DIST_BACKEND overrides."""
+    from nanotel_amd.cli import dist_backend
+    assert dist_backend(8, 8, None, 8, env={}) == "nccl"
+    assert dist_backend(2, 2, None, 1, env={}) == "gloo"
+    assert dist_backend(2, 2, 0, 8, env={}) == "gloo"
+    assert dist_backend(1, 1, None, 8, env={}) == "gloo"
+    assert dist_backend(8, 8, None, 8, env={"NT_DIST_BACKEND": "gloo"}) == "gloo"
+    assert dist_backend(1, 1, None, 1, env={"NT_DIST_BACKEND": "nccl"}) == "nccl"

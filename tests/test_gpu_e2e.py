@@ -95,18 +95,20 @@ def test_driver_use_filter_gpu_matches_oracle_driver(tmp_path):
 
 
 def test_cli_two_ranks_match_one(tmp_path):
-    """The command line under torch.distributed.run with 2 ranks (chunks dealt
-    round-robin, one serial all_reduce per round, rows gathered to rank 0)
-    writes the same files as one process.  Both ranks use GPU 0 here, so the
-    collectives run on gloo (NT_DIST_BACKEND); on a node each rank has its GPU
-    and RCCL."""
+    """The command line under torch.distributed.run with 2 ranks (sharded
+    ingest: the ranks count the input's files between them and each reads only
+    its blocks of chunks -- one chunk a block here, NT_GROUP_CHUNKS; one serial
+    all_reduce per group, rows gathered to rank 0) writes the same files as one
+    process.  Both ranks use GPU 0 here, so the collectives run on gloo
+    (NT_DIST_BACKEND); on a node each rank has its GPU and RCCL (the default,
+    cli.dist_backend)."""
     import socket
     import subprocess
     import sys
     inp = _make_input(str(tmp_path), False)
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ, PYTHONPATH=os.path.join(root, "telomere-analyzer_amd"), NT_DIST_BACKEND="gloo",
-               HSA_ENABLE_IPC_MODE_LEGACY="0")
+               HSA_ENABLE_IPC_MODE_LEGACY="0", NT_GROUP_CHUNKS="1")
     args = ["-i", inp, "--format", "fasta", "--patterns", "TTAGGG", "-n", "4", "--device", "0"]
     one = str(tmp_path / "one")
     subprocess.run([sys.executable, "-m", "nanotel_amd", "--save_path", one] + args, env=env, check=True,

@@ -223,3 +223,102 @@ def test_written_reads_match_reference(tmp_path):
 def test_reverse_complement_matches_oracle():
     s = "ACGTNRYKMSWBDHVacgtn"
     assert reverse_complement(s.encode()).decode().upper() == O.reverse_complement(s).upper()
+
+
+def _all_records(path, fmt):
+    return sum(_chunks(path, fmt, 1000), [])
+
+
+@pytest.mark.parametrize("fmt", ["fastq", "fasta"])
+def test_shard_ranges_find_every_record_start(tmp_path, fmt):
+    """nt_reader_shard_range over N byte ranges of the concatenated plain files
+    (a directory of three files, one empty): the ranks' record starts are the
+    records of the unsharded reader, each exactly once, the chain check
+    first(r) == next(r - 1) holds, and a seek to any start reads that record.
+    FASTQ quality lines start with '@' and '+' (the resynchronisation must not
+    take them for headers), CRLF line ends, blank lines between records, empty
+    sequences; FASTA wraps at 60 with blank and ';' lines."""
+    rng = np.random.default_rng(17)
+    recs = [(f"r{i} x", "".join(rng.choice(list("ACGTN"), int(rng.integers(0 if i % 9 else 1, 400)))))
+            for i in range(90)]
+    d = tmp_path / "in"
+    d.mkdir()
+    if fmt == "fastq":
+        recs = [(n, s or "A") for n, s in recs]
+
+        def w(p, rs):
+            with open(p, "w", newline="") as f:
+                for i, (n, s) in enumerate(rs):
+                    q = "".join(rng.choice(list("@+I#"), len(s)))
+                    f.write(f"@{n}\r\n{s}\r\n+\r\n{q}\r\n" + ("\r\n" if i % 4 == 3 else ""))
+    else:
+        def w(p, rs):
+            with open(p, "w") as f:
+                for n, s in rs:
+                    f.write(f">{n}\n" + "".join(s[i:i + 60] + "\n" for i in range(0, len(s), 60)) + "\n;c\n")
+    w(d / "a", recs[:40])
+    (d / "b").write_bytes(b"")
+    w(d / "c", recs[40:])
+    want = _all_records(str(d), fmt)
+    assert want == recs
+    for world in (1, 2, 3, 7, 40, 300):
+        with Reader(str(d), fmt) as r:
+            plain, S = r.layout()
+            assert plain and S == sum(os.path.getsize(d / x) for x in "abc")
+            pos, prev_next = [], None
+            for k in range(world):
+                p, first, nxt = r.shard_range(S * k // world, S * (k + 1) // world)
+                if k:
+                    assert first == prev_next, (world, k)
+                assert all(S * k // world <= x < S * (k + 1) // world for x in p)
+                prev_next = nxt
+                pos += [int(x) for x in p]
+            assert prev_next == S
+            assert len(pos) == len(recs) and pos == sorted(pos)
+        for i in (0, 39, 40, 41, 89):
+            with Reader(str(d), fmt) as r:
+                r.layout()
+                r.seek_byte(pos[i])
+                ch = r.next_chunk(3)
+                assert [(ch.name(j), ch.seq(j).decode()) for j in range(ch.n)] == recs[i:i + 3]
+    with Reader(str(d), fmt) as r:
+        r.layout()
+        r.seek_byte(S)
+        assert r.next_chunk(5) is None
+
+
+def test_count_files_plan_and_record_seek(tmp_path):
+    """The run-directory form: per-file record counts (whole gzip parts on host
+    threads), a plan that names only some parts, seeks to (part, record) --
+    forward within the open part and into a later one -- and reads that
+    continue across the planned parts."""
+    rng = np.random.default_rng(23)
+    recs = [(f"q{i}", "".join(rng.choice(list("ACGT"), int(rng.integers(1, 300))))) for i in range(50)]
+    d = tmp_path / "run"
+    d.mkdir()
+    cuts = [0, 9, 9, 20, 31, 44, 50]
+    for k in range(len(cuts) - 1):
+        _write_fastq(d / f"p{k}.fastq.gz", recs[cuts[k]:cuts[k + 1]], gz=True)
+    with Reader(str(d), "fastq") as r:
+        assert r.layout()[0] is False
+        assert list(r.count_files([0, 1, 2, 3, 4, 5])) == [9, 0, 11, 11, 13, 6]
+        assert list(r.count_files([4])) == [13]
+    with Reader(str(d), "fastq") as r:
+        r.plan([0, 1, 2, 4, 5])
+        r.seek_record(0, 3)
+        ch = r.next_chunk(4)
+        assert [ch.name(j) for j in range(ch.n)] == [n for n, _ in recs[3:7]]
+        r.seek_record(0, 8)  # forward in the open part, then on across the empty part 1
+        ch = r.next_chunk(3)
+        assert [ch.name(j) for j in range(ch.n)] == [n for n, _ in recs[8:11]]
+        r.seek_record(4, 12)  # part 3 is not in the plan: skipped
+        ch = r.next_chunk(5)
+        assert [ch.name(j) for j in range(ch.n)] == [n for n, _ in recs[43:48]]
+        from nanotel_amd import NanoTelError
+        with pytest.raises(NanoTelError):
+            r.seek_record(3, 0)  # outside the plan
+    with Reader(str(d), "fastq") as r:
+        r.next_chunk(1)
+        from nanotel_amd import NanoTelError
+        with pytest.raises(NanoTelError):
+            r.plan([0])  # only before the first read
