@@ -197,6 +197,18 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
  * reference processes its chunks one after another (NanoTel.R:2171-2268);
  * this only overlaps the device work of consecutive ones. */
 int nt_set_pipelined(nt_ctx* ctx, int on);
+/* Pipelined only: a call's INPUTS (planes, lengths, offsets, exception
+ * lists, the T-layout and bundle lists) are read by its last calling kernel
+ * after nt_scan_call returns, so they must not be overwritten (or freed) until
+ * that calling is done.  nt_wait_call(ctx, back) makes the context stream wait
+ * for the calling of the call `back` calls before the latest one (0 = the
+ * latest, 1 = the one before); work enqueued on the context stream after it
+ * may then overwrite that call's inputs.  A caller refilling ONE input set
+ * waits with back = 0 before each refill; one alternating two input sets
+ * waits with back = 1 (keeping the overlap).  Calls further back (back >= 2)
+ * are already ordered on the context stream: each call's scans wait for the
+ * calling of the call two before it.  nt_join waits for all of them. */
+int nt_wait_call(nt_ctx* ctx, uint32_t back);
 int nt_join(nt_ctx* ctx);
 
 /* Measurement: with profiling on, every nt_scan_call records HIP events on
@@ -212,6 +224,14 @@ int64_t nt_kernel_times(nt_ctx* ctx, double* scan_ms, double* call_ms);
 /* Scan-kernel launches (bundle-scan ranges count one each) behind the last
  * nt_kernel_times: scan_ms / this = the scan kernel's average launch. */
 int64_t nt_kernel_launches(const nt_ctx* ctx);
+/* The calling kernels' own spans behind the last nt_kernel_times (events on
+ * the stream each ran on, so a calling kernel hidden beside a scan range is
+ * timed too): *call_ms = their sum; returns how many launches. */
+int64_t nt_call_kernel_times(const nt_ctx* ctx, double* call_ms);
+/* Calling-kernel launches since nt_create: out[0] ahead-of-time, out[1] the
+ * specialised (hiprtc) kernel -- a benchmark checks that none of its timed
+ * launches fell back to the ahead-of-time kernel. */
+int nt_call_launch_counts(const nt_ctx* ctx, int64_t* out2);
 /* 1 if the last nt_scan_call ran the calling kernel specialised for the
  * program's patterns (hiprtc; batches of >= 65,536 reads once it is built,
  * every batch with NT_CALL_JIT=1), 0 for the ahead-of-time one (same results). */

@@ -169,6 +169,13 @@ struct nt_ctx {
   std::vector<std::array<hipEvent_t, 3 + 2 * (kMaxTsub + 1)>> ev;  // + the per-read scan of list reads
   std::vector<int> ev_nt;  // bundle-scan ranges of each recorded call
   int64_t last_launches = 0;  // scan-kernel launches of the last nt_kernel_times window
+  // the calling kernels' own spans (events on the stream each runs on) of the
+  // recorded calls: per call up to kMaxTsub + 1 launches
+  std::vector<std::array<hipEvent_t, 2 * (kMaxTsub + 2)>> cev;
+  std::vector<int> cev_n;
+  double last_call_ms = 0.0;      // their sum over the last nt_kernel_times window
+  int64_t last_call_launches = 0;
+  int64_t call_launches[2] = {0, 0};  // calling launches since nt_create: [0] ahead-of-time, [1] specialised
   size_t n_ev = 0;  // calls recorded since the last nt_kernel_times
   bool jit = false;  // hiprtc-specialised scan kernels (nt_jit.cpp)
   void* jit_fn[4] = {};  // [no hit counters ? 2 : 0] + [global scratch ? 1 : 0]
@@ -270,10 +277,25 @@ static hipError_t launch_call(nt_ctx* ctx, void* cfn, const NtBatch* B, const Nt
   const uint32_t* thr = (const uint32_t*)ctx->thr.p;
   const uint32_t ts = (uint32_t)ctx->thr_h.size();
   const int np = ctx->prog.n_pass;
-  if (cfn) return nt_cjit_launch(cfn, np, ctx->cu_count, s, ctx->prog_dev, B, O, tm, thr, ts, fix_last);
-  const uint64_t lanes = (B->list ? B->n_list : B->n_reads) * (np <= 2 ? 2u : 4u);
-  const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((lanes + 255) / 256, (uint64_t)ctx->cu_count * 64));
-  return nt_dev_launch_call(ctx->prog_dev, B, O, tm, thr, ts, fix_last, long_tvr(ctx->prog), grid, s);
+  ++ctx->call_launches[cfn ? 1 : 0];
+  // profiling: events around the calling kernel on its own stream (its span,
+  // whether or not a scan runs beside it)
+  hipEvent_t* ce = nullptr;
+  if (ctx->profile && ctx->n_ev > 0 && ctx->cev_n[ctx->n_ev - 1] < nt_ctx::kMaxTsub + 2) {
+    const int k = ctx->cev_n[ctx->n_ev - 1]++;
+    ce = &ctx->cev[ctx->n_ev - 1][2 * k];
+    (void)hipEventRecord(ce[0], s);
+  }
+  hipError_t e;
+  if (cfn) {
+    e = nt_cjit_launch(cfn, np, ctx->cu_count, s, ctx->prog_dev, B, O, tm, thr, ts, fix_last);
+  } else {
+    const uint64_t lanes = (B->list ? B->n_list : B->n_reads) * (np <= 2 ? 2u : 4u);
+    const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((lanes + 255) / 256, (uint64_t)ctx->cu_count * 64));
+    e = nt_dev_launch_call(ctx->prog_dev, B, O, tm, thr, ts, fix_last, long_tvr(ctx->prog), grid, s);
+  }
+  if (ce) (void)hipEventRecord(ce[1], s);
+  return e;
 }
 
 static int hip_fail(nt_ctx* ctx, hipError_t e, const char* what) {
@@ -351,6 +373,15 @@ int nt_join(nt_ctx* ctx) {
       (e = hipStreamWaitEvent(ctx->stream, ctx->ev_call, 0)) != hipSuccess)
     return hip_fail(ctx, e, "nt_join");
   return NT_OK;
+}
+
+int nt_wait_call(nt_ctx* ctx, uint32_t back) {
+  if (!ctx) return NT_E_ARG;
+  if (!ctx->pipelined || !ctx->ev_done[0] || back >= 2 || ctx->pipe_i < 1 + (uint64_t)back) return NT_OK;
+  (void)hipSetDevice(ctx->device);
+  // call c = pipe_i - 1 - back recorded ev_done[c & 1] after its last calling
+  const hipError_t e = hipStreamWaitEvent(ctx->stream, ctx->ev_done[(ctx->pipe_i - 1 - back) & 1], 0);
+  return e == hipSuccess ? NT_OK : hip_fail(ctx, e, "nt_wait_call");
 }
 
 int nt_set_pipelined(nt_ctx* ctx, int on) {
@@ -482,7 +513,14 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
   auto wg_bytes = [&](uint32_t nwc) { return (uint64_t)nt_dev_wave_words(noslots, nh, np, nwc) * 4u * 4u; };
   uint32_t cap_nw = max_nw;
   uint64_t len_cap = max_len;
-  if (wg_bytes(max_nw) > kLdsCapBytes) {
+  // the ahead-of-time scan keeps n_hits x 64 hit counters per wave in LDS:
+  // from ~32 patterns on not even a read of no window fits the workgroup's
+  // LDS, and every read takes the global-scratch instantiation
+  const bool lds_fits = wg_bytes(0) <= kLdsCapBytes;
+  if (!lds_fits) {
+    cap_nw = 0;
+    len_cap = 0;
+  } else if (wg_bytes(max_nw) > kLdsCapBytes) {
     uint32_t lo = 0, hi = max_nw;
     while (lo < hi) {
       const uint32_t mid = (lo + hi + 1) / 2;
@@ -561,11 +599,17 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
       std::array<hipEvent_t, 3 + 2 * (nt_ctx::kMaxTsub + 1)> a{};
       for (hipEvent_t& x : a)
         if ((e = hipEventCreate(&x)) != hipSuccess) return hip_fail(ctx, e, "hipEventCreate");
+      std::array<hipEvent_t, 2 * (nt_ctx::kMaxTsub + 2)> c{};
+      for (hipEvent_t& x : c)
+        if ((e = hipEventCreate(&x)) != hipSuccess) return hip_fail(ctx, e, "hipEventCreate");
       ctx->ev.push_back(a);
       ctx->ev_nt.push_back(0);
+      ctx->cev.push_back(c);
+      ctx->cev_n.push_back(0);
     }
     ev = ctx->ev[ctx->n_ev++].data();
     ctx->ev_nt[ctx->n_ev - 1] = 0;
+    ctx->cev_n[ctx->n_ev - 1] = 0;
     (void)hipEventRecord(ev[0], ctx->stream);
   }
   if ((e = hipMemsetAsync(queue, 0, nqueue * NT_QUEUE_WORDS * 8, ctx->stream)) != hipSuccess) return hip_fail(ctx, e, "hipMemsetAsync(queue)");
@@ -680,7 +724,7 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
     // timed launch of the scan kernels (nt_kernel_times)
     const int pe = (ev && tscan && n_scan > 0) ? ctx->ev_nt[ctx->n_ev - 1] : -1;
     if (pe >= 0) (void)hipEventRecord(ev[3 + 2 * pe], ctx->stream);
-    if (dbg_skip_scan || n_scan == 0)
+    if (dbg_skip_scan || n_scan == 0 || !lds_fits)
       e = hipSuccess;
     else if (ctx->jit)
       e = nt_jit_launch(jit_lds, (int)grid, lds_bytes, ctx->stream, ctx->prog_dev,
@@ -823,6 +867,19 @@ int nt_call_jit_wait(nt_ctx* ctx) {
 
 int64_t nt_kernel_launches(const nt_ctx* ctx) { return ctx ? ctx->last_launches : NT_E_ARG; }
 
+int64_t nt_call_kernel_times(const nt_ctx* ctx, double* call_ms) {
+  if (!ctx) return NT_E_ARG;
+  if (call_ms) *call_ms = ctx->last_call_ms;
+  return ctx->last_call_launches;
+}
+
+int nt_call_launch_counts(const nt_ctx* ctx, int64_t* out2) {
+  if (!ctx || !out2) return NT_E_ARG;
+  out2[0] = ctx->call_launches[0];
+  out2[1] = ctx->call_launches[1];
+  return NT_OK;
+}
+
 int nt_set_profiling(nt_ctx* ctx, int on) {
   if (!ctx) return NT_E_ARG;
   ctx->profile = on != 0;
@@ -857,6 +914,21 @@ int64_t nt_kernel_times(nt_ctx* ctx, double* scan_ms, double* call_ms) {
     a += x;
     b += y;
   }
+  double cms = 0.0;
+  int64_t cl = 0;
+  for (size_t i = 0; i < ctx->n_ev; ++i) {
+    for (int k = 0; k < ctx->cev_n[i]; ++k) {
+      hipEvent_t* ce = &ctx->cev[i][2 * k];
+      hipError_t e = hipEventSynchronize(ce[1]);
+      float z = 0.f;
+      if (e == hipSuccess) e = hipEventElapsedTime(&z, ce[0], ce[1]);
+      if (e != hipSuccess) return hip_fail(ctx, e, "hipEventElapsedTime(call)");
+      cms += z;
+      ++cl;
+    }
+  }
+  ctx->last_call_ms = cms;
+  ctx->last_call_launches = cl;
   if (scan_ms) *scan_ms = a;
   if (call_ms) *call_ms = b;
   ctx->last_launches = launches;

@@ -260,33 +260,14 @@ void cache_write(const std::string& dir, const std::string& path, const std::vec
 }
 
 // The code object of src for arch (--offload-arch=...): from the on-disk
-// cache, else compiled by hiprtc (and cached).
-bool get_code(const std::string& arch, const std::string& src, std::vector<char>& code, std::string& err) {
+// cache (unless fresh), else compiled by hiprtc (and cached).  The cache key
+// hashes the source, the embedded headers and every compiler option (the
+// fixed ones below included: -ffp-contract decides the fp64 densities'
+// rounding), plus the hiprtc version.  *cpath_out: the cache file used.
+bool get_code(const std::string& arch, const std::string& src, std::vector<char>& code, std::string& err,
+              bool fresh = false, std::string* cpath_out = nullptr) {
   const char* hdrs[] = {kJitCommon, kJitDevice, kJitScan, kJitTScan, kJitCall};
   const char* names[] = {"nt_common.h", "nt_device.h", "nt_scan.h", "nt_tscan.h", "nt_call.h"};
-  const std::string dir = cache_dir();
-  std::string cpath;
-  if (!dir.empty()) {
-    uint64_t h = 1469598103934665603ull;
-    h = fnv1a(h, src.data(), src.size());
-    for (const char* x : hdrs) h = fnv1a(h, x, std::strlen(x));
-    h = fnv1a(h, arch.data(), arch.size());
-    const char* xo = std::getenv("NT_JIT_OPTS");
-    if (xo) h = fnv1a(h, xo, std::strlen(xo));
-    int maj = 0, mnr = 0;
-    (void)hiprtcVersion(&maj, &mnr);
-    h = fnv1a(h, &maj, sizeof maj);
-    h = fnv1a(h, &mnr, sizeof mnr);
-    char hex[24];
-    std::snprintf(hex, sizeof hex, "%016llx", (unsigned long long)h);
-    cpath = dir + "/nt_" + hex + ".co";
-    if (cache_read(cpath, code)) return true;
-  }
-  hiprtcProgram prog;
-  if (hiprtcCreateProgram(&prog, src.c_str(), "nt_jit.hip", 5, hdrs, names) != HIPRTC_SUCCESS) {
-    err = "hiprtcCreateProgram failed";
-    return false;
-  }
   std::vector<std::string> extra;  // NT_JIT_OPTS: extra compiler options (tuning experiments)
   if (const char* v = std::getenv("NT_JIT_OPTS")) {
     std::string t;
@@ -306,6 +287,28 @@ bool get_code(const std::string& arch, const std::string& src, std::vector<char>
   std::vector<const char*> opts = {arch.c_str(), "-O3", "-std=c++17", "-ffp-contract=off", "-mllvm",
                                    "-amdgpu-sched-strategy=max-ilp"};
   for (const std::string& x : extra) opts.push_back(x.c_str());
+  const std::string dir = cache_dir();
+  std::string cpath;
+  if (!dir.empty()) {
+    uint64_t h = 1469598103934665603ull;
+    h = fnv1a(h, src.data(), src.size());
+    for (const char* x : hdrs) h = fnv1a(h, x, std::strlen(x));
+    for (const char* o : opts) h = fnv1a(h, o, std::strlen(o) + 1);  // NUL-separated
+    int maj = 0, mnr = 0;
+    (void)hiprtcVersion(&maj, &mnr);
+    h = fnv1a(h, &maj, sizeof maj);
+    h = fnv1a(h, &mnr, sizeof mnr);
+    char hex[24];
+    std::snprintf(hex, sizeof hex, "%016llx", (unsigned long long)h);
+    cpath = dir + "/nt_" + hex + ".co";
+    if (cpath_out) *cpath_out = cpath;
+    if (!fresh && cache_read(cpath, code)) return true;
+  }
+  hiprtcProgram prog;
+  if (hiprtcCreateProgram(&prog, src.c_str(), "nt_jit.hip", 5, hdrs, names) != HIPRTC_SUCCESS) {
+    err = "hiprtcCreateProgram failed";
+    return false;
+  }
   const hiprtcResult rc = hiprtcCompileProgram(prog, (int)opts.size(), opts.data());
   if (rc != HIPRTC_SUCCESS) {
     size_t n = 0;
@@ -338,8 +341,17 @@ std::string device_arch(int device) {
 // src as a loaded module on the calling thread's device
 bool compile_module(int device, const std::string& src, hipModule_t& mod, std::string& err) {
   std::vector<char> code;
-  if (!get_code(device_arch(device), src, code, err)) return false;
-  const hipError_t he = hipModuleLoadData(&mod, code.data());
+  std::string cpath;
+  const std::string arch = device_arch(device);
+  if (!get_code(arch, src, code, err, false, &cpath)) return false;
+  hipError_t he = hipModuleLoadData(&mod, code.data());
+  if (he != hipSuccess && !cpath.empty()) {
+    // a cached object the runtime rejects (truncated, another runtime's):
+    // dropped and compiled afresh, once
+    (void)std::remove(cpath.c_str());
+    if (!get_code(arch, src, code, err, true)) return false;
+    he = hipModuleLoadData(&mod, code.data());
+  }
   if (he != hipSuccess) {
     err = std::string("hipModuleLoadData: ") + hipGetErrorString(he);
     return false;

@@ -88,6 +88,7 @@ SIGNATURES = {
     "nt_synchronize": (ctypes.c_int, [_P]),
     "nt_set_pipelined": (ctypes.c_int, [_P, ctypes.c_int]),
     "nt_join": (ctypes.c_int, [_P]),
+    "nt_wait_call": (ctypes.c_int, [_P, ctypes.c_uint32]),
     "nt_compile": (ctypes.c_int, [_P, ctypes.POINTER(NtParams), ctypes.POINTER(NtProgramInfo)]),
     "nt_window_count": (ctypes.c_int64, [ctypes.c_int64, ctypes.c_int32]),
     "nt_window_rows": (ctypes.c_uint64, [ctypes.c_int64]),
@@ -105,6 +106,8 @@ SIGNATURES = {
     "nt_kernel_times": (ctypes.c_int64, [_P, ctypes.POINTER(ctypes.c_double),
                                          ctypes.POINTER(ctypes.c_double)]),
     "nt_kernel_launches": (ctypes.c_int64, [_P]),
+    "nt_call_kernel_times": (ctypes.c_int64, [_P, ctypes.POINTER(ctypes.c_double)]),
+    "nt_call_launch_counts": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int64)]),
     "nt_call_jit_state": (ctypes.c_int, [_P]),
     "nt_call_jit_wait": (ctypes.c_int, [_P]),
     "nt_jit_prebuild": (ctypes.c_int, [ctypes.POINTER(NtParams), ctypes.c_char_p]),

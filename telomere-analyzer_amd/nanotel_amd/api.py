@@ -111,6 +111,19 @@ class NanoTel:
         ranges launches once per range): scan_ms / this = one launch."""
         return int(_check(lib().nt_kernel_launches(self._h), self._h))
 
+    def call_kernel_times(self):
+        """(calling launches, their summed own span in ms) behind the last
+        kernel_times(): events on the stream each calling kernel ran on."""
+        ms = ctypes.c_double()
+        n = _check(lib().nt_call_kernel_times(self._h, ctypes.byref(ms)), self._h)
+        return int(n), ms.value
+
+    def call_launch_counts(self):
+        """Calling-kernel launches since creation: (ahead-of-time, specialised)."""
+        out = (ctypes.c_int64 * 2)()
+        _check(lib().nt_call_launch_counts(self._h, out), self._h)
+        return int(out[0]), int(out[1])
+
     def call_jit(self):
         """True if the last scan_call() ran the calling kernel specialised for
         the patterns (hiprtc), False for the ahead-of-time one."""
@@ -136,6 +149,12 @@ class NanoTel:
         complete after join() / synchronize().  Consecutive calls need their
         own output buffers."""
         _check(lib().nt_set_pipelined(self._h, int(bool(on))), self._h)
+
+    def wait_call(self, back=0):
+        """nt_wait_call: the context stream waits until the calling of the call
+        `back` calls before the latest one is done (its inputs may then be
+        overwritten by work enqueued on the context stream)."""
+        _check(lib().nt_wait_call(self._h, int(back)), self._h)
 
     def join(self):
         """nt_join: the launch stream waits for every calling launched so far."""

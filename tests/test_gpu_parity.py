@@ -199,6 +199,25 @@ def test_many_patterns(cfg, jit):
         assert nt.tscan == (cfg is MANY[0])  # equal-length lists take the bundle scan
 
 
+def _n_mers(k, n, seed):
+    rng = np.random.default_rng(seed)
+    out = ["TTAGGG"]
+    while len(out) < n:
+        m = "".join(rng.choice(list("ACGT"), k))
+        if m not in out:
+            out.append(m)
+    return " ".join(out)
+
+
+def test_many_patterns_aot_lds_overflow():
+    """33 patterns + 2 TVRs (68 hit counters): the ahead-of-time per-read scan
+    keeps 64 hit counters per wave and counter in LDS, more than a workgroup
+    may take even for a read without windows -- every read goes to the
+    global-scratch instantiation instead of a failing LDS launch."""
+    cfg = dict(patterns=_n_mers(6, 33, 5), tvr_patterns="TGAGGG TTGGGG")
+    _random_reads(cfg, False, check_tscan=False)
+
+
 def test_many_patterns_specialised_call(monkeypatch):
     monkeypatch.setenv("NT_CALL_JIT", "1")
     nt = _random_reads(MANY[0], True, check_tscan=False)
@@ -562,6 +581,74 @@ def test_pipelined_batches_match_serial():
             else:
                 assert torch.equal(o[k], r[k]), (i, k)
     assert int((refs[0]["flags"] & 1).sum()) > 1000  # telomeric reads: the calling did work
+    nt.close()
+
+
+@pytest.mark.parametrize("back", [0, 1], ids=["one_input_set", "two_input_sets"])
+def test_pipelined_calls_with_rewritten_inputs(back):
+    """Pipelined calls whose INPUTS are rewritten between calls: a
+    caller with one input set waits for the previous call's calling
+    (nt_wait_call(ctx, 0)) before refilling it on the context stream; one with
+    two alternating sets waits for the call before that (back = 1), keeping the
+    overlap.  Every call's outputs equal the serial calls' bit for bit."""
+    import torch
+    from nanotel_amd import synth_params
+    from nanotel_amd.api import DeviceBundles
+    n, read_len = 8192, 10000
+    nt = _nt(patterns="TTAGGG")
+    st = torch.cuda.Stream()
+    nt.set_stream(st.cuda_stream)
+    batches = []
+    with torch.cuda.stream(st):
+        for first in (0, 70000, 140000):
+            t = _device_batch(nt, synth_params(read_len=read_len, first_read=first), n, read_len, hits=False)
+            b, keep = _device_bundles(nt, t, n, read_len)
+            batches.append((t, b, keep))
+        keys = ("start", "end", "dens", "flags", "wc")
+
+        def run(t, b, o):
+            nt.scan_call_device(t["planes"].data_ptr(), t["blk_off"].data_ptr(), t["lens"].data_ptr(),
+                                t["win_off"].data_ptr(), n, n * t["rows"], read_len, o["start"].data_ptr(),
+                                o["end"].data_ptr(), o["dens"].data_ptr(), o["flags"].data_ptr(),
+                                o["wc"].data_ptr(), bundles=b)
+
+        refs = []
+        for t, b, _ in batches:
+            o = {k: torch.full_like(t[k], 0x55) for k in keys}
+            run(t, b, o)
+            nt.synchronize()
+            refs.append(o)
+        # the input sets the caller rewrites: planes and T-layout (the uniform
+        # layout and the bundle lists are the same for every batch here)
+        sets = []
+        for _ in range(back + 1):
+            t0, _, k0 = batches[0]
+            x = dict(t0)
+            x["planes"] = torch.empty_like(t0["planes"])
+            tpl = torch.empty_like(k0["tplanes"])
+            xb = DeviceBundles(tpl.data_ptr(), k0["bnd_read"].data_ptr(), k0["bnd_stripe"].data_ptr(),
+                               batches[0][1].n_bundles, 0, 0, batches[0][1].tplane_bytes)
+            sets.append((x, xb, tpl))
+        order = [0, 1, 2, 0, 2, 1]
+        outs = [{k: torch.full_like(batches[i][0][k], 0x55) for k in keys} for i in order]
+        nt.set_pipelined(True)
+        for c, (i, o) in enumerate(zip(order, outs)):
+            x, xb, tpl = sets[c % len(sets)]
+            if c >= len(sets):
+                nt.wait_call(back)  # the calling that still reads this set
+            x["planes"].copy_(batches[i][0]["planes"])
+            tpl.copy_(batches[i][2]["tplanes"])
+            run(x, xb, o)
+        nt.join()
+        nt.synchronize()
+        nt.set_pipelined(False)
+    for i, o in zip(order, outs):
+        t, r = batches[i][0], refs[i]
+        for k in keys:
+            if k == "wc":
+                assert torch.equal(_valid_counts(t, n, nt.n_pass, o[k]), _valid_counts(t, n, nt.n_pass, r[k])), (i, k)
+            else:
+                assert torch.equal(o[k], r[k]), (i, k)
     nt.close()
 
 

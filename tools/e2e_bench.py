@@ -25,33 +25,56 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "telomere-analyzer_amd"))
 
 
-def write_input(path, n, L, gz, seed=20260501, parts=1):
-    """One file, or with parts > 1 a run directory of `parts` files (as a
-    sequencer writes them: fastq_pass/part_000.fastq.gz, ...)."""
+def _pool(L, seed, k=512):
+    """k distinct synthetic FASTQ bodies (sequence + quality lines) of length L."""
     rng = np.random.default_rng(seed)
     acgt = np.frombuffer(b"ACGT", np.uint8)
     unit = np.frombuffer(b"TTAGGG", np.uint8)
+    out = []
+    for _ in range(k):
+        s = acgt[rng.integers(0, 4, L)]
+        if rng.random() < 0.5:
+            t = min(L, int(rng.integers(1000, 15001)))
+            tract = np.resize(unit, t)
+            sub = rng.random(t) < 0.02
+            tract[sub] = acgt[rng.integers(0, 4, int(sub.sum()))]
+            s[:t] = tract
+        out.append(b"\n" + s.tobytes() + b"\n+\n" + b"I" * L + b"\n")
+    return out
+
+
+def _write_part(args):
+    name, r0, r1, L, gz, seed = args
+    pool = _pool(L, seed)
+    op = (lambda p, m: gzip.open(p, m, compresslevel=1)) if gz else open
+    with op(name, "wb") as f:
+        buf = []
+        for r in range(r0, r1):
+            buf.append(b"@read_%d" % r + pool[r % len(pool)])
+            if len(buf) == 256:
+                f.write(b"".join(buf))
+                buf = []
+        f.write(b"".join(buf))
+
+
+def write_input(path, n, L, gz, seed=20260501, parts=1):
+    """One file, or with parts > 1 a run directory of `parts` files (as a
+    sequencer writes them: fastq_pass/part_000.fastq.gz, ...).  The reads
+    cycle through a pool of 512 synthetic ones (names stay unique); the parts
+    are written by parallel processes."""
     if parts > 1:
         os.makedirs(path, exist_ok=True)
         names = [os.path.join(path, "part_%03d.fastq%s" % (k, ".gz" if gz else "")) for k in range(parts)]
     else:
         names = [path]
     per = (n + len(names) - 1) // len(names)
-    r = 0
-    for name in names:
-        op = (lambda p, m: gzip.open(p, m, compresslevel=1)) if gz else open
-        with op(name, "wb") as f:
-            for _ in range(min(per, n - r)):
-                s = acgt[rng.integers(0, 4, L)]
-                if rng.random() < 0.5:
-                    t = min(L, int(rng.integers(1000, 15001)))
-                    tract = np.resize(unit, t)
-                    sub = rng.random(t) < 0.02
-                    tract[sub] = acgt[rng.integers(0, 4, int(sub.sum()))]
-                    s[:t] = tract
-                q = b"I" * L
-                f.write(b"@read_%d\n" % r + s.tobytes() + b"\n+\n" + q + b"\n")
-                r += 1
+    jobs = [(nm, k * per, min(n, (k + 1) * per), L, gz, seed) for k, nm in enumerate(names)]
+    if len(jobs) > 1:
+        import multiprocessing as mp
+        with mp.get_context("spawn").Pool(min(16, len(jobs))) as pool:
+            pool.map(_write_part, jobs)
+    else:
+        _write_part(jobs[0])
 
 
 def main():
@@ -64,6 +87,7 @@ def main():
     ap.add_argument("--parts", type=int, default=1, help="write the input as a directory of this many files")
     ap.add_argument("--dir", default="/tmp/nt_e2e")
     ap.add_argument("--profile", default="", help="cProfile the summary-only run into this file (text)")
+    ap.add_argument("--no-reads-run", action="store_true", help="skip the run that writes reads/*.fasta.gz")
     a = ap.parse_args()
     os.makedirs(a.dir, exist_ok=True)
     inp = os.path.join(a.dir, "run" if a.parts > 1 else "reads.fastq" + (".gz" if a.gz else ""))
@@ -79,7 +103,7 @@ def main():
     # warm-up (hiprtc specialisation, device buffers) on a small prefix-free run
     driver.run(inp, os.path.join(a.dir, "warm"), "TTAGGG", fmt="fastq", nrec=10000, write_reads=False,
                plot=False, log=lambda *x: None)
-    runs = [("summary_only", False, False), ("with_reads_fasta_gz", True, False)]
+    runs = [("summary_only", False, False)] + ([] if a.no_reads_run else [("with_reads_fasta_gz", True, False)])
     if a.plots:
         runs.append(("with_reads_and_plots", True, True))
     for key, write_reads, plot in runs:

@@ -14,6 +14,6 @@ for spec in "$@"; do
   ( for kv in $spec; do k=${kv%%=*}; v=${kv#*=}; export "$k=${v//+/ }"; done
     timeout -k 10 300 python bench.py --no-cpu-baseline ${BENCH_ARGS:-} ) > $log 2>&1
   st=$?
-  python3 -c "import json; d=json.loads(open('$log').read().strip().splitlines()[-1]); r=d['roofline']; print('value', d['value'], 'ms', d['ms_per_step'], 'scan', r['kernel_avg_ms'], 'call', r['call_kernel_avg_ms'])" || tail -3 $log
+  python3 -c "import json; d=json.loads(open('$log').read().strip().splitlines()[-1]); r=d['roofline']; print('value', d['value'], 'ms', d['ms_per_step'], 'scan', r['kernel_avg_ms'], 'call', r.get('call_exposed_ms'), 'callk', r['call_kernel_avg_ms'])" || tail -3 $log
   if [ $st -eq 124 ] || [ $st -gt 128 ]; then echo "status $st: stopping"; break; fi
 done
