@@ -385,10 +385,15 @@ def render_eps(ops):
 _JPEG_FONTS = {}  # (face, size) -> PIL font, loaded once per process
 
 
-def render_jpeg(ops, W, H, path):
-    """Rasterise the same device operations with PIL (y flipped, 1 pt = 1 px)."""
+def render_jpeg(ops, W, H, path, S=3):
+    """Rasterise the same device operations with PIL (y flipped, 1 pt = 1 px at
+    R's 72 dpi), as R's cairo jpeg() device does: anti-aliased -- drawn at S
+    times the size and box-filtered down --, lines of lwd 1 = 1/96 in = 0.75 px,
+    and text set to the Helvetica widths the layout was computed with (the
+    DejaVu glyphs, the only TrueType face here, scaled horizontally to them;
+    R's device substitutes a Helvetica-metric face)."""
     from PIL import Image, ImageDraw, ImageFont
-    img = Image.new("RGB", (int(W), int(H)), (255, 255, 255))
+    img = Image.new("RGB", (int(W) * S, int(H) * S), (255, 255, 255))
     dr = ImageDraw.Draw(img)
     fonts = _JPEG_FONTS
 
@@ -406,12 +411,18 @@ def render_jpeg(ops, W, H, path):
 
     clip = (0.0, 0.0, W, H)
 
-    def fy(y):
-        return H - y
+    def P(x, y):
+        return (x * S, (H - y) * S)
+
+    def width(st):
+        return max(1, int(round(0.75 * S * st.get("lwd", 1.0))))
 
     def inside(x0, y0, x1, y1):
         return not (max(x0, x1) < clip[0] or min(x0, x1) > clip[2] or max(y0, y1) < clip[1]
                     or min(y0, y1) > clip[3])
+
+    def cl(x, y):
+        return min(max(x, clip[0]), clip[2]), min(max(y, clip[1]), clip[3])
 
     for op in ops:
         kind = op[0]
@@ -419,42 +430,53 @@ def render_jpeg(ops, W, H, path):
             clip = op[1]
         elif kind == "polygon":
             xs, ys, fill, col, st = op[1:]
-            pts = [(min(max(x, clip[0]), clip[2]), fy(min(max(y, clip[1]), clip[3])))
-                   for x, y in zip(xs, ys) if not (math.isnan(x) or math.isnan(y))]
+            pts = [P(*cl(x, y)) for x, y in zip(xs, ys) if not (math.isnan(x) or math.isnan(y))]
             if len(pts) >= 3:
-                dr.polygon(pts, fill=fill, outline=col)
+                if fill is not None:
+                    dr.polygon(pts, fill=fill)
+                if col is not None:
+                    dr.line(pts + [pts[0]], fill=col, width=width(st), joint="curve")
         elif kind == "line":
             x0, y0, x1, y1, col, st = op[1:]
             if inside(x0, y0, x1, y1):
-                wd = max(1, int(round(st["lwd"])))
+                wd = width(st)
                 if st["lty"]:  # lty 2: 4 on, 4 off (in units of the line width * 0.75 pt)
                     ln = math.hypot(x1 - x0, y1 - y0)
                     step = 4 * 0.75 * st["lwd"]
                     t = 0.0
                     while t < ln:
                         u = min(ln, t + step)
-                        dr.line([(x0 + (x1 - x0) * t / ln, fy(y0 + (y1 - y0) * t / ln)),
-                                 (x0 + (x1 - x0) * u / ln, fy(y0 + (y1 - y0) * u / ln))], fill=col, width=wd)
+                        dr.line([P(x0 + (x1 - x0) * t / ln, y0 + (y1 - y0) * t / ln),
+                                 P(x0 + (x1 - x0) * u / ln, y0 + (y1 - y0) * u / ln)], fill=col, width=wd)
                         t += 2 * step
                 else:
-                    dr.line([(x0, fy(y0)), (x1, fy(y1))], fill=col, width=wd)
+                    dr.line([P(x0, y0), P(x1, y1)], fill=col, width=wd)
         elif kind == "rect":
             x0, y0, x1, y1, fill, col, st = op[1:]
-            xa, xb = sorted((max(min(x0, clip[2]), clip[0]), max(min(x1, clip[2]), clip[0])))
-            ya, yb = sorted((fy(max(min(y0, clip[3]), clip[1])), fy(max(min(y1, clip[3]), clip[1]))))
+            (xa, ya), (xb, yb) = P(*cl(x0, y0)), P(*cl(x1, y1))
+            xa, xb = sorted((xa, xb))
+            ya, yb = sorted((ya, yb))
             if xb > xa or fill is not None:
-                dr.rectangle([xa, ya, xb, yb], fill=fill, outline=col)
+                if fill is not None:
+                    dr.rectangle([xa, ya, xb, yb], fill=fill)
+                if col is not None:
+                    dr.line([(xa, ya), (xb, ya), (xb, yb), (xa, yb), (xa, ya)], fill=col, width=width(st))
         elif kind == "text":
             x, y, s, hadj, rot, face, cex, col = op[1:]
-            f = font(face, _fsize(cex))
-            w = dr.textlength(s, font=f)
+            size = _fsize(cex)
+            f = font(face, size * S)
+            target = max(1, int(round(str_width(s, face, size) * S)))  # Helvetica width, px
+            asc, desc = f.getmetrics()
+            tmp = Image.new("RGBA", (int(dr.textlength(s, font=f)) + 2, asc + desc), (255, 255, 255, 0))
+            ImageDraw.Draw(tmp).text((0, asc), s, font=f, fill=col, anchor="ls")
+            tmp = tmp.resize((target, tmp.height), Image.BILINEAR)
+            bx, by = P(x, y)
             if rot == 90:
-                tmp = Image.new("RGBA", (int(w) + 2, _fsize(cex) + 6), (255, 255, 255, 0))
-                ImageDraw.Draw(tmp).text((0, 0), s, font=f, fill=col)
                 tmp = tmp.rotate(90, expand=True)
-                img.paste(tmp, (int(x - 0.8 * _fsize(cex)), int(fy(y) - hadj * tmp.height)), tmp)
+                img.paste(tmp, (int(round(bx - asc)), int(round(by - (1.0 - hadj) * target))), tmp)
             else:
-                dr.text((x - hadj * w, fy(y) - _fsize(cex)), s, font=f, fill=col)
+                img.paste(tmp, (int(round(bx - hadj * target)), int(round(by - asc))), tmp)
+    img = img.resize((int(W), int(H)), Image.BOX)
     img.save(path, "JPEG", quality=75)
 
 

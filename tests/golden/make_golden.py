@@ -8,6 +8,8 @@ Outputs (all *data*, no reference source):
   example_summary.csv             -- Example/Example_output/summary.csv (2023 code version)
   reads/{1..4}.fasta              -- Example/Example_output/reads/*.fasta (written telomeric reads)
   eps/read{1..4}.eps              -- Example/Example_output/single_read_plots_adj/read*.eps (plots)
+  jpeg_adj/read{1..4}.jpeg        -- Example/Example_output/single_read_plots_adj/read*.jpeg (R's
+                                     cairo jpeg() of the same plots; pixel parity, tests/test_plots.py)
   example_window_counts.json      -- per-window covered-base counts for P1 (exact)
                                      and P2 (1 mismatch), decoded from the density
                                      polygons of Example_output/single_read_plots_adj/read*.eps
@@ -89,6 +91,10 @@ def main():
         shutil.copyfile(os.path.join(REF, "Example_output", "reads", f"{serial}.fasta"),
                         os.path.join(HERE, "reads", f"{serial}.fasta"))
     # the single-read EPS plots as the reference wrote them (expected outputs of plots.py)
+    os.makedirs(os.path.join(HERE, "jpeg_adj"), exist_ok=True)
+    for serial in range(1, 5):
+        shutil.copyfile(os.path.join(REF, "Example_output", "single_read_plots_adj", f"read{serial}.jpeg"),
+                        os.path.join(HERE, "jpeg_adj", f"read{serial}.jpeg"))
     os.makedirs(os.path.join(HERE, "eps"), exist_ok=True)
     for serial in range(1, 5):
         shutil.copyfile(os.path.join(REF, "Example_output", "single_read_plots_adj", f"read{serial}.eps"),

@@ -397,6 +397,43 @@ def test_error_behaviour():
     assert e.value.name == "NT_E_PATTERN"
 
 
+@pytest.mark.parametrize("tvr", [None, "TTGGGG"], ids=["p2", "p3_split"])
+def test_error_rows_agree_across_calling_forms(tvr, monkeypatch):
+    """Rows of reads the reference errors on (find_right_telo on a 0-row table,
+    --check_right_edge, reads of <= 50 bases): the ahead-of-time calling kernel
+    and the specialised one (a kernel per pass for 3-pass programs, its errors
+    carried through end = -2 / -3 to the combine kernel) write the same rows
+    -- start = end = -1, density 0 for the failing pass, the error flag --
+    beside normal rows, and nt_analyze_host returns NT_E_RIGHT_EMPTY."""
+    import ctypes
+    from nanotel_amd._lib import lib
+    rng = np.random.default_rng(44)
+    seqs = [_telo_read(rng, int(rng.integers(300, 6000)), motif="CCCTAA", where="right") for _ in range(40)]
+    seqs[7] = "ACGT" * 10
+    seqs[23] = "CCCTAA" * 8
+    bseqs = [x.encode() for x in seqs]
+    ptrs = (ctypes.c_char_p * len(bseqs))(*bseqs)
+    lens = np.array([len(b) for b in bseqs], np.uint64)
+    got = []
+    for jit in ("0", "1"):
+        monkeypatch.setenv("NT_CALL_JIT", jit)
+        nt = _nt(patterns="CCCTAA", tvr_patterns=tvr, check_right_edge=True)
+        o = dict(start=np.zeros((40, 3), np.int32), end=np.zeros((40, 3), np.int32),
+                 density=np.zeros((40, 3)), flags=np.zeros(40, np.uint8))
+        rc = lib().nt_analyze_host(nt.handle, ctypes.addressof(ptrs), lens.ctypes.data, 40,
+                                   o["start"].ctypes.data, o["end"].ctypes.data, o["density"].ctypes.data,
+                                   o["flags"].ctypes.data, None, None)
+        assert rc == -5  # NT_E_RIGHT_EMPTY
+        assert nt.call_jit() == (jit == "1")
+        got.append(o)
+        nt.close()
+    for k in ("start", "end", "density", "flags"):
+        assert np.array_equal(got[0][k], got[1][k]), k
+    assert got[0]["flags"][7] & 0x20 and got[0]["flags"][23] & 0x20
+    assert (got[0]["start"][7, :2] == -1).all() and (got[0]["end"][7, :2] == -1).all()
+    assert (got[0]["flags"] & 1).sum() > 5
+
+
 def test_device_synth_matches_host_generator():
     import torch
     from nanotel_amd import NanoTel, read_blocks, synth_params, synth_read_ascii

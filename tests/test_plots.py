@@ -118,3 +118,40 @@ def test_plot_worker_processes(tmp_path):
             assert (tmp_path / "a" / rel).read_bytes() == (tmp_path / "b" / rel).read_bytes()
         assert (tmp_path / "a" / f"single_read_plots_adj/read{j[0]}.eps").read_text() == open(
             os.path.join(GOLD, "eps", f"read{j[0]}.eps")).read()
+
+
+def _psnr(a, b):
+    import numpy as np
+    mse = float(((a - b) ** 2).mean())
+    return 10 * np.log10(255.0 ** 2 / max(mse, 1e-9))
+
+
+@pytest.mark.parametrize("serial", [1, 2, 3, 4])
+def test_example_jpeg_pixels_match_reference(tmp_path, serial):
+    """The Example's single_read_plots_adj/read<serial>.jpeg (R's cairo jpeg()
+    device, NanoTel.R:1876-1896) against ours, drawn from the golden window
+    counts: anti-aliased at R's 72 dpi, lines of 0.75 px, text set to the
+    Helvetica widths (DejaVu glyphs: the only face here).  Thresholds:
+      * the plot region (the density polygons, the telomere bars, axes' box,
+        no text): PSNR >= 28 dB, mean absolute difference <= 3 (of 255);
+      * the whole image (glyph shapes differ: DejaVu against R's Helvetica
+        substitute): PSNR >= 18.5 dB, mean absolute difference <= 8.
+    (The reference's full-axis single_read_plots/read*.jpeg come from an older
+    plot -- no gray area in the legend, "read length" in lower case -- like its
+    summary.csv, so only the _adj plots are compared.)"""
+    import numpy as np
+    from PIL import Image
+    g, rows = _golden()
+    rec, row = g["reads"][serial - 1], rows[serial - 1]
+    subs = plots.window_table(rec["n"], g["L"], rec["p1_counts"])
+    subs_mm = plots.window_table(rec["n"], g["L"], rec["p2_counts"])
+    for d in ("single_read_plots", "single_read_plots_adj"):  # create_dirs (NanoTel.R:1978-1996)
+        (tmp_path / d).mkdir()
+    plots.write_read_plots(str(tmp_path), str(serial), rec["n"], subs, subs_mm, int(row[4]), int(row[5]),
+                           int(row[8]), int(row[9]))
+    a = np.asarray(Image.open(tmp_path / "single_read_plots_adj" / f"read{serial}.jpeg").convert("RGB")).astype(float)
+    b = np.asarray(Image.open(os.path.join(GOLD, "jpeg_adj", f"read{serial}.jpeg")).convert("RGB")).astype(float)
+    assert a.shape == b.shape == (300, 750, 3)
+    r = (slice(60, 225), slice(62, 575))  # inside the plot box, left of the legend
+    assert _psnr(a[r], b[r]) >= 28.0 and np.abs(a[r] - b[r]).mean() <= 3.0
+    assert _psnr(a, b) >= 18.5 and np.abs(a - b).mean() <= 8.0
