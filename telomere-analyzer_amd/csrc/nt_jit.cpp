@@ -73,22 +73,34 @@ const char* const kTypedefs =
 
 }  // namespace
 
-// The bundle scan (nt_tscan.h) covers programs whose patterns share one length
-// m >= 2 and whose TVRs share one length, with subseq_length L <= 170 (8-bit
-// window counts of the transposed output) and 2 (max m - 1) < L (the read's
-// last window, recounted by the calling kernel, holds every position whose
-// letters reach past the read end), and patterns / TVRs of at most 32 letters
-// (the walk's history registers grow with the longest).  Others take the
-// per-read scan only.
+// The bundle scan (nt_tscan.h) covers programs whose patterns are at least 2
+// letters long, in at most kTsMaxGroups (4) distinct lengths per list (one
+// walk group per length; mixed-length lists such as "TTAGGG TTAGG"), with
+// subseq_length L <= 170 (8-bit window counts of the transposed output) and
+// 2 (max m - 1) < L (the read's last window, recounted by the calling kernel,
+// holds every position whose letters reach past the read end), and patterns /
+// TVRs of at most 32 letters (the walk's history registers grow with the
+// longest).  Others take the per-read scan only.
 bool nt_tscan_eligible(const NtProgram& P) {
   if (P.n_pat < 1 || P.L > 170) return false;
-  int mp = P.pat[0].m, mt = P.n_tvr ? P.tvr[0].m : 0;
-  for (int i = 1; i < P.n_pat; ++i)
-    if (P.pat[i].m != mp) return false;
-  for (int i = 1; i < P.n_tvr; ++i)
-    if (P.tvr[i].m != mt) return false;
-  const int M = mp > mt ? mp : mt;
-  return mp >= 2 && M <= 32 && 2 * (M - 1) < P.L;
+  auto lengths = [](const NtPat* v, int n, int& mn, int& mx) {
+    bool seen[65] = {};
+    int d = 0;
+    for (int i = 0; i < n; ++i) {
+      const int m = v[i].m;
+      mn = m < mn ? m : mn;
+      mx = m > mx ? m : mx;
+      if (m >= 1 && m <= 64 && !seen[m]) {
+        seen[m] = true;
+        ++d;
+      }
+    }
+    return d;
+  };
+  int mn = 1 << 30, M = 0;
+  const int dp = lengths(P.pat, P.n_pat, mn, M);
+  const int dt = lengths(P.tvr, P.n_tvr, mn, M);
+  return mn >= 2 && dp <= 4 && dt <= 4 && M <= 32 && 2 * (M - 1) < P.L;
 }
 
 namespace {

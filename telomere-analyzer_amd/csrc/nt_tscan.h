@@ -387,6 +387,228 @@ struct TPipe {
   }
 };
 
+// Distinct pattern lengths of a list (ascending): mixed-length lists (e.g.
+// "TTAGGG TTAGG"; the reference takes any list, NanoTel.R:2322-2334, 360-393)
+// run one group of patterns per length.
+constexpr int kTsMaxGroups = 4;
+template <class List>
+struct LLens;
+template <class... P>
+struct LLens<CtList<P...>> {
+  static constexpr bool has(int m) { return ((P::kM == m) || ... || false); }
+  static constexpr int count() {
+    int c = 0;
+    for (int m = 1; m <= 64; ++m) c += has(m) ? 1 : 0;
+    return c;
+  }
+  static constexpr int kN = count();
+  static constexpr int at(int i) {  // the i-th distinct length
+    for (int m = 1; m <= 64; ++m)
+      if (has(m) && i-- == 0) return m;
+    return 1;
+  }
+};
+
+// The walk pipeline of a program whose patterns (or TVRs) differ in length:
+// TPipe's steps, one group per distinct length m -- the hits of the starts
+// x - (m - 1) whose last letter is the position x, that group's sliding-OR
+// spread (width m), and the coverage of the counted position x - kLam as the
+// OR over the groups of spread_g[x - kLam + m_g - 1] (kLam >= every m_g - 1).
+// Single-length programs keep TPipe (same code as before).
+template <class TP, class Pats, class Tvrs>
+struct TPipeMixed {
+  static constexpr int kM = TP::kM;
+  static constexpr int kNTvr = TP::kNTvr, kNPat = TP::kNPat;
+  static constexpr int HD = 2 * kM;
+  static constexpr uint32_t kTests = LTests<Pats>::kMask | LTests<Tvrs>::kMask;
+  using LP = LLens<Pats>;
+  static constexpr int GP = LP::kN;
+  static constexpr int GT = kNTvr > 0 ? LLens<Tvrs>::kN : 1;
+  static_assert(GP <= kTsMaxGroups && GT <= kTsMaxGroups, "pattern lengths per list (nt_tscan_eligible)");
+  template <int g>
+  static constexpr int mp() { return LP::at(g); }
+  template <int g>
+  static constexpr int mt() {
+    if constexpr (kNTvr > 0) return LLens<Tvrs>::at(g);
+    else return 1;
+  }
+  static constexpr int smax() {
+    int s = 0;
+    for (int g = 0; g < GP; ++g) {
+      int w = 1, k = 0, m = LP::at(g);
+      while (w < m) { w = 3 * w <= m ? 3 * w : m; ++k; }
+      s = k > s ? k : s;
+    }
+    if (kNTvr > 0)
+      for (int g = 0; g < GT; ++g) {
+        int w = 1, k = 0, m = LLens<Tvrs>::at(g);
+        while (w < m) { w = 3 * w <= m ? 3 * w : m; ++k; }
+        s = k > s ? k : s;
+      }
+    return s;
+  }
+  static constexpr int kS = smax();
+  uint32_t hT[16][HD];
+  uint32_t h0[GP][kS + 1][HD], h1[GP][kS + 1][HD], ht[GT][kS + 1][HD];
+  BitCount bc[3];
+
+  __device__ __forceinline__ void init() {
+#pragma unroll
+    for (int t = 0; t < HD; ++t) {
+#pragma unroll
+      for (int c = 0; c < 16; ++c) hT[c][t] = 0u;
+#pragma unroll
+      for (int s = 0; s <= kS; ++s) {
+#pragma unroll
+        for (int g = 0; g < GP; ++g) h0[g][s][t] = h1[g][s][t] = 0u;
+#pragma unroll
+        for (int g = 0; g < GT; ++g) ht[g][s][t] = 0u;
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+#pragma unroll
+      for (int b = 0; b < 8; ++b) bc[p].acc[b] = 0u;
+  }
+
+  template <class Sp, int s, int X, int NN>
+  __device__ __forceinline__ static uint32_t stage(const uint32_t (&w)[NN]) {
+    constexpr int a = Sp::width(s - 1), b = Sp::width(s);
+    if constexpr (3 * a <= b) return or3(w[X], w[X - a], w[X - 2 * a]);
+    else if constexpr (2 * a >= b) return w[X] | w[X - (b - a)];
+    else return or3(w[X], w[X - a], w[X - (b - a)]);
+  }
+
+  template <int N, bool kCount, bool kVarV, class Get, class Hook>
+  __device__ __forceinline__ void run(Get&& get, Hook&& hook) {
+    constexpr int NN = HD + N;
+    uint32_t Ts[16][NN];
+    uint32_t a0[GP][kS + 1][NN], a1[GP][kS + 1][NN], at[GT][kS + 1][NN];
+#pragma unroll
+    for (int t = 0; t < HD; ++t) {
+#pragma unroll
+      for (int c = 0; c < 16; ++c)
+        if ((kTests >> c) & 1u) Ts[c][t] = hT[c][t];
+#pragma unroll
+      for (int s = 0; s <= kS; ++s) {
+#pragma unroll
+        for (int g = 0; g < GP; ++g) {
+          a0[g][s][t] = h0[g][s][t];
+          a1[g][s][t] = h1[g][s][t];
+        }
+#pragma unroll
+        for (int g = 0; g < GT; ++g) at[g][s][t] = ht[g][s][t];
+      }
+    }
+    static_for<0, N>([&](auto ui) {
+      constexpr int u = decltype(ui)::value, x = HD + u;
+      const uint3 pl = get(ui);
+#pragma unroll
+      for (int c = 0; c < 16; ++c)
+        if ((kTests >> c) & 1u) Ts[c][x] = kVarV ? (tt_test(c, pl.x, pl.y) & pl.z) : tt_test(c, pl.x, pl.y);
+      hook(ui);
+      static_for<0, GP>([&](auto gi) {  // patterns of length m: the start x - (m - 1)
+        constexpr int g = decltype(gi)::value, m = mp<g>();
+        constexpr int j0 = x - (m - 1);
+        uint32_t e0 = 0u, e1 = 0u;
+        static_for<0, kNPat>([&](auto pi) {
+          using D = typename LAt<Pats, decltype(pi)::value>::type;
+          if constexpr (D::kM == m) {
+            uint32_t q[m];
+#pragma unroll
+            for (int j = 0; j < m; ++j) q[j] = Ts[D::kTT[j] & 15][j0 + j];
+            uint32_t b0, b1;
+            tcombine<m, false>(q, b0, b1);
+            e0 |= b0;
+            e1 |= b1;
+          }
+        });
+        a0[g][0][x] = e0;
+        a1[g][0][x] = e1;
+        static_for<1, Spread<m>::kS + 1>([&](auto si) {
+          constexpr int s = decltype(si)::value;
+          a0[g][s][x] = stage<Spread<m>, s, x>(a0[g][s - 1]);
+          a1[g][s][x] = stage<Spread<m>, s, x>(a1[g][s - 1]);
+        });
+      });
+      if constexpr (kNTvr > 0) {
+        static_for<0, GT>([&](auto gi) {  // TVRs (exact)
+          constexpr int g = decltype(gi)::value, m = mt<g>();
+          constexpr int j0 = x - (m - 1);
+          uint32_t e = 0u;
+          static_for<0, kNTvr>([&](auto ti) {
+            using D = typename LAt<Tvrs, decltype(ti)::value>::type;
+            if constexpr (D::kM == m) {
+              uint32_t q[m];
+#pragma unroll
+              for (int j = 0; j < m; ++j) q[j] = Ts[D::kTT[j] & 15][j0 + j];
+              uint32_t b0, b1;
+              tcombine<m, true>(q, b0, b1);
+              e |= b0;
+            }
+          });
+          at[g][0][x] = e;
+          static_for<1, Spread<m>::kS + 1>([&](auto si) {
+            constexpr int s = decltype(si)::value;
+            at[g][s][x] = stage<Spread<m>, s, x>(at[g][s - 1]);
+          });
+        });
+      }
+      if constexpr (kCount) {  // the coverage of position x - kLam: OR over the groups
+        constexpr int kLam = TP::kLam;
+        uint32_t c0 = 0u, c1 = 0u, ct = 0u;
+        static_for<0, GP>([&](auto gi) {
+          constexpr int g = decltype(gi)::value, m = mp<g>();
+          constexpr int y = x - (kLam + 1 - m);
+          c0 |= a0[g][Spread<m>::kS][y];
+          c1 |= a1[g][Spread<m>::kS][y];
+        });
+        bc[0].template push<0, u>(c0);
+        bc[1].template push<0, u>(c1);
+        if constexpr (kNTvr > 0) {
+          static_for<0, GT>([&](auto gi) {
+            constexpr int g = decltype(gi)::value, m = mt<g>();
+            constexpr int y = x - (kLam + 1 - m);
+            ct |= at[g][Spread<m>::kS][y];
+          });
+          bc[2].template push<0, u>(c1 | ct);
+        }
+      }
+    });
+    if constexpr (kCount) {
+      bc[0].template flush<0, N>();
+      bc[1].template flush<0, N>();
+      if constexpr (kNTvr > 0) bc[2].template flush<0, N>();
+    }
+#pragma unroll
+    for (int t = 0; t < HD; ++t) {
+#pragma unroll
+      for (int c = 0; c < 16; ++c)
+        if ((kTests >> c) & 1u) hT[c][t] = Ts[c][N + t];
+#pragma unroll
+      for (int s = 0; s <= kS; ++s) {
+#pragma unroll
+        for (int g = 0; g < GP; ++g) {
+          h0[g][s][t] = a0[g][s][N + t];
+          h1[g][s][t] = a1[g][s][N + t];
+        }
+#pragma unroll
+        for (int g = 0; g < GT; ++g) ht[g][s][t] = at[g][s][N + t];
+      }
+    }
+  }
+};
+
+// TPipe for single-length lists, TPipeMixed otherwise
+template <class TP, class Pats, class Tvrs, bool kMixed = (LLens<Pats>::kN > 1) || (LLens<Tvrs>::kN > 1)>
+struct TPipeSel {
+  using type = TPipe<TP, Pats, Tvrs>;
+};
+template <class TP, class Pats, class Tvrs>
+struct TPipeSel<TP, Pats, Tvrs, true> {
+  using type = TPipeMixed<TP, Pats, Tvrs>;
+};
+
 #ifndef NT_TS_PIN
 #define NT_TS_PIN 1
 #endif
@@ -466,7 +688,7 @@ struct TWalker {
   int vb[3];   // byte offset of block k + r's slot 0 (r = -1, 0, 1) in this stripe; < 0 / past the end: zeros
   int vbn[3];  // the same in the next stripe
   uint4 S[D];  // the ring: stream slot f sits in S[f % D]
-  TPipe<TP, Pats, Tvrs> pp;
+  typename TPipeSel<TP, Pats, Tvrs>::type pp;
 
   __device__ __forceinline__ uint4 ld(int voff, int soff) {
     const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, NT_TS_LOAD_AUX);
@@ -600,7 +822,7 @@ struct TWalkerH {
   uint4 S[D];      // the ring: stream slot f sits in S[f % D]
   uint4 Hs[kNH > 0 ? kNH : 1], Ts[kNT];  // own head / tail slots
   uint4 XL[kNT], XR[kNH > 0 ? kNH : 1];  // lane 0's left / lane 63's right neighbour slots
-  TPipe<TP, Pats, Tvrs> pp;
+  typename TPipeSel<TP, Pats, Tvrs>::type pp;
 
   __device__ __forceinline__ uint4 ld(int voff, int soff) {
     const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, NT_TS_LOAD_AUX);

@@ -157,7 +157,7 @@ def _write_run_log(save_path, t0, input_path, files, patterns, tvr_patterns, rc,
     n = int(lengths.size)
     log.print(f"Total reads in sample: {n}")
     log.print("Summary statistics of the sample reads length:")
-    log.summary([int(x) for x in lengths])
+    log.summary(np.asarray(lengths))
     log.print(f"Number of reads which identified as Telomeric: {len(rows)}")
     pct = r_as_character(round(100 * len(rows) / n, 2)) if n else "NaN"
     log.print(f"% of total reads: {pct}%")

@@ -84,7 +84,10 @@ def _zapsmall(v, digits):
 def r_summary(x):
     """summary(x) of a numeric vector: (names, values, NA count) -- Min, the
     type-7 quartiles, median, mean, max; NA's when x holds NAs."""
-    v = np.asarray([np.nan if e is None else float(e) for e in x], np.float64)
+    if isinstance(x, np.ndarray):  # (NA as NaN): no per-element Python work for millions of reads
+        v = x.astype(np.float64, copy=False)
+    else:
+        v = np.asarray([np.nan if e is None else float(e) for e in x], np.float64)
     na = int(np.isnan(v).sum())
     f = v[~np.isnan(v)]
     names = ["Min.", "1st Qu.", "Median", "Mean", "3rd Qu.", "Max."]

@@ -199,6 +199,22 @@ def test_many_patterns(cfg, jit):
         assert nt.tscan == (cfg is MANY[0])  # equal-length lists take the bundle scan
 
 
+# mixed-length lists through the bundle scan (one walk group per distinct
+# length, nt_tscan.h TPipeMixed)
+MIXED = [
+    dict(patterns="TTAGGG TTAGG"),
+    dict(patterns="TTAGGG TTAGG CCCTAAA", tvr_patterns="TGAGGG TTGGG"),
+    dict(patterns="TTAGGG TTAGGGTTAGGG TTAGG", subseq_length=50, min_density=0.5),
+    dict(patterns="TTAGGG TTRGG", tvr_patterns="TTAGGGTTAGGGTTAGGGTTAGGGTTAGGGTT TGAGG"),
+]
+
+
+@pytest.mark.parametrize("cfg", MIXED, ids=["6_5", "6_5_7_tvr_6_5", "6_12_5_L50", "6_5_tvr_32_5"])
+def test_mixed_length_lists_bundle_scan(cfg):
+    nt = _random_reads(cfg, True, check_tscan=False)
+    assert nt.tscan, "mixed-length list not on the bundle scan"
+
+
 def _n_mers(k, n, seed):
     rng = np.random.default_rng(seed)
     out = ["TTAGGG"]
