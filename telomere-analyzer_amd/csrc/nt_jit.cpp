@@ -119,13 +119,26 @@ std::string jit_source(const NtProgram& P) {
 #ifndef NT_TSCAN_WAVES_EU
 #define NT_TSCAN_WAVES_EU 2
 #endif
-extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT_TSCAN_WAVES_EU)))
+#if NT_TS_WS  // 4 walker waves + 1 writer wave (nt_tscan.h)
+extern "C" __global__ void __launch_bounds__(320) __attribute__((amdgpu_waves_per_eu(NT_TSCAN_WAVES_EU)))
+nt_tscan_jit(NtBatch B, NtOut O, uint64_t* __restrict__ tmask, unsigned long long* __restrict__ queue,
+             uint32_t thr_full) {
+  __shared__ uint32_t tsl[nt::ts_ws_lds_words<TJit::kNP>()];
+  nt::tscan_bundles_ws<TJit, TPats, TTvrs>(B, O, tmask, queue, thr_full, tsl);
+}
+#else
+#ifndef NT_TS_DBG_THREADS  // timing experiments: a block of more waves, the extra ones idle
+#define NT_TS_DBG_THREADS 256
+#endif
+extern "C" __global__ void __launch_bounds__(NT_TS_DBG_THREADS) __attribute__((amdgpu_waves_per_eu(NT_TSCAN_WAVES_EU)))
 nt_tscan_jit(NtBatch B, NtOut O, uint64_t* __restrict__ tmask, unsigned long long* __restrict__ queue,
              uint32_t thr_full) {
   constexpr int kW = nt::ts_lds_words<TJit::kNP>();
   __shared__ uint32_t tsl[4 * kW];
+  if (threadIdx.x >= 256) return;
   nt::tscan_bundles<TJit, TPats, TTvrs>(B, O, tmask, queue, thr_full, tsl + (threadIdx.x >> 6) * kW);
 }
+#endif
 )";
   }
   s += R"(
@@ -304,7 +317,12 @@ bool get_code(const std::string& arch, const std::string& src, std::vector<char>
   if (!dir.empty()) {
     uint64_t h = 1469598103934665603ull;
     h = fnv1a(h, src.data(), src.size());
-    for (const char* x : hdrs) h = fnv1a(h, x, std::strlen(x));
+    // the headers the source reaches: nt_common / nt_device / nt_scan always,
+    // nt_tscan.h and nt_call.h when it includes them (a bundle-scan change
+    // leaves the calling kernels' objects valid, and the other way round)
+    for (int i = 0; i < 5; ++i)
+      if (i < 3 || src.find(std::string("#include \"") + names[i] + "\"") != std::string::npos)
+        h = fnv1a(h, hdrs[i], std::strlen(hdrs[i]));
     for (const char* o : opts) h = fnv1a(h, o, std::strlen(o) + 1);  // NUL-separated
     int maj = 0, mnr = 0;
     (void)hiprtcVersion(&maj, &mnr);
@@ -417,12 +435,22 @@ bool nt_jit_get(int device, const NtProgram& P, void* fn[4], void** tfn, std::st
   return true;
 }
 
+// a JIT kernel's block size (its __launch_bounds__: the bundle scan has 320
+// threads with walker / writer waves, 256 without)
+static int jit_threads(void* fn) {
+  int v = 0;
+  if (hipFuncGetAttribute(&v, HIP_FUNC_ATTRIBUTE_MAX_THREADS_PER_BLOCK, (hipFunction_t)fn) != hipSuccess || v <= 0)
+    return 256;
+  return v;
+}
+
 hipError_t nt_tjit_launch(void* fn, int grid, hipStream_t stream, const NtBatch* B, const NtOut* O,
                           uint64_t* tmask, unsigned long long* queue, uint32_t thr_full) {
   NtBatch b = *B;
   NtOut o = *O;
   void* args[] = {&b, &o, &tmask, &queue, &thr_full};
-  return hipModuleLaunchKernel((hipFunction_t)fn, (unsigned)grid, 1, 1, 256, 1, 1, 0, stream, args, nullptr);
+  return hipModuleLaunchKernel((hipFunction_t)fn, (unsigned)grid, 1, 1, (unsigned)jit_threads(fn), 1, 1, 0, stream,
+                               args, nullptr);
 }
 
 hipError_t nt_jit_launch(void* fn, int grid, size_t lds_bytes, hipStream_t stream,
@@ -438,7 +466,7 @@ hipError_t nt_jit_launch(void* fn, int grid, size_t lds_bytes, hipStream_t strea
 
 int nt_jit_blocks_per_cu(void* fn, size_t lds_bytes) {
   int nb = 0;
-  if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (hipFunction_t)fn, 256, lds_bytes) !=
+  if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (hipFunction_t)fn, jit_threads(fn), lds_bytes) !=
       hipSuccess)
     return 0;
   return nb;

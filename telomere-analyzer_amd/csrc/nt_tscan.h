@@ -1230,4 +1230,393 @@ __device__ __forceinline__ void tscan_bundles(const NtBatch& B, const NtOut& O, 
   }
 }
 
+
+// ======================================================================
+// Walker / writer waves (NT_TS_WS, the default).
+//
+// On gfx9 a wave's vector-memory counter covers its loads AND its stores, in
+// issue order: once a wave has issued a store, every later wait for one of its
+// loads also waits for that store to be acknowledged.  The bundle scan's walk
+// keeps 8 loads in flight per lane and waits on the oldest; with any global
+// store in the stripe loop -- the count rows every second stripe, the bitmask /
+// checkpoint flush every kF -- those waits took the stores' write latency:
+// 0.3 ms of a 1.47 ms launch (c50k; timing builds: no stores 1.17 ms, either
+// kind alone 1.47-1.52).  tools/rw_mix_bench.hip isolates it: a read stream
+// with one store per 1,000 loads runs 28 % slower, whether the stores go to
+// HBM or to a 4 MB L2-resident region; the same stores from OTHER waves cost
+// nothing.  So the stores move to a writer wave:
+//  * workgroup = 4 walker waves (one per SIMD, the walk and the output stage's
+//    arithmetic exactly as before, into LDS) + 1 writer wave;
+//  * a walker posts store jobs (the count rows of a stripe pair; a flush of
+//    bitmask words and checkpoints) to its ring in LDS; the writer takes them
+//    in order, reads the rows from the walker's LDS and issues the global
+//    stores; it never waits on its stores;
+//  * the walker's LDS rows are single-buffered (the writer drains a job in
+//    about a microsecond, a stripe's walk takes ~9): before overwriting them the
+//    walker checks that the writer is done with the job that read them; the
+//    slot metadata alternate between two buffers per bundle.
+// Synchronisation is LDS only (s_waitcnt lgkmcnt(0) before publishing a
+// counter, never a vmcnt wait in the walker): counters posted / done per
+// walker, a finished flag; the writer exits when every walker has finished
+// and every posted job is done.
+//
+// Measured (1 M x 50 kb, one launch, no calling beside it):
+// the walkers then never wait on a store and the job handshake costs nothing
+// (writer acknowledging without storing: 2.03-2.08 ms, as the old kernel
+// without stores), but the writer's stores still cost 0.6 ms (2.61-2.78 ms,
+// the old kernel 2.72-2.76): with them the step moves 15.1 GB (13.7 read, 1.4
+// written) at 5.5-5.8 TB/s against the ~6.2 TB/s a read + write stream
+// sustains, so the scan is bound by HBM read + write bandwidth, not by the
+// stores' latency -- and the fifth wave's registers and LDS leave the calling
+// kernel beside the scan a third of its room (0.53 -> 1.5 ms).  Off by
+// default; NT_TS_WS=1 (NT_JIT_OPTS=-DNT_TS_WS=1) builds it.
+#ifndef NT_TS_WS
+#define NT_TS_WS 0
+#endif
+constexpr int kTsRing = 16;   // store jobs in flight per walker
+constexpr int kTsCtl = 4 + kTsRing;  // per walker: posted, done, finished, pad, ring
+constexpr uint32_t kJobCnt = 1u, kJobFlush = 2u;
+
+template <int kNP>
+constexpr int ts_ws_walker_words() {
+  return 2 * NT_BUNDLE * kTsSlotWords + TsAux<kNP>::kWords + kNP * NT_BUNDLE;
+}
+template <int kNP>
+constexpr int ts_ws_lds_words() {
+  return 4 * (ts_ws_walker_words<kNP>() + kTsCtl);
+}
+
+// LDS-typed volatile accesses (a volatile access through a generic pointer
+// stays a FLAT access -- counted in vmcnt, waited with vmcnt(0) -- which put
+// every writer job behind its own stores' acknowledgements)
+typedef __attribute__((address_space(3))) uint32_t lds_u32_t;
+__device__ __forceinline__ void lds_publish_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ uint32_t lds_peek(const uint32_t* p) {
+  const uint32_t v = *(const volatile lds_u32_t*)(p);
+  asm volatile("" ::: "memory");
+  return v;
+}
+__device__ __forceinline__ void lds_put(uint32_t* p, uint32_t v) {
+  asm volatile("" ::: "memory");
+  *(volatile lds_u32_t*)(p) = v;
+}
+
+#ifndef NT_TS_WS_DBG  // timing experiments only (results wrong): 1 = the writer stores nothing,
+#define NT_TS_WS_DBG 0   // 2 = no jobs at all (walkers post nothing, the writer returns at once),
+#endif                   // 3 = no flush stores, 4 = no count stores, 5 = counts as 1 KB pieces, no flush
+template <int kNP>
+struct TsWsRegion {  // one walker's LDS (uint32 words)
+  uint32_t* base;
+  __device__ __forceinline__ TSlot* sl(int buf) const {
+    return reinterpret_cast<TSlot*>(base + buf * NT_BUNDLE * kTsSlotWords);
+  }
+  __device__ __forceinline__ uint32_t* ct() const { return base + 2 * NT_BUNDLE * kTsSlotWords; }
+  __device__ __forceinline__ uint32_t* tmb() const { return ct() + TsAux<kNP>::kCtWords; }
+  __device__ __forceinline__ uint32_t* ckb() const { return tmb() + TsAux<kNP>::kTmWords; }
+  __device__ __forceinline__ uint32_t* tot() const { return ckb() + TsAux<kNP>::kCkWords; }
+};
+
+// The writer's side of a count-row job: stripe pair ending at st (or the
+// bundle's last, single stripe), every pass -- the rows' 128 windows as whole
+// lines, store c covering slots 8 c .. 8 c + 7, lane 8 i + q = the 16 bytes
+// (windows 16 q ..) of slot 8 c + i.
+template <int kNP>
+__device__ __forceinline__ void ts_write_counts(const NtOut& O, const TsWsRegion<kNP>& R, const TSlot* sl, int st,
+                                                int lane, uint32_t dbg_seq = 0u, int dbg_w = 0) {
+#pragma unroll
+  for (int p = 0; p < kNP; ++p) {
+    const uint32_t* ctp = R.ct() + p * NT_BUNDLE * 32;
+    uint4 m[4], x[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int s = 8 * c + (lane >> 3), q = lane & 7;
+      m[c] = *reinterpret_cast<const uint4*>(sl + s);
+      x[c] = *reinterpret_cast<const uint4*>(ctp + s * 32 + 4 * q);
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int q = lane & 7, kq = (st >> 1) * 2 * kWave + 16 * q;
+      if (kq < (int)m[c].x) {
+        uint8_t* w = reinterpret_cast<uint8_t*>(O.win_counts) + u64of(m[c].y, m[c].z) +
+                     (uint64_t)p * NT_WIN_ROWS((uint64_t)m[c].x) + kq;
+        if (NT_TS_WS_DBG == 5)  // timing only: the same bytes as 1 KB contiguous pieces
+          w = reinterpret_cast<uint8_t*>(O.win_counts) + ((uint64_t)blockIdx.x * 4 + dbg_w) * 65536 +
+              ((dbg_seq * 8 + p * 4 + c) % 64) * 1024 + lane * 16;
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4 vv = {x[c].x, x[c].y, x[c].z, x[c].w};
+        __builtin_nontemporal_store(vv, reinterpret_cast<u32x4*>(w));
+      }
+    }
+  }
+}
+
+// The writer's side of a flush job: the bitmask words and checkpoints of
+// stripes st0 .. st0 + fs (and, at the bundle's last stripe, the reads'
+// totals), coalesced runs of each read's row.
+template <int kNP>
+__device__ __forceinline__ void ts_write_flush(uint64_t* __restrict__ tmask, const TsWsRegion<kNP>& R,
+                                               const TSlot* sl, int st0, int fs, bool last, int lane) {
+  using Aux = TsAux<kNP>;
+  const uint32_t* tmb = R.tmb();
+  const uint32_t* ckb = R.ckb();
+  constexpr int kI1 = NT_BUNDLE * Aux::kF / kWave, kI2 = NT_BUNDLE * 4 * Aux::kF / kWave;
+#pragma unroll
+  for (int p = 0; p < kNP; ++p) {
+    uint32_t n1[kI1], n2[kI2], c2[kI2];
+    uint2 a1[kI1], a2[kI2];
+    uint64_t v1[kI1];
+#pragma unroll
+    for (int i = 0; i < kI1; ++i) {
+      const int e = i * kWave + lane, s = e / Aux::kF, w = e % Aux::kF;
+      const uint32_t* ts = reinterpret_cast<const uint32_t*>(sl + s);
+      n1[i] = ts[0];
+      a1[i] = *reinterpret_cast<const uint2*>(ts + 4);
+      v1[i] = *reinterpret_cast<const uint64_t*>(tmb + ((p * NT_BUNDLE + s) * Aux::kF + w) * 2);
+    }
+#pragma unroll
+    for (int i = 0; i < kI2; ++i) {
+      const int e = i * kWave + lane, s = e / (4 * Aux::kF), g = e % (4 * Aux::kF);
+      const uint32_t* ts = reinterpret_cast<const uint32_t*>(sl + s);
+      n2[i] = ts[0];
+      a2[i] = *reinterpret_cast<const uint2*>(ts + 4);
+      c2[i] = ckb[(p * NT_BUNDLE + s) * 4 * Aux::kF + g];
+    }
+#pragma unroll
+    for (int i = 0; i < kI1; ++i) {
+      const int e = i * kWave + lane, w = e % Aux::kF, sw = st0 + w;
+      const int nw = (int)n1[i];
+      if (w <= fs && sw * kWave < nw) tmask[u64of(a1[i].x, a1[i].y) + (uint64_t)p * aux_nmw(nw) + sw] = v1[i];
+    }
+#pragma unroll
+    for (int i = 0; i < kI2; ++i) {
+      const int e = i * kWave + lane, g = e % (4 * Aux::kF), jj = 4 * st0 + g;
+      const int nw = (int)n2[i];
+      if (g < 4 * (fs + 1) && nw > 0 && 16 * jj <= nw)
+        reinterpret_cast<uint32_t*>(tmask + u64of(a2[i].x, a2[i].y) + (uint64_t)kNP * aux_nmw(nw))[
+            p * aux_nck(nw) + jj] = c2[i];
+    }
+  }
+  if (last && lane < NT_BUNDLE) {  // a read whose windows end with the bundle's last stripe: its total
+    const uint32_t* ts = reinterpret_cast<const uint32_t*>(sl + lane);
+    const int nw = (int)ts[0];
+    const uint2 ab = *reinterpret_cast<const uint2*>(ts + 4);
+#pragma unroll
+    for (int p = 0; p < kNP; ++p) {
+      const uint32_t v = R.tot()[p * NT_BUNDLE + lane];
+      if (v != 0xFFFFFFFFu && nw > 0)
+        reinterpret_cast<uint32_t*>(tmask + u64of(ab.x, ab.y) + (uint64_t)kNP * aux_nmw(nw))[
+            p * aux_nck(nw) + (nw >> 4)] = v;
+    }
+  }
+}
+
+template <int kNP>
+__device__ void ts_writer(const NtOut& O, uint64_t* __restrict__ tmask, uint32_t* lds) {
+  if (NT_TS_WS_DBG == 2) return;
+  const int lane = threadIdx.x & (kWave - 1);
+  uint32_t* ctl = lds + 4 * ts_ws_walker_words<kNP>();
+  uint32_t dn[4] = {0u, 0u, 0u, 0u};
+  for (;;) {
+    bool any = false;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      uint32_t* c = ctl + w * kTsCtl;
+      const uint32_t posted = lds_peek(c);
+      while (dn[w] < posted) {
+        const uint32_t job = c[4 + dn[w] % kTsRing];
+        const TsWsRegion<kNP> R{lds + w * ts_ws_walker_words<kNP>()};
+        const TSlot* sl = R.sl((job >> 2) & 1u);
+        const int st = (int)(job >> 10), fs = (int)((job >> 4) & 63u);
+        if (NT_TS_WS_DBG == 1) {
+        } else if (job & kJobCnt) {
+          if (NT_TS_WS_DBG != 4) ts_write_counts<kNP>(O, R, sl, st, lane, dn[w], w);
+        } else {
+          if (NT_TS_WS_DBG != 3 && NT_TS_WS_DBG != 5) ts_write_flush<kNP>(tmask, R, sl, st - fs, fs, (job >> 3) & 1u, lane);
+        }
+        lds_publish_wait();  // the job's LDS reads have returned: its rows may be overwritten
+        lds_put(c + 1, ++dn[w]);
+        any = true;
+      }
+    }
+    if (!any) {
+      bool all = true;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const uint32_t* c = ctl + w * kTsCtl;
+        all = all && lds_peek(c + 2) != 0u && lds_peek(c) == dn[w];
+      }
+      if (all) return;
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+}
+
+// A walker: tscan_bundles' loop with its global stores posted to the writer.
+template <class TP, class Pats, class Tvrs>
+__device__ void ts_walker(const NtBatch& B, uint64_t* __restrict__ tmask, unsigned long long* __restrict__ queue,
+                          uint32_t thr_full, uint32_t* lds, int wv) {
+  constexpr int kL = TP::kL, kNP = TP::kNP, kT = TP::kT;
+  static_assert(kL <= 170, "8-bit counts (nt_tscan_eligible)");
+  using Aux = TsAux<kNP>;
+  const int lane = threadIdx.x & (kWave - 1);
+  const TsWsRegion<kNP> R{lds + wv * ts_ws_walker_words<kNP>()};
+  uint32_t* ctl = lds + 4 * ts_ws_walker_words<kNP>() + wv * kTsCtl;
+  uint32_t* ct = R.ct();
+  uint32_t* tmb = R.tmb();
+  uint32_t* ckb = R.ckb();
+  uint32_t posted = 0u;
+  int64_t cnt_job = -1, flush_job = -1, buf_job[2] = {-1, -1};
+  auto wait_done = [&](int64_t seq) {  // the writer has finished job seq
+    if (seq < 0 || NT_TS_WS_DBG == 2) return;
+    while ((int64_t)lds_peek(ctl + 1) <= seq) __builtin_amdgcn_s_sleep(1);
+  };
+  auto post = [&](uint32_t job) -> int64_t {
+    if (NT_TS_WS_DBG == 2) return -1;
+    while (posted - lds_peek(ctl + 1) >= (uint32_t)kTsRing) __builtin_amdgcn_s_sleep(1);
+    ctl[4 + posted % kTsRing] = job;
+    lds_publish_wait();  // the job's rows and its ring entry are in LDS
+    lds_put(ctl, ++posted);
+    return (int64_t)posted - 1;
+  };
+  const uint32_t sel2 = (lane & 2) ? 0x03020706u : 0x05040100u;
+  const uint32_t sel1 = (lane & 1) ? 0x03070105u : 0x06020400u;
+  const int ms = lane & (NT_BUNDLE - 1), mh = lane >> 5;
+  const uint64_t nb = B.n_bundles;
+  uint32_t qi = blockIdx.x % NT_QUEUES, qtried = 0;
+  auto claim = [&]() -> uint64_t {
+    while (qtried < NT_QUEUES) {
+      const uint64_t q0 = nb * qi / NT_QUEUES, q1 = nb * (qi + 1) / NT_QUEUES;
+      unsigned long long v = 0;
+      if (lane == 0) v = atomicAdd(queue + qi * NT_QUEUE_STRIDE, 1ull);
+      const uint64_t o = uniform_u64(v);
+      if (o < q1 - q0) return q0 + o;
+      qi = qi + 1 == NT_QUEUES ? 0 : qi + 1;
+      ++qtried;
+    }
+    return nb;
+  };
+  int bi = 0;  // bundles this walker has taken (slot buffer bi & 1)
+  for (uint64_t b = claim(); b < nb; b = claim(), ++bi) {
+    const int sb = bi & 1;
+    wait_done(buf_job[sb]);  // the writer is done with the bundle that used this slot buffer
+    TSlot* sl = R.sl(sb);
+    uint32_t n_max;
+    {
+      const uint32_t r = B.bnd_read[b * NT_BUNDLE + (lane & 31)];
+      const bool o = r != 0xFFFFFFFFu;
+      const uint32_t len = o ? B.len[r] : 0u;
+      const uint64_t wo = o ? B.win_off[r] : 0ull;
+      if (lane < NT_BUNDLE) {
+        TSlot t;
+        t.len = len;
+        t.nw = o ? (uint32_t)split_window_count(len, kL) : 0u;
+        t.r = r;
+        t.occ = o ? 1u : 0u;
+        const uint64_t wb = wo * kNP, ab = aux_base(wo, r, kNP);
+        t.wb_lo = (uint32_t)wb;
+        t.wb_hi = (uint32_t)(wb >> 32);
+        t.ab_lo = (uint32_t)ab;
+        t.ab_hi = (uint32_t)(ab >> 32);
+        t.run[0] = t.run[1] = t.run[2] = 0u;
+        t.pad = 0u;
+        sl[lane] = t;
+      }
+      n_max = (uint32_t)__builtin_amdgcn_readfirstlane((int)len);  // slot 0 = the longest
+    }
+    const int nblk = ((int)n_max + kL - 1) / kL;
+    const int nst = (nblk + kWave - 1) / kWave;
+    const uint64_t g0 = uniform_u64(B.bnd_stripe[b]), g1 = uniform_u64(B.bnd_stripe[b + 1]);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint32_t*>(B.tplanes) + g0 * (uint64_t)kT * kWave * 4, (short)0,
+        (int)((g1 - g0) * (uint64_t)kT * kWave * 16), 0x00020000);
+    wave_sync();
+    TWalker<TP, Pats, Tvrs> wk;
+    wk.rs = rs;
+    wk.set_stripe(0, lane, lane < nblk);
+    if (NT_TS_XPRIME) wk.prime();
+    for (int st = 0; st < nst; ++st) {
+      const int k = st * kWave + lane;
+      if (!NT_TS_XPRIME) wk.prime();
+      uint32_t acc[3][8];
+      wk.walk(k == 0, acc);
+      wk.set_stripe(st + 1, lane, k + kWave < nblk);
+      const TSlot& mt = sl[ms];
+      const int m_nw = (int)mt.nw;
+      const int k0 = st * kWave + 32 * mh;
+      const int nv = m_nw - k0 < 0 ? 0 : (m_nw - k0 > 32 ? 32 : m_nw - k0);
+      const int fs = st % Aux::kF;
+      if ((st & 1) == 0) wait_done(cnt_job);  // a new stripe pair: the last pair's rows are stored
+      if (fs == 0) wait_done(flush_job);      // a new flush group: the last group's words are stored
+      const bool last = st == nst - 1;
+#pragma unroll
+      for (int p = 0; p < kNP; ++p) {
+        uint32_t* ctp = ct + p * NT_BUNDLE * 32;
+        const int half = (st & 1) * 16;
+        uint32_t W[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) W[t] = acc[p][t];
+        uint32_t ge = ~0u;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          const uint32_t tm = ((thr_full >> t) & 1u) ? ~0u : 0u;
+          ge = (W[t] & ge) | (~tm & (W[t] | ge));
+        }
+        if (thr_full > 255u) ge = 0u;
+        transpose8(W);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) W[j] = quad_byte_transpose(W[j], sel2, sel1);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ctp[(8 * (lane & 3) + j) * 32 + half + (lane >> 2)] = W[j];
+        const uint32_t tb = half_bit_transpose(ge, lane) & (nv >= 32 ? ~0u : ((1u << nv) - 1u));
+        tmb[((p * NT_BUNDLE + ms) * Aux::kF + fs) * 2 + mh] = tb;
+        wave_sync();
+        const uint4 va = *reinterpret_cast<const uint4*>(ctp + ms * 32 + half + 8 * mh);
+        const uint4 vb = *reinterpret_cast<const uint4*>(ctp + ms * 32 + half + 8 * mh + 4);
+        uint32_t ga = 0u, gb = 0u;
+        ga = __builtin_amdgcn_udot4(va.x, 0x01010101u, ga, false);
+        ga = __builtin_amdgcn_udot4(va.y, 0x01010101u, ga, false);
+        ga = __builtin_amdgcn_udot4(va.z, 0x01010101u, ga, false);
+        ga = __builtin_amdgcn_udot4(va.w, 0x01010101u, ga, false);
+        gb = __builtin_amdgcn_udot4(vb.x, 0x01010101u, gb, false);
+        gb = __builtin_amdgcn_udot4(vb.y, 0x01010101u, gb, false);
+        gb = __builtin_amdgcn_udot4(vb.z, 0x01010101u, gb, false);
+        gb = __builtin_amdgcn_udot4(vb.w, 0x01010101u, gb, false);
+        const uint32_t mine = ga + gb;
+        const uint32_t other = (uint32_t)__shfl_xor((int)mine, 32, kWave);
+        const uint32_t run = mt.run[p];
+        const uint32_t c0 = run + (mh ? other : 0u);
+        uint32_t* ckr = ckb + (p * NT_BUNDLE + ms) * 4 * Aux::kF + 4 * fs + 2 * mh;
+        ckr[0] = c0;
+        ckr[1] = c0 + ga;
+        if (last && mh)  // the read's total when its windows end with this stripe
+          R.tot()[p * NT_BUNDLE + ms] = 16 * ((k0 >> 4) + 2) == m_nw ? c0 + mine : 0xFFFFFFFFu;
+        wave_sync();
+        if (mh == 0) sl[ms].run[p] = run + mine + other;
+      }
+      if ((st & 1) || last) cnt_job = post(kJobCnt | ((uint32_t)sb << 2) | ((uint32_t)st << 10));
+      if (fs == Aux::kF - 1 || last) {
+        flush_job = post(kJobFlush | ((uint32_t)sb << 2) | ((last ? 1u : 0u) << 3) | ((uint32_t)fs << 4) |
+                         ((uint32_t)st << 10));
+      }
+      buf_job[sb] = (int64_t)posted - 1;
+      wave_sync();
+    }
+    wave_sync();
+  }
+  lds_publish_wait();
+  lds_put(ctl + 2, 1u);  // finished (after the last job was posted)
+}
+
+// The bundle scan with walker / writer waves: 5 waves a workgroup.
+template <class TP, class Pats, class Tvrs>
+__device__ __forceinline__ void tscan_bundles_ws(const NtBatch& B, const NtOut& O, uint64_t* __restrict__ tmask,
+                                                 unsigned long long* __restrict__ queue, uint32_t thr_full,
+                                                 uint32_t* lds) {
+  constexpr int kNP = TP::kNP;
+  const int wv = threadIdx.x >> 6;
+  if (threadIdx.x < 4 * kTsCtl) lds[4 * ts_ws_walker_words<kNP>() + threadIdx.x] = 0u;  // control words
+  __syncthreads();
+  if (wv < 4) ts_walker<TP, Pats, Tvrs>(B, tmask, queue, thr_full, lds, wv);
+  else ts_writer<kNP>(O, tmask, lds);
+}
 }  // namespace nt
