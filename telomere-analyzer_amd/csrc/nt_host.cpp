@@ -939,6 +939,11 @@ int64_t nt_kernel_times(nt_ctx* ctx, double* scan_ms, double* call_ms) {
 
 // Pack a host chunk (2-bit planes + exception lists, --rc fused) and upload
 // it to the context's device buffers; B describes the device batch.
+static bool host_tlayout() {
+  const char* v = std::getenv("NT_HOST_TLAYOUT");
+  return v && v[0] == '1';
+}
+
 static int upload_reads(nt_ctx* ctx, const char* const* seqs, const uint64_t* lens, uint64_t n_reads,
                         nt_batch* B, uint64_t* max_len, bool want_bundles) {
   const int L = ctx->prog.L;
@@ -1047,15 +1052,33 @@ static int upload_reads(nt_ctx* ctx, const char* const* seqs, const uint64_t* le
   }
   if (nb) {
     lap(3);
-    if ((e = ctx->h_tplanes.ensure(tpb)) != hipSuccess) return hip_fail(ctx, e, "hipHostMalloc(tplanes)");
-    int rc = nt_bundle_layout_host(hp, h_blk, h_len, h_bread.data(), h_bstripe.data(), nb, L,
-                                   (uint32_t*)ctx->h_tplanes.p, tpb);
-    if (rc) return fail(ctx, rc, "nt_bundle_layout_host");
-    lap(2);
-    NT_UP_PTR(tplanes, ctx->h_tplanes.p, tpb);
     NT_UP(bnd_read, h_bread);
     NT_UP(bnd_stripe, h_bstripe);
     if (nl) { NT_UP(list, h_list); }
+    if (host_tlayout()) {
+      // NT_HOST_TLAYOUT=1: the T-layout built on the host and uploaded beside
+      // the planes (round 3; twice the upload bytes, 98 ms of host time per 8
+      // Gbases on a 16-core share -- the end-to-end bound)
+      if ((e = ctx->h_tplanes.ensure(tpb)) != hipSuccess) return hip_fail(ctx, e, "hipHostMalloc(tplanes)");
+      int rc = nt_bundle_layout_host(hp, h_blk, h_len, h_bread.data(), h_bstripe.data(), nb, L,
+                                     (uint32_t*)ctx->h_tplanes.p, tpb);
+      if (rc) return fail(ctx, rc, "nt_bundle_layout_host");
+      lap(2);
+      NT_UP_PTR(tplanes, ctx->h_tplanes.p, tpb);
+    } else {
+      // the device transposer from the uploaded planes (about 1 ms per 8 Gbases
+      // of GPU time; nt_bundle_layout), on the context stream before the scan
+      if ((e = ctx->tplanes.ensure(tpb)) != hipSuccess) return hip_fail(ctx, e, "hipMalloc(tplanes)");
+      const uint64_t stripe_bytes = (uint64_t)((L + 1) / 2) * 64 * 16;
+      NtBatch Bt{(const uint32_t*)ctx->planes.p, (const uint64_t*)ctx->blk_off.p, (const uint32_t*)ctx->len.p,
+                 (const uint64_t*)ctx->win_off.p, nullptr, nullptr, nullptr, n_reads, nullptr, 0,
+                 (const uint32_t*)ctx->tplanes.p, (const uint32_t*)ctx->bnd_read.p,
+                 (const uint64_t*)ctx->bnd_stripe.p, nb};
+      e = nt_dev_launch_bundle(&Bt, tpb / stripe_bytes, (uint32_t*)ctx->tplanes.p, L, ctx->prog.div32_m,
+                               ctx->prog.div32_s, ctx->stream, ctx->cu_count);
+      if (e != hipSuccess) return hip_fail(ctx, e, "launch nt_bundle_kernel");
+      lap(2);
+    }
     // the vectors are pageable: finish their copies before they go
     if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess) return hip_fail(ctx, e, "hipStreamSynchronize");
   }

@@ -175,6 +175,16 @@ struct nt_reader {
   // bytes the parser walked over (records, kept or skipped) and bytes inflated
   uint64_t bytes_parsed = 0, bytes_inflated = 0;
   size_t rec_at = 0;  // header offset (in the window) of the last record parsed
+  // FASTQ fast path (a mapped plain file): records indexed in parallel slices
+  // without reading the quality lines (fq_index_slice); fq_mode 1 = on for
+  // the open file, 0 = off (the line parser)
+  struct FqRec {
+    uint64_t hdr, name_at, name_len, seq_at, seq_len, end;
+  };
+  std::vector<FqRec> fq;
+  size_t fq_i = 0;
+  uint64_t fq_scan = 0;
+  int fq_mode = 0;
   // the current file's bytes: a mapping of the whole plain file, a whole gzip
   // part inflated ahead (Prefetcher), or windows of a gzip stream (serial inflate)
   gzFile gz = nullptr;
@@ -352,8 +362,19 @@ void start(nt_reader* r) {
   }
 }
 
+// the FASTQ fast path's state for a new position of the open file
+void fq_reset(nt_reader* r, uint64_t pos, bool mapped) {
+  r->fq.clear();
+  r->fq_i = 0;
+  r->fq_scan = pos;
+  const char* v = std::getenv("NT_READER_FQ_FAST");  // 0: the line parser for FASTQ too
+  const bool off = v && v[0] == '0';
+  r->fq_mode = (r->format == 1 && mapped && !off) ? 1 : 0;
+}
+
 bool open_next(nt_reader* r) {
   close_source(r);
+  r->fq_mode = 0;
   r->win.reset();
   r->pos = r->end = r->scan = 0;
   r->nl.clear();
@@ -405,6 +426,7 @@ bool open_next(nt_reader* r) {
     r->end = b->size;
     r->src_eof = true;
     r->active = true;
+    fq_reset(r, 0, b->map != nullptr);
     return true;
   }
   r->gz = gzopen(path.c_str(), "rb");
@@ -554,6 +576,116 @@ int parse_record(nt_reader* r, bool lens_only, std::vector<uint64_t>* skip_lens)
   return 1;
 }
 
+size_t resync(const char* d, size_t n, size_t o, int format);
+size_t nl_at(const char* d, size_t n, size_t p);
+
+// offset of the first non-blank line at or after p (blank: "\n" or "\r\n")
+size_t skip_blank(const char* d, size_t n, size_t p) {
+  for (;;) {
+    if (p < n && d[p] == '\n') ++p;
+    else if (p + 1 < n && d[p] == '\r' && d[p + 1] == '\n') p += 2;
+    else return p;
+  }
+}
+
+// One FASTQ record whose header is at p (p past any blank lines) with the
+// line parser's semantics (parse_record): '@' name, the sequence line, a '+'
+// line, quality lines up to the sequence's length -- a single quality line
+// of exactly that length is skipped without being read (its newline is
+// checked), otherwise its lines are walked.  Returns 1 (rec, next = the
+// offset after the record's last line), 0 (p at the end), -1 malformed.
+int fq_parse_one(const char* d, size_t n, size_t p, nt_reader::FqRec& rec, size_t& next) {
+  if (p >= n) return 0;
+  if (d[p] != '@') return -1;
+  const size_t eh = nl_at(d, n, p);
+  if (eh >= n) return -1;
+  size_t ne = eh;
+  if (ne > p + 1 && d[ne - 1] == '\r') --ne;
+  const size_t s0 = eh + 1, es = nl_at(d, n, s0);
+  size_t se = es;
+  if (se > s0 && d[se - 1] == '\r') --se;
+  if (es >= n) return -1;  // no '+' line
+  const size_t pl = es + 1;
+  if (pl >= n || d[pl] != '+') return -1;
+  const size_t ep = nl_at(d, n, pl);
+  const uint64_t sl = se - s0;
+  size_t c = ep >= n ? n : ep + 1;
+  if (sl > 0 && c < n) {
+    const size_t qe = c + sl;
+    if (qe == n) {
+      c = n;
+    } else if (qe < n && d[qe] == '\n') {
+      c = qe + 1;
+    } else if (qe + 1 < n && d[qe] == '\r' && d[qe + 1] == '\n') {
+      c = qe + 2;
+    } else {  // wrapped (or longer) quality: its lines, up to the sequence's length
+      uint64_t ql = 0;
+      while (ql < sl && c < n) {
+        const size_t e = nl_at(d, n, c);
+        size_t le = e;
+        if (le > c && d[le - 1] == '\r') --le;
+        ql += le - c;
+        c = e >= n ? n : e + 1;
+      }
+    }
+  }
+  rec.hdr = p;
+  rec.name_at = p + 1;
+  rec.name_len = ne - p - 1;
+  rec.seq_at = s0;
+  rec.seq_len = sl;
+  rec.end = c;
+  next = c;
+  return 1;
+}
+
+// Index the records that start in the next slice of the mapped FASTQ file
+// (up to 1 GB) on the host threads: each thread resynchronises in its part
+// (an '@' line whose second next line starts with '+'), parses records up to
+// its part's end, and the parts must chain (thread t's first record is where
+// thread t - 1 stopped).  Returns 1 (records appended; fq_scan moved on), 0
+// (the file is done), -1 (a part did not chain or a record is malformed: the
+// caller goes on with the line parser from fq_scan).
+int fq_index_slice(nt_reader* r) {
+  const char* d = r->win->data;
+  const size_t n = r->end;
+  const size_t a = skip_blank(d, n, r->fq_scan);
+  if (a >= n) return 0;
+  constexpr size_t kSlice = 1ull << 30;
+  const size_t b = std::min(n, a + kSlice);
+  const unsigned nt = (b - a) >= (8u << 20) ? host_threads() : 1u;
+  struct Part {
+    std::vector<nt_reader::FqRec> recs;
+    size_t first = 0, next = 0;
+    bool bad = false;
+  };
+  std::vector<Part> part(nt);
+  par(nt, [&](unsigned t) {
+    Part& P = part[t];
+    const size_t lo = a + (b - a) * t / nt, hi = a + (b - a) * (t + 1) / nt;
+    size_t p = t == 0 ? a : skip_blank(d, n, resync(d, n, lo, 1));
+    P.first = p;
+    while (p < hi && p < n) {
+      nt_reader::FqRec rec;
+      size_t nx = 0;
+      const int k = fq_parse_one(d, n, p, rec, nx);
+      if (k == 0) break;
+      if (k < 0) {
+        P.bad = true;
+        break;
+      }
+      P.recs.push_back(rec);
+      p = skip_blank(d, n, nx);
+    }
+    P.next = p;
+  });
+  for (unsigned t = 0; t < nt; ++t)
+    if (part[t].bad || (t && part[t].first != part[t - 1].next)) return -1;
+  for (auto& P : part) r->fq.insert(r->fq.end(), P.recs.begin(), P.recs.end());
+  r->fq_scan = part[nt - 1].next;
+  return 1;
+}
+
 // Up to nrec records into the chunk store (or their lengths only); returns
 // the count, or -1 on error.
 int64_t read_records(nt_reader* r, uint64_t nrec, bool lens_only, std::vector<uint64_t>* skip_lens) {
@@ -564,6 +696,47 @@ int64_t read_records(nt_reader* r, uint64_t nrec, bool lens_only, std::vector<ui
     if (!r->active) {
       if (!open_next(r)) break;
       ref = false;
+      continue;
+    }
+    if (r->fq_mode == 1) {  // FASTQ fast path: records from the slice index
+      if (r->fq_i < r->fq.size()) {
+        const nt_reader::FqRec& q = r->fq[r->fq_i++];
+        const char* b = r->win->data;
+        r->bytes_parsed += q.end - r->pos;
+        r->pos = q.end;
+        r->rec_at = q.hdr;
+        ++r->rec_in_file;
+        ++got;
+        if (lens_only) {
+          skip_lens->push_back(q.seq_len);
+          continue;
+        }
+        S.seq_len.push_back(q.seq_len);
+        S.name_ptr.push_back(b + q.name_at);
+        S.name_len.push_back(q.name_len);
+        S.seq_ptr.push_back(b + q.seq_at);
+        S.seq_blob.push_back(0);
+        S.seq_off.push_back(0);
+        if (!ref) {
+          S.refs.push_back(r->win);
+          ref = true;
+        }
+        continue;
+      }
+      r->fq.clear();
+      r->fq_i = 0;
+      const int k = fq_index_slice(r);
+      if (k > 0) continue;
+      if (k == 0) {  // the file is done
+        r->pos = r->end;
+        close_source(r);
+        continue;
+      }
+      // the line parser from here on (it reports a malformed record where it is)
+      r->fq_mode = 0;
+      r->pos = r->scan = (size_t)r->fq_scan;
+      r->nl.clear();
+      r->nl_i = 0;
       continue;
     }
     const int k = parse_record(r, lens_only, skip_lens);
@@ -945,6 +1118,7 @@ int nt_reader_seek(nt_reader* r, int mode, uint64_t a, uint64_t b) {
     r->pos = r->scan = off;
     r->nl.clear();
     r->nl_i = 0;
+    fq_reset(r, off, r->win && r->win->map != nullptr);
     return NT_OK;
   }
   std::vector<uint64_t> lens;

@@ -322,3 +322,56 @@ def test_count_files_plan_and_record_seek(tmp_path):
         from nanotel_amd import NanoTelError
         with pytest.raises(NanoTelError):
             r.plan([0])  # only before the first read
+
+
+def test_fastq_fast_path_matches_line_parser(tmp_path, monkeypatch):
+    """The FASTQ fast path (mapped plain files: records indexed in parallel
+    slices, single quality lines skipped unread) gives the line parser's
+    records, chunks and errors: CRLF, blank lines between records, empty
+    sequences, quality lines starting with '@' / '+', a wrapped quality, a
+    quality longer than its sequence, a last record without a newline, a
+    truncated quality at the end, and a malformed record after good ones."""
+    rng = np.random.default_rng(29)
+    recs = [(f"r{i} d", "".join(rng.choice(list("ACGTN"), int(rng.integers(0 if i % 7 else 1, 3000)))))
+            for i in range(300)]
+
+    def body(i, n, s, crlf):
+        nl = "\r\n" if crlf else "\n"
+        q = "".join(rng.choice(list("@+I#"), len(s)))
+        if i % 50 == 7 and len(s) > 10:  # wrapped quality
+            q = q[:5] + nl + q[5:]
+        if i % 50 == 9:  # longer quality (accepted as the line parser does)
+            q = q + "II"
+        return f"@{n}{nl}{s}{nl}+{nl}{q}{nl}" + (nl if i % 11 == 3 else "")
+
+    cases = {}
+    cases["mixed"] = "".join(body(i, n, s, i % 3 == 0) for i, (n, s) in enumerate(recs))
+    cases["no_final_newline"] = cases["mixed"].rstrip("\r\n")
+    cases["truncated_quality"] = cases["mixed"] + "@tail\nACGTACGT\n+\nIII"
+    cases["malformed"] = cases["mixed"] + "@bad\nACGT\nIIII\n"
+    big = "".join(body(i, f"b{i}", "ACGT" * 2500, False) for i in range(4000))  # 40 MB: several threads
+    cases["big"] = big
+
+    def read_all(path, nrec):
+        out, err = [], None
+        try:
+            with Reader(str(path), "fastq") as r:
+                while True:
+                    ch = r.next_chunk(nrec)
+                    if ch is None:
+                        break
+                    out.append([(ch.name(i), ch.seq(i)) for i in range(ch.n)])
+        except Exception as ex:  # noqa: BLE001
+            err = str(ex)
+        return out, err
+
+    for key, txt in cases.items():
+        p = tmp_path / f"{key}.fastq"
+        p.write_bytes(txt.encode())
+        for nrec in (7, 1000):
+            monkeypatch.setenv("NT_READER_FQ_FAST", "0")
+            slow = read_all(p, nrec)
+            monkeypatch.setenv("NT_READER_FQ_FAST", "1")
+            fast = read_all(p, nrec)
+            assert fast == slow, (key, nrec)
+        assert (slow[1] is not None) == (key == "malformed"), (key, slow[1])
