@@ -21,6 +21,8 @@ import os
 import sys
 import time
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "telomere-analyzer_amd"))
 
@@ -132,6 +134,26 @@ def cpu_baseline(cfg, budget_s=12.0):
     return out
 
 
+def exc_synth(n, read_len, frac, rank):
+    """Exception lists for --n-frac: every round(1/frac)-th read carries one N
+    (Biostrings code 15) at a seeded random position -> (exc_off [n+1],
+    exc_pos, exc_code) host arrays, or None.  The planes keep the generator's
+    base there: the scans re-evaluate every start that touches an exception
+    from its code, so the reads are the synthetic reads with an N at that
+    position (tests/test_gpu_parity.py checks this against the oracle)."""
+    if frac <= 0:
+        return None
+    k = max(1, int(round(1.0 / frac)))
+    carriers = np.arange(0, n, k)
+    rng = np.random.default_rng(4321 + rank)
+    pos = rng.integers(0, read_len, carriers.size).astype(np.uint32)
+    cnt = np.zeros(n, np.uint32)
+    cnt[carriers] = 1
+    off = np.zeros(n + 1, np.uint32)
+    np.cumsum(cnt, out=off[1:])
+    return off, pos, np.full(carriers.size, 15, np.uint8)
+
+
 def _free_port():
     import socket
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
@@ -166,6 +188,9 @@ def main():
     ap.add_argument("--per-read", action="store_true", help="per-read scan only (no bundle layout)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="serial batches: each step waits for its own last calling kernel (nt_set_pipelined off)")
+    ap.add_argument("--n-frac", type=float, default=0.0,
+                    help="fraction of reads carrying one N (an exception list entry at a random position): the "
+                         "bundle scan takes them, the calling kernel recounts their windows near it")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     args = ap.parse_args()
     if args.gpus < 1:
@@ -233,6 +258,10 @@ def main():
     sp = synth_params(first_read=rank * n, read_len=L, variant_rate=cfg["variant"], rc_layout=cfg["rc"])
     nt.synth_device(sp, n, planes.data_ptr())
     nt.uniform_layout_device(n, L, blk_off.data_ptr(), lens.data_ptr(), win_off.data_ptr())
+    # --n-frac: reads with one non-ACGT letter (N, Biostrings code 15) each
+    exc_h = exc_synth(n, L, args.n_frac, rank)
+    exc_d = [torch.from_numpy(a.view(np.int32) if a.dtype == np.uint32 else a).to(dev) for a in exc_h] if exc_h else []
+    exc_ptrs = [a.data_ptr() for a in exc_d] if exc_d else [0, 0, 0]
     # the bundle layout (the reads transposed 32 to a bundle, the bundle scan's
     # copy of them), built on the device before the timed region like the planes
     bundles, keep = None, []
@@ -251,15 +280,16 @@ def main():
     out_bytes = sum(x.numel() * x.element_size() for x in (start, end, dens, flags, wc))
     want_pipe = not args.no_pipeline
     if nt.tscan and not args.per_read:
-        import numpy as np
         lens_h = np.full(n, L, np.uint32)
-        plan = nt.bundle_plan(lens_h)
+        # reads whose letters reach too many windows stay on the per-read scan
+        marks = nt.exc_marks(lens_h, exc_h[0], exc_h[1]) if exc_h else None
+        plan = nt.bundle_plan(lens_h, marks)
         free, _ = torch.cuda.mem_get_info(dev)
         if plan.tplane_bytes + aux_bytes + margin > free:
             per = plan.tplane_bytes / max(1, n)
             k = int((free - aux_bytes - margin) / per) // 32 * 32 if free > aux_bytes + margin else 0
             if k >= 32 * 128:  # at least two bundle ranges' worth
-                has_exc = np.zeros(n, np.uint8)
+                has_exc = np.zeros(n, np.uint8) if marks is None else marks.copy()
                 has_exc[k:] = 1
                 plan = nt.bundle_plan(lens_h, has_exc)
                 cap_note = (f"bundle layout for {k} of {n} reads (planes + layout beside the outputs fill "
@@ -273,7 +303,6 @@ def main():
         plan = None
     if plan is not None:
         from nanotel_amd.api import DeviceBundles
-        import numpy as np
         scan_path = "bundle" if len(plan.list) == 0 else f"bundle + per-read ({len(plan.list)} reads)"
         if cap_note:
             scan_path += "; " + cap_note
@@ -306,7 +335,8 @@ def main():
         k_step[0] += 1
         nt.scan_call_device(planes.data_ptr(), blk_off.data_ptr(), lens.data_ptr(), win_off.data_ptr(),
                             n, n * rows, L, o[0].data_ptr(), o[1].data_ptr(), o[2].data_ptr(),
-                            o[3].data_ptr(), o[4].data_ptr(), bundles=bundles)
+                            o[3].data_ptr(), o[4].data_ptr(), exc_off=exc_ptrs[0], exc_pos=exc_ptrs[1],
+                            exc_code=exc_ptrs[2], bundles=bundles)
 
     # the specialised calling kernel builds in the background on the first
     # large batch: wait for it, so that no timed (or warm-up) step runs the
@@ -386,6 +416,7 @@ def main():
                        "patterns": cfg["patterns"], "subseq_length": 100, "min_density": 0.6,
                        "passes": npass, "telomeric_reads_rank0": telo, "scan_path": scan_path,
                        "pipelined": pipelined,
+                       **({"reads_with_an_n": round(args.n_frac, 6)} if args.n_frac > 0 else {}),
                        "parallelism": f"dp{world} (read shards)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),

@@ -157,13 +157,25 @@ int nt_pack_reads(const char* const* seqs, const uint64_t* lens, uint64_t n_read
                   uint64_t* win_off, uint32_t* exc_off, uint32_t* exc_pos, uint8_t* exc_code);
 
 /* --- bundle layout (the bundle scan's copy of the reads) ------------------- */
+/* Host: which reads with non-ACGT letters must stay on the per-read scan.
+ * The bundle scan takes reads with exceptions too: the calling kernel recounts
+ * the windows within (longest pattern - 1) of an exception exactly, as it
+ * recounts every bundled read's last window -- up to NT_EXC_WINDOWS (16) such
+ * windows a read.  has_exc[r] = 1 for the reads with more (their exceptions
+ * from nt_pack_reads: exc_off [n+1], exc_pos; exc_off NULL = none), 0 for the
+ * rest: pass it to nt_bundle_plan.  Replaces no reference interface (the
+ * reference has no bundles; Biostrings matches any subject, NanoTel.R:360-393). */
+int nt_exc_marks(nt_ctx* ctx, const uint32_t* len, const uint32_t* exc_off, const uint32_t* exc_pos,
+                 uint64_t n_reads, uint8_t* has_exc);
 /* Host: group the reads of a batch 32 to a bundle (longest first; the compiled
  * program fixes the block size L).  has_exc (NULL = none) marks reads that
- * stay outside the bundles and go to the per-read scan: reads with non-ACGT
- * letters (nt_pack_reads' exception lists), or any the caller leaves there
- * (e.g. to bound the T-layout's memory when a batch's planes and its layout
- * do not both fit); so do the reads of any program the bundle scan does not
- * cover (then *n_bundles = 0).  Outputs:
+ * stay outside the bundles and go to the per-read scan: reads whose non-ACGT
+ * letters reach too many windows (nt_exc_marks; marking every read with an
+ * exception list is allowed too), or any the caller leaves there (e.g. to
+ * bound the T-layout's memory when a batch's planes and its layout do not
+ * both fit); so do the reads of any program the bundle scan does not cover
+ * (then *n_bundles = 0).  A read with exceptions in a bundle needs the
+ * batch's exception lists in the nt_batch of nt_scan_call.  Outputs:
  * bnd_read [ceil(n/32)*32], bnd_stripe [ceil(n/32)+1], list [n] (the reads
  * left out, in order), and the bytes of the T-layout buffer. */
 int nt_bundle_plan(nt_ctx* ctx, const uint32_t* len, const uint8_t* has_exc, uint64_t n_reads,
@@ -172,8 +184,9 @@ int nt_bundle_plan(nt_ctx* ctx, const uint32_t* len, const uint8_t* has_exc, uin
 /* Host (ingest): write the T-layout of the planned bundles into the host
  * buffer tplanes (tplane_bytes from the plan; every byte written) from host
  * planes packed by nt_pack_reads -- a 32 x 32 bit transpose per 32-base block
- * (AVX2), all host threads.  nt_analyze_host builds its batches' T-layout this
- * way and uploads it beside the planes (no device transposer per batch). */
+ * (AVX2), all host threads.  (nt_analyze_host builds its batches' T-layout on
+ * the device with the transposer of nt_bundle_layout after the planes'
+ * upload; NT_HOST_TLAYOUT=1 takes this host build instead.) */
 int nt_bundle_layout_host(const uint32_t* planes, const uint64_t* blk_off, const uint32_t* len,
                           const uint32_t* bnd_read, const uint64_t* bnd_stripe, uint64_t n_bundles,
                           int32_t subseq_length, uint32_t* tplanes, uint64_t tplane_bytes);

@@ -865,22 +865,44 @@ static __device__ __forceinline__ int search_left(const Lane& c, const Pw<K>& w,
 // window nw (the read's total, when nw is a multiple of 16) and its bit of the
 // telomeric bitmask (threshold of its own width) are rewritten.  Idempotent
 // for reads of the per-read scan.
-static __device__ __forceinline__ void call_fix_last(Lane& c, const uint32_t* __restrict__ thr, uint32_t thr_size) {
+//
+// A read with non-ACGT letters scanned in a bundle (nt_common.h, exc_windows)
+// has the windows near its exceptions recounted the same way first, each
+// checkpoint after them moved by the difference.  A read whose exceptions
+// reach more than NT_EXC_WINDOWS windows was left on the per-read scan: its
+// counts are exact and only its last window is recounted.  One coverage site
+// for all of them (the windows in a rolled loop).
+static __device__ __forceinline__ void call_fix_windows(Lane& c, const uint32_t* __restrict__ thr, uint32_t thr_size) {
   if (c.nw <= 0) return;
-  const int last = c.nw - 1, a = last * c.L;
-  const int exact = cov_count(c, a, c.n - 1);
-  const int old = wcount(c, last);
-  if (exact != old) {
-    if (c.c8) static_cast<uint8_t*>(const_cast<void*>(c.cnt))[last] = (uint8_t)exact;
-    else static_cast<uint16_t*>(const_cast<void*>(c.cnt))[last] = (uint16_t)exact;
-    if ((c.nw & 15) == 0) const_cast<uint32_t*>(c.ck)[c.nw >> 4] += (uint32_t)(exact - old);
+  int ne = 0;
+  if (c.rc.n_exc) {
+    ne = exc_windows(c.rc.exc_pos, (uint32_t)c.rc.n_exc, c.n, c.L, c.nw, c.prog->m_max, NT_EXC_WINDOWS, [](int) {});
+    if (ne > NT_EXC_WINDOWS) ne = 0;
   }
-  const uint32_t w = (uint32_t)(c.n - a);
-  const bool tel = (uint32_t)exact >= thr[w < thr_size ? w : thr_size - 1];
-  uint64_t* tw = const_cast<uint64_t*>(c.tm) + (last >> 6);
-  const uint64_t m = 1ull << (last & 63), x = *tw;
-  const uint64_t y = tel ? (x | m) : (x & ~m);
-  if (y != x) *tw = y;
+  for (int k = 0; k <= ne; ++k) {
+    int w = c.nw - 1;  // the last window after the exception windows
+    if (k < ne) {
+      int i = 0;
+      exc_windows(c.rc.exc_pos, (uint32_t)c.rc.n_exc, c.n, c.L, c.nw, c.prog->m_max, k + 1, [&](int x) {
+        if (i++ == k) w = x;
+      });
+    }
+    const int a = w * c.L, b = w == c.nw - 1 ? c.n - 1 : a + c.L - 1;
+    const int exact = cov_count(c, a, b);
+    const int old = wcount(c, w);
+    if (exact != old) {
+      if (c.c8) static_cast<uint8_t*>(const_cast<void*>(c.cnt))[w] = (uint8_t)exact;
+      else static_cast<uint16_t*>(const_cast<void*>(c.cnt))[w] = (uint16_t)exact;
+      // the checkpoints after window w (covered bases before window 16 j)
+      for (int j = (w >> 4) + 1; j <= (c.nw >> 4); ++j) const_cast<uint32_t*>(c.ck)[j] += (uint32_t)(exact - old);
+    }
+    const uint32_t wd = (uint32_t)(b - a + 1);
+    const bool tel = (uint32_t)exact >= thr[wd < thr_size ? wd : thr_size - 1];
+    uint64_t* tw = const_cast<uint64_t*>(c.tm) + (w >> 6);
+    const uint64_t m = 1ull << (w & 63), x = *tw;
+    const uint64_t y = tel ? (x | m) : (x & ~m);
+    if (y != x) *tw = y;
+  }
 }
 
 // find_telo_position_wraper (NanoTel.R:1080-1155) + density (NanoTel.R:1840).
@@ -1013,7 +1035,7 @@ static __device__ __forceinline__ void run_pass(const NtProgram* __restrict__ pr
     Lane c;
     init_lane(c, prog, B, O, tmask, r, kPass, tm_lds, pw_lds);
 #ifndef NT_DBG_NO_FIXLAST
-    if (fix_last) call_fix_last(c, thr, thr_size);
+    if (fix_last) call_fix_windows(c, thr, thr_size);
 #endif
     int s = -1, e = -1;
     double d = 0.0;
@@ -1060,7 +1082,7 @@ static __device__ __forceinline__ void run(const NtProgram* __restrict__ prog, N
         Lane c;
         init_lane(c, prog, B, O, tmask, r, p, tm_lds, pw_lds);
 #ifndef NT_DBG_NO_FIXLAST  // timing experiments only (wrong results for bundled reads)
-        if (fix_last) call_fix_last(c, thr, thr_size);
+        if (fix_last) call_fix_windows(c, thr, thr_size);
 #endif
         call_pass(c, s, e, d, flags);
         if (s == -1) flags |= 1u << (NT_FLAG_NA_SHIFT + p);

@@ -83,9 +83,48 @@ struct NtProgram {
   uint32_t div32_s;
   uint32_t thr_size;      // entries of the per-width telomeric threshold table
   int32_t cnt8;           // window counts are uint8 (L <= 170), else uint16
+  int32_t m_max;          // longest pattern or TVR
   NtPat pat[NT_MAX_PAT];
   NtPat tvr[NT_MAX_PAT];
 };
+
+#if defined(__HIPCC_RTC__) || defined(__HIP__)
+#define NT_HOSTDEV __host__ __device__
+#else
+#define NT_HOSTDEV
+#endif
+
+// Reads with a few non-ACGT letters take the bundle scan too.  The T-layout
+// holds A at their exception positions, so a window holding a position within
+// m_max - 1 of one may be counted wrong there; the calling kernel recounts
+// those windows exactly from the read's planes and exception list
+// (call_fix_windows, nt_call.h), as it recounts every bundled read's last
+// window.  A read whose exceptions reach more than NT_EXC_WINDOWS windows
+// before its last stays on the per-read scan (nt_exc_marks -> nt_bundle_plan).
+#define NT_EXC_WINDOWS 16
+
+// The windows before the last (nw - 1) that hold a position within mm - 1 of
+// an exception (positions ascending), in order: f(w) for each of the first
+// cap; returns how many there are, or cap + 1 when there are more.
+template <class F>
+NT_HOSTDEV inline int exc_windows(const uint32_t* pos, uint32_t n_exc, int n, int L, int nw, int mm, int cap, F&& f) {
+  int cnt = 0, next = 0;  // next: the first window not visited yet
+  for (uint32_t i = 0; i < n_exc && next < nw - 1; ++i) {
+    const int p = (int)pos[i];
+    const int a = p - (mm - 1) < 0 ? 0 : p - (mm - 1);
+    const int b = p + (mm - 1) > n - 1 ? n - 1 : p + (mm - 1);
+    int w0 = a / L, w1 = b / L;
+    if (w1 > nw - 2) w1 = nw - 2;
+    if (w0 < next) w0 = next;
+    for (int w = w0; w <= w1; ++w) {
+      if (cnt == cap) return cap + 1;
+      ++cnt;
+      f(w);
+    }
+    if (w1 + 1 > next) next = w1 + 1;
+  }
+  return cnt;
+}
 
 // T-layout ("bundles", the bundle scan's copy of the reads, nt_tscan.h):
 //   reads grouped NT_BUNDLE to a bundle, slots sorted by length (non-increasing;

@@ -788,6 +788,21 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
   return NT_OK;
 }
 
+// has_exc[r] = 1 for the reads whose exceptions reach more than NT_EXC_WINDOWS
+// windows before their last (they stay on the per-read scan); the others are
+// left as they are.
+static void exc_marks(const NtProgram& P, const uint32_t* len, const uint32_t* exc_off, const uint32_t* exc_pos,
+                      uint64_t n_reads, uint8_t* has_exc) {
+  parallel_for(n_reads, [&](uint64_t r) {
+    const uint32_t e0 = exc_off[r], e1 = exc_off[r + 1];
+    if (e1 == e0) return;
+    const int nw = (int)window_count((int64_t)len[r], P.L);
+    if (exc_windows(exc_pos + e0, e1 - e0, (int)len[r], P.L, nw, P.m_max, NT_EXC_WINDOWS, [](int) {}) >
+        NT_EXC_WINDOWS)
+      has_exc[r] = 1;
+  });
+}
+
 // Bundles of the bundle scan: the eligible reads (no non-ACGT letter, the
 // program covered by nt_tscan.h) sorted by length, longest first (ties in
 // input order), 32 to a bundle; a bundle's T-layout is ceil(ceil(n_max / L) /
@@ -827,6 +842,18 @@ int nt_bundle_plan(nt_ctx* ctx, const uint32_t* len, const uint8_t* has_exc, uin
   *n_bundles = nb;
   *n_list = nl;
   *tplane_bytes = g * stripe_bytes;
+  return NT_OK;
+}
+
+int nt_exc_marks(nt_ctx* ctx, const uint32_t* len, const uint32_t* exc_off, const uint32_t* exc_pos,
+                 uint64_t n_reads, uint8_t* has_exc) {
+  if (!ctx || (n_reads && (!len || !has_exc))) return NT_E_ARG;
+  if (!ctx->compiled) return fail(ctx, NT_E_STATE, "nt_compile() not called");
+  std::memset(has_exc, 0, n_reads);
+  if (exc_off && n_reads) {
+    if (!exc_pos && exc_off[n_reads] > exc_off[0]) return NT_E_ARG;
+    exc_marks(ctx->prog, len, exc_off, exc_pos, n_reads, has_exc);
+  }
   return NT_OK;
 }
 
@@ -1038,8 +1065,10 @@ static int upload_reads(nt_ctx* ctx, const char* const* seqs, const uint64_t* le
   std::vector<uint32_t> h_bread, h_list;
   std::vector<uint64_t> h_bstripe;
   if (ctx->tjit_fn && want_bundles) {
-    std::vector<uint8_t> hx(n_reads);
-    for (uint64_t r = 0; r < n_reads; ++r) hx[r] = cnt[r] > 0;
+    // reads with non-ACGT letters join the bundles unless their exceptions
+    // reach more than NT_EXC_WINDOWS windows (nt_common.h)
+    std::vector<uint8_t> hx(n_reads, 0);
+    if (te) exc_marks(ctx->prog, h_len, h_eoff.data(), h_epos.data(), n_reads, hx.data());
     h_bread.resize((n_reads + NT_BUNDLE - 1) / NT_BUNDLE * NT_BUNDLE + NT_BUNDLE);
     h_bstripe.resize((n_reads + NT_BUNDLE - 1) / NT_BUNDLE + 2);
     h_list.resize(n_reads + 1);

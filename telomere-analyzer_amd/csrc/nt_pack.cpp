@@ -295,8 +295,10 @@ int make_program(const nt_params* prm, NtProgram& P, std::vector<uint32_t>& thr,
   // 8-bit window counts when every window is under 256 bases: the last window
   // (merged with a short tail by split_telo) is < 1.5 L wide
   P.cnt8 = P.L <= 170 ? 1 : 0;
+  P.m_max = 1;
   for (int i = 0; i < P.n_pat + P.n_tvr; ++i) {
     NtPat& X = i < P.n_pat ? P.pat[i] : P.tvr[i - P.n_pat];
+    P.m_max = X.m > P.m_max ? X.m : P.m_max;
     for (int j = 0; j < X.m; ++j)
       for (int b = 0; b < 4; ++b) {
         X.tm_scan[j][b] = ((X.tt_scan[j] >> b) & 1u) ? 0xFFFFFFFFu : 0u;

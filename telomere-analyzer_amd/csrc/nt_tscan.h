@@ -35,7 +35,7 @@
 // past a read), so the LAST window of every read -- whose width may differ
 // from L, and into which split_telo may have merged a short last block
 // (NanoTel.R:220) -- is recounted exactly by the calling kernel from the
-// per-read planes (call_fix_last, nt_call.h).
+// per-read planes (call_fix_windows, nt_call.h).
 #pragma once
 #include "nt_scan.h"
 
@@ -648,7 +648,7 @@ struct TPipeSel<TP, Pats, Tvrs, true> {
 // [0, kL) per pass go to acc.  P < 0 of block 0 are outside every read
 // (Biostrings' out-of-bound start -1, masked in the prologue); the read ends
 // are not masked -- the T-layout holds A there -- so the calling kernel
-// recounts the last window of every read (call_fix_last).
+// recounts the last window of every read (call_fix_windows).
 template <class TP, class Pats, class Tvrs>
 struct TWalker {
   static constexpr int kL = TP::kL, kLam = TP::kLam, kT = TP::kT;

@@ -97,6 +97,7 @@ SIGNATURES = {
                                      _U64P, _U64P]),
     "nt_pack_reads": (ctypes.c_int, [_P, _P, ctypes.c_uint64, ctypes.c_int32, ctypes.c_int32, _P, _P,
                                      _P, _P, _P, _P, _P]),
+    "nt_exc_marks": (ctypes.c_int, [_P, _P, _P, _P, ctypes.c_uint64, _P]),
     "nt_bundle_plan": (ctypes.c_int, [_P, _P, _P, ctypes.c_uint64, _P, _P, _U64P, _P, _U64P, _U64P]),
     "nt_bundle_layout_host": (ctypes.c_int, [_P, _P, _P, _P, _P, ctypes.c_uint64, ctypes.c_int32, _P,
                                              ctypes.c_uint64]),

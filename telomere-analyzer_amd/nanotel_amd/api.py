@@ -271,6 +271,18 @@ class NanoTel:
                        b.tplanes if b else None, b.bnd_read if b else None, b.bnd_stripe if b else None,
                        b.n_bundles if b else 0, (b.list or None) if b else None, b.n_list if b else 0)
 
+    def exc_marks(self, lengths, exc_off, exc_pos):
+        """nt_exc_marks on host arrays: uint8 per read, 1 = its non-ACGT letters
+        reach more than NT_EXC_WINDOWS windows (keep it on the per-read scan:
+        pass the result to bundle_plan)."""
+        ln = np.ascontiguousarray(lengths, np.uint32)
+        eo = np.ascontiguousarray(exc_off, np.uint32)
+        ep = np.ascontiguousarray(exc_pos, np.uint32)
+        out = np.zeros(max(1, ln.size), np.uint8)
+        _check(lib().nt_exc_marks(self._h, ln.ctypes.data, eo.ctypes.data, ep.ctypes.data if ep.size else None,
+                                  ln.size, out.ctypes.data), self._h)
+        return out[:ln.size]
+
     def bundle_plan(self, lengths, has_exc=None):
         """nt_bundle_plan on host arrays: returns a BundlePlan (numpy arrays)."""
         ln = np.ascontiguousarray(lengths, np.uint32)

@@ -215,6 +215,99 @@ def test_mixed_length_lists_bundle_scan(cfg):
     assert nt.tscan, "mixed-length list not on the bundle scan"
 
 
+# Reads with a few non-ACGT letters through the bundle scan (VERDICT r3 item
+# 6): the T-layout holds A at the letters; the calling kernel recounts every
+# window within (longest pattern - 1) of one (call_fix_windows, nt_call.h).
+EXC_WINDOWS = 16  # NT_EXC_WINDOWS (nt_common.h)
+
+
+def _exc_windows(pos, n, L, mm):
+    """exc_windows (nt_common.h) restated: the windows before the last that
+    hold a position within mm - 1 of an exception."""
+    from nanotel_amd import window_count
+    nw = window_count(n, L)
+    out = set()
+    for p in pos:
+        a, b = max(p - (mm - 1), 0), min(p + mm - 1, n - 1)
+        out.update(w for w in range(a // L, min(b // L, nw - 2) + 1))
+    return sorted(out)
+
+
+def _sparse_exception_reads(seed, L=100):
+    rng = np.random.default_rng(seed)
+    letters = "NNNNRY-"
+    seqs = []
+    for i in range(640):
+        n = int(rng.choice([int(rng.integers(150, 1200)), int(rng.integers(1200, 9000)),
+                            int(rng.integers(9000, 30000))]))
+        s = list(_telo_read(rng, n, where=["left", "right", "mid"][i % 3], tract=(100, min(n, 4000))))
+        kind = i % 8
+        if kind == 1:  # one letter anywhere
+            pos = [int(rng.integers(0, n))]
+        elif kind == 2:  # at the read's ends and around window boundaries
+            k = int(rng.integers(1, max(2, n // L)))
+            pos = [0, n - 1, min(n - 1, k * L - 1), min(n - 1, k * L), min(n - 1, k * L + 5)]
+        elif kind == 3:  # a run inside the tract area
+            a = int(rng.integers(0, max(1, min(n, 4000) - 40)))
+            pos = list(range(a, min(n, a + int(rng.integers(5, 40)))))
+        elif kind == 4:  # a few scattered letters
+            pos = sorted(int(x) for x in rng.integers(0, n, int(rng.integers(2, 6))))
+        elif kind == 5:  # spread over more than NT_EXC_WINDOWS windows: the per-read scan
+            pos = list(range(int(rng.integers(0, 50)), n, 2 * L + 7))
+        elif kind == 6:  # inside the last window only
+            pos = [n - 1 - int(rng.integers(0, min(n, 60)))]
+        else:
+            pos = []
+        for p in pos:
+            s[p] = letters[int(rng.integers(0, len(letters)))]
+        seqs.append("".join(s))
+    return seqs
+
+
+@pytest.mark.parametrize("cfg", [
+    dict(patterns="TTAGGG"),
+    dict(patterns="YYAGGG"),
+    dict(patterns="TTAGGN"),
+    dict(patterns="TTAGGG TCAGGG", tvr_patterns="TGAGGG TTGGGG"),
+    dict(patterns="TTAGGG TTAGG", tvr_patterns="TTAGGGTTAGGGTTAGGG"),
+    dict(patterns="TTAGGG", subseq_length=37, min_density=0.3),
+], ids=["fixed", "iupac", "pattern_n", "p3", "mixed_18_tvr", "L37"])
+def test_sparse_exceptions_take_the_bundle_scan(cfg):
+    L = cfg.get("subseq_length", 100)
+    seqs = _sparse_exception_reads(zlib.crc32(str(sorted(cfg.items())).encode()), L)
+    nt = _nt(**cfg)
+    assert nt.tscan
+    # which reads the bundles take: nt_exc_marks against the restated rule
+    mm = max(len(p) for p in (cfg["patterns"] + " " + cfg.get("tvr_patterns", "")).split())
+    exc_off, exc_pos = [0], []
+    for s in seqs:
+        exc_pos += [i for i, ch in enumerate(s) if ch not in "ACGTacgt"]
+        exc_off.append(len(exc_pos))
+    lens = np.array([len(s) for s in seqs], np.uint32)
+    marks = nt.exc_marks(lens, np.array(exc_off, np.uint32), np.array(exc_pos, np.uint32))
+    want = [len(_exc_windows(exc_pos[exc_off[r]:exc_off[r + 1]], len(seqs[r]), L, mm)) > EXC_WINDOWS
+            for r in range(len(seqs))]
+    assert marks.tolist() == [int(x) for x in want]
+    with_exc = sum(1 for r in range(len(seqs)) if exc_off[r + 1] > exc_off[r])
+    assert 0 < int(marks.sum()) < with_exc // 2  # most reads with letters are bundled
+    res = nt.analyze(seqs, want_windows=True, want_hits=False)
+    compare(nt, res, oracle_rows(seqs, cfg["patterns"], tvr=cfg.get("tvr_patterns"), L=L,
+                                 min_density=cfg.get("min_density", 0.6)), check_hits=False)
+    assert res["telomeric"].sum() > 20
+
+
+def test_sparse_exceptions_specialised_call(monkeypatch):
+    # the same recounts in the calling kernel specialised for the patterns
+    monkeypatch.setenv("NT_CALL_JIT", "1")
+    seqs = _sparse_exception_reads(77)
+    for pats, tvr in (("TTAGGG", None), ("TTAGGG TCAGGG", "TGAGGG TTGGGG")):
+        nt = _nt(patterns=pats, tvr_patterns=tvr)
+        res = nt.analyze(seqs, want_windows=True, want_hits=False)
+        assert nt.call_jit(), "the specialised calling kernel did not run"
+        compare(nt, res, oracle_rows(seqs, pats, tvr=tvr), check_hits=False)
+        nt.close()
+
+
 def _n_mers(k, n, seed):
     rng = np.random.default_rng(seed)
     out = ["TTAGGG"]
@@ -588,6 +681,52 @@ def test_device_bundle_scan_matches_per_read_scan(read_len):
     compare(nt, res, oracle_rows(seqs, "TTAGGG"), check_windows=False, check_hits=False)
 
 
+@pytest.mark.parametrize("tvr", [None, "TGAGGG TTGGGG"], ids=["p2", "p3"])
+def test_device_bundles_with_sparse_exceptions(tvr):
+    # bench.py --n-frac: device-generated reads, one N in every 4th read as an
+    # exception list entry only (the planes and the T-layout keep the
+    # generator's base there), all of them in the bundles; against the oracle
+    # on the reads with that letter written in, window counts included
+    import torch
+    import bench
+    from nanotel_amd import synth_params, synth_read_ascii
+    n, read_len = 320, 12000
+    pats = "TTAGGG TCAGGG" if tvr else "TTAGGG"
+    nt = _nt(patterns=pats, tvr_patterns=tvr)
+    sp = synth_params(read_len=read_len, first_read=77, variant_rate=0.05 if tvr else 0.0)
+    t = _device_batch(nt, sp, n, read_len, hits=False)
+    off, pos, code = bench.exc_synth(n, read_len, 0.25, 0)
+    assert len(pos) == n // 4
+    ex = [torch.from_numpy(off.view(np.int32)).cuda(), torch.from_numpy(pos.view(np.int32)).cuda(),
+          torch.from_numpy(code).cuda()]
+    marks = nt.exc_marks(np.full(n, read_len, np.uint32), off, pos)
+    assert int(marks.sum()) == 0  # one letter each: every read in a bundle
+    b, keep = _device_bundles(nt, t, n, read_len, marks)
+    assert b.n_list == 0
+    nt.scan_call_device(t["planes"].data_ptr(), t["blk_off"].data_ptr(), t["lens"].data_ptr(),
+                        t["win_off"].data_ptr(), n, n * t["rows"], read_len, t["start"].data_ptr(),
+                        t["end"].data_ptr(), t["dens"].data_ptr(), t["flags"].data_ptr(), t["wc"].data_ptr(),
+                        exc_off=ex[0].data_ptr(), exc_pos=ex[1].data_ptr(), exc_code=ex[2].data_ptr(), bundles=b)
+    nt.synchronize()
+    idx = list(range(0, 96, 4)) + [1, 2, 3, 5, 6]
+    seqs = []
+    for i in idx:
+        s = list(synth_read_ascii(sp, i))
+        for e in range(int(off[i]), int(off[i + 1])):
+            s[int(pos[e])] = "N"
+        seqs.append("".join(s))
+    res = {"start": t["start"].cpu().numpy().reshape(n, 3)[idx], "end": t["end"].cpu().numpy().reshape(n, 3)[idx],
+           "density": t["dens"].cpu().numpy().reshape(n, 3)[idx], "flags": t["flags"].cpu().numpy()[idx]}
+    res["telomeric"] = (res["flags"] & 1) != 0
+    orows = oracle_rows(seqs, pats, tvr=tvr, want_hits=False)
+    compare(nt, res, orows, check_windows=False, check_hits=False)
+    wc = _valid_counts(t, n, nt.n_pass).cpu().numpy().view(nt.count_dtype)
+    for k, i in enumerate(idx):
+        for p in range(nt.n_pass):
+            assert wc[i, p].tolist() == orows[k]["win_counts"][p], (i, p)
+    assert res["telomeric"].sum() > 3
+
+
 def test_pipelined_batches_match_serial():
     """nt_set_pipelined: each call's last bundle range's calling runs beside the
     next call's scan (the bench's stream of batches).  Four calls over three
@@ -709,7 +848,9 @@ def test_pipelined_calls_with_rewritten_inputs(back):
 def test_bundle_ranges_with_mixed_lengths_and_exceptions(tvr):
     # enough bundles for the two bundle-scan ranges (calling beside the scan),
     # reads of many lengths (bundles sorted by length, ragged ends, reads of one
-    # window) and ~4 % of reads with N / IUPAC letters (left to the per-read scan)
+    # window) and ~4 % of reads with N / IUPAC letters (the short ones in the
+    # bundles, their windows near the letters recounted; the long ones, whose
+    # letters reach more than NT_EXC_WINDOWS windows, on the per-read scan)
     rng = np.random.default_rng(20261016)
     seqs = []
     for i in range(4500):
