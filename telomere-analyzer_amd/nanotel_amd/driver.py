@@ -553,8 +553,13 @@ def run(input_path, save_path, patterns, fmt="fastq", nrec=10000, rc=False, min_
         stats["bytes_parsed"], stats["bytes_inflated"] = rdr.stats()
         stats.update({"host_" + k: v for k, v in nt.host_times().items()} if hasattr(nt, "host_times") else {})
         stats["groups_rounds"] = g
+    tc = time.time()
     rdr.close()
+    tc2 = time.time()
     nt.close()
+    if stats is not None:  # (inside "final")
+        stats["final_close_reader"] = tc2 - tc
+        stats["final_close_ctx"] = time.time() - tc2
     if rank != 0:
         return None, None
     lengths = np.concatenate(lengths_all) if lengths_all else np.zeros(0, np.uint64)
