@@ -200,9 +200,20 @@ struct Pos {
 #endif
 constexpr int kTmRegs = NT_CALL_TM_LDS ? NT_CALL_TM_WORDS : 8;  // bitmask words held per lane
 
+constexpr int kExcLocal = 4;
+#ifndef NT_DBG_NO_EXC_FIX  // timing experiments only (results wrong): no exception-window recounts
+#define NT_DBG_NO_EXC_FIX 0
+#endif
+#ifndef NT_DBG_NO_EXC_PATCH  // timing experiments only (results wrong): neighbourhoods ignore exceptions
+#define NT_DBG_NO_EXC_PATCH 0
+#endif
+
 // Per-lane state of one read-pass.
 struct Lane {
   ReadCtx rc;
+  uint32_t exc_lo, exc_hi;        // the read's first / last exception position (n_exc > 0)
+  uint32_t xpos[kExcLocal];       // its exception positions when n_exc <= kExcLocal
+  uint32_t xcode;                 // and their codes, 8 bits each
   const NtProgram* prog;
   const void* cnt;       // this pass's window counts: uint8 when c8, else uint16
   bool c8;
@@ -220,6 +231,120 @@ struct Lane {
   uint64_t tmw[kTmRegs];
 #endif
 };
+
+// A neighbourhood's hit words with the read's non-ACGT letters applied,
+// patch_exceptions' result (nt_device.h; scan semantics: fixed = code
+// equality, else IUPAC bit-set AND; positions outside the read mismatch) for
+// every start of [hb, hb + 32 NH).  Bit-parallel over a touched word's 32
+// starts: its hits are recomputed from the plane words in registers (Lw / Hw
+// / Vw: positions [hb + 32 t, + 31], t < NP) with every exception letter
+// counted as a match, then each exception letter's mismatches are added (a
+// 2-bit saturating count, one exception letter per start and exception).  A
+// read of at most kExcLocal letters has them in the lane's registers
+// (Lane::xpos / xcode): no memory access.  (patch_exceptions per hit word
+// looked every letter of every touched start up in memory; per start in
+// registers it still made the calling kernel, latency-bound, the pipeline's
+// bottleneck at c10k with 10 % of the reads carrying an N.)  One copy per
+// pattern site: the touched words are selected by index.
+template <int NH, int NP>
+__device__ __forceinline__ void patch_words(const Lane& c, int64_t hb, const uint32_t* Lw, const uint32_t* Hw,
+                                            const uint32_t* Vw, const NtPat& P, uint32_t* x0, uint32_t* x1) {
+  const ReadCtx& rc = c.rc;
+  const int m = P.m;
+  const int64_t n = rc.n;
+  const int64_t shi = hb + 32 * NH - 1;  // the last start
+  const int64_t xlo = hb > 0 ? hb : 0;
+  int64_t xhi = shi + m - 1;
+  if (xhi > n - 1) xhi = n - 1;
+  if (xlo > xhi || xhi < (int64_t)c.exc_lo || xlo > (int64_t)c.exc_hi || NT_DBG_NO_EXC_PATCH) return;
+  const bool cached = rc.n_exc <= kExcLocal;
+  auto exc_at = [&](int32_t i) -> int64_t {  // position of exception i
+    uint32_t xi = 0u;
+#pragma unroll
+    for (int k = 0; k < kExcLocal; ++k) xi = k == i ? c.xpos[k] : xi;
+    return cached ? (int64_t)xi : (int64_t)rc.exc_pos[i];
+  };
+  auto code_of = [&](int32_t i) -> uint32_t {
+    return cached ? ((c.xcode >> (8 * (i & 3))) & 255u) : (uint32_t)rc.exc_code[i];
+  };
+  const int32_t i0 = cached ? 0 : exc_lower_bound(rc, xlo);
+  const bool eqx = P.fixed != 0;
+  int hdone = -1;  // words <= hdone recomputed
+  for (int32_t i = i0; i < rc.n_exc; ++i) {
+    const int64_t x = exc_at(i);
+    if (x > xhi) break;
+    if (x < xlo) continue;
+    int h0 = (int)((x - m + 1 - hb) >> 5), h1 = (int)((x - hb) >> 5);  // (arithmetic shifts: floor)
+    if (h0 <= hdone) h0 = hdone + 1;
+    if (h0 < 0) h0 = 0;
+    if (h1 > NH - 1) h1 = NH - 1;
+    for (int h = h0; h <= h1; ++h) {
+      const int64_t base = hb + 32 * h;
+      // the exception letters of [base, base + 95] as bits (the starts' letters reach base + 31 + m - 1)
+      const int32_t kb = cached ? 0 : exc_lower_bound(rc, base);
+      uint32_t e0 = 0u, e1 = 0u, e2 = 0u;
+      for (int32_t k = kb; k < rc.n_exc; ++k) {
+        const int64_t y = exc_at(k) - base;
+        if (y > 95) break;
+        if (y < 0) continue;
+        const uint32_t bit = 1u << (uint32_t)(y & 31);
+        e0 |= y < 32 ? bit : 0u;
+        e1 |= (y >= 32 && y < 64) ? bit : 0u;
+        e2 |= y >= 64 ? bit : 0u;
+      }
+      uint32_t L0 = 0u, L1 = 0u, L2 = 0u, H0 = 0u, H1 = 0u, H2 = 0u, V0 = 0u, V1 = 0u, V2 = 0u;
+#pragma unroll
+      for (int u = 0; u < NP; ++u) {
+        L0 = u == h ? Lw[u] : L0;
+        H0 = u == h ? Hw[u] : H0;
+        V0 = u == h ? Vw[u] : V0;
+        L1 = u == h + 1 ? Lw[u] : L1;
+        H1 = u == h + 1 ? Hw[u] : H1;
+        V1 = u == h + 1 ? Vw[u] : V1;
+        L2 = u == h + 2 ? Lw[u] : L2;
+        H2 = u == h + 2 ? Hw[u] : H2;
+        V2 = u == h + 2 ? Vw[u] : V2;
+      }
+      uint32_t a0 = 0xFFFFFFFFu, a1 = 0xFFFFFFFFu;
+      for (int j = 0; j < m; ++j) {  // the letters j of the 32 starts, exception letters as matches
+        const bool lo = j < 32;
+        const uint32_t sj = (uint32_t)(j & 31);
+        const uint32_t Ls = lo ? funnel(L1, L0, sj) : funnel(L2, L1, sj);
+        const uint32_t Hs = lo ? funnel(H1, H0, sj) : funnel(H2, H1, sj);
+        const uint32_t Vs = lo ? funnel(V1, V0, sj) : funnel(V2, V1, sj);
+        const uint32_t Es = lo ? funnel(e1, e0, sj) : funnel(e2, e1, sj);
+        const uint32_t* t = P.tm_scan[j];
+        const uint32_t q = (bfi(Hs, bfi(Ls, t[3], t[2]), bfi(Ls, t[1], t[0])) & Vs) | Es;
+        a1 = (a1 & q) | a0;
+        a0 &= q;
+      }
+      if (m <= 1) a1 &= V0;
+      // each exception letter's mismatches (one letter per start and exception)
+      for (int32_t k = kb; k < rc.n_exc; ++k) {
+        const int64_t y = exc_at(k) - base;
+        if (y > 31 + m - 1) break;
+        if (y < 0) continue;
+        const uint32_t cd = code_of(k);
+        uint32_t M = 0u;
+        for (int j = 0; j < m; ++j) {
+          const int64_t sb = y - j;  // the start whose letter j is y
+          const uint32_t pc = P.code[j];
+          const bool mm = eqx ? (cd != pc) : ((cd & pc) == 0u);
+          M |= (mm && sb >= 0 && sb < 32) ? (1u << (uint32_t)sb) : 0u;
+        }
+        a1 = (a1 & ~M) | (a0 & M);
+        a0 &= ~M;
+      }
+#pragma unroll
+      for (int u = 0; u < NH; ++u) {
+        x0[u] = u == h ? a0 : x0[u];
+        x1[u] = u == h ? a1 : x1[u];
+      }
+    }
+    if (h1 > hdone) hdone = h1;
+  }
+}
+
 
 __device__ __forceinline__ int wstart(const Lane& c, int i) { return 1 + i * c.L; }
 __device__ __forceinline__ int wend(const Lane& c, int i) { return i == c.nw - 1 ? c.n : wstart(c, i) + c.L - 1; }
@@ -372,11 +497,7 @@ static __device__ __forceinline__ void nb_compute(const Lane& c, int q0, const N
     launder_words<NP>(Hw, Hp);
     launder_words<NP>(Vw, Vp);
     words_hits<NH, kX, decltype(d), kPass == 0>(d, Lp, Hp, Vp, x0, x1);
-    if (c.rc.n_exc) {
-#pragma unroll
-      for (int h = 0; h < NH; ++h)
-        patch_exceptions(c.rc, (int64_t)q0 + 32 * (h + T0), 0, c.n - 1, *d.P, false, x0[h], x1[h]);
-    }
+    if (c.rc.n_exc) patch_words<NH, NP>(c, (int64_t)q0 + 32 * T0, Lw, Hw, Vw, *d.P, x0, x1);
     // coverage word ci (i = ci - E) from hit words i and i - 1 (patterns <= 18 letters)
     const bool k1 = pk(c) != 0;
 #pragma unroll
@@ -401,11 +522,7 @@ static __device__ __forceinline__ void nb_compute(const Lane& c, int q0, const N
       launder_words<NP>(Hw, Hp);
       launder_words<NP>(Vw, Vp);
       words_hits<NH, kX>(d, Lp, Hp, Vp, x0, x1);
-      if (c.rc.n_exc) {
-#pragma unroll
-        for (int h = 0; h < NH; ++h)
-          patch_exceptions(c.rc, (int64_t)q0 + 32 * (h + T0), 0, c.n - 1, *d.P, false, x0[h], x1[h]);
-      }
+      if (c.rc.n_exc) patch_words<NH, NP>(c, (int64_t)q0 + 32 * T0, Lw, Hw, Vw, *d.P, x0, x1);
       if (ptvr(c)) {
 #pragma unroll
         for (int ci = 0; ci < NC; ++ci) {
@@ -790,7 +907,8 @@ static __device__ __forceinline__ void hits_at_w(const Lane& c, const Pw<K>& w, 
     Vw[0] = range_mask(base, vlo, vhi);
     Vw[1] = range_mask((int64_t)base + 32, vlo, vhi);
     words_hits<1, 0>(d, Lw, Hw, Vw, &a0, &a1);
-    if (c.rc.n_exc) patch_exceptions(c.rc, base, vlo, vhi, *d.P, true, a0, a1);
+    if (c.rc.n_exc && (int64_t)base + 31 + d.m() - 1 >= c.exc_lo && (int64_t)base <= c.exc_hi)
+      patch_exceptions(c.rc, base, vlo, vhi, *d.P, true, a0, a1);
   }
 }
 
@@ -857,6 +975,33 @@ static __device__ __forceinline__ int search_left(const Lane& c, const Pw<K>& w,
   return new_start;
 }
 
+// exc_windows (nt_common.h, the rule nt_exc_marks applies on the host) over
+// the lane's exceptions: from its registers when the read has at most
+// kExcLocal, else from memory.
+template <class F>
+static __device__ __forceinline__ int lane_exc_windows(const Lane& c, int cap, F&& f) {
+  const int mm = c.prog->m_max, L = c.L, nw = c.nw, n = c.n;
+  int cnt = 0, next = 0;
+  for (int32_t i = 0; i < c.rc.n_exc && next < nw - 1; ++i) {
+    uint32_t xi = 0u;
+#pragma unroll
+    for (int k = 0; k < kExcLocal; ++k) xi = k == i ? c.xpos[k] : xi;
+    const int p = c.rc.n_exc <= kExcLocal ? (int)xi : (int)c.rc.exc_pos[i];
+    const int a = p - (mm - 1) < 0 ? 0 : p - (mm - 1);
+    const int b = p + (mm - 1) > n - 1 ? n - 1 : p + (mm - 1);
+    int w0 = a / L, w1 = b / L;
+    if (w1 > nw - 2) w1 = nw - 2;
+    if (w0 < next) w0 = next;
+    for (int w = w0; w <= w1; ++w) {
+      if (cnt == cap) return cap + 1;
+      ++cnt;
+      f(w);
+    }
+    if (w1 + 1 > next) next = w1 + 1;
+  }
+  return cnt;
+}
+
 // The last window of a read scanned by the bundle scan (nt_tscan.h): that scan
 // does not mask the read ends, so the window holding them -- whose width may
 // differ from L, and into which split_telo may have merged a short last block
@@ -875,15 +1020,15 @@ static __device__ __forceinline__ int search_left(const Lane& c, const Pw<K>& w,
 static __device__ __forceinline__ void call_fix_windows(Lane& c, const uint32_t* __restrict__ thr, uint32_t thr_size) {
   if (c.nw <= 0) return;
   int ne = 0;
-  if (c.rc.n_exc) {
-    ne = exc_windows(c.rc.exc_pos, (uint32_t)c.rc.n_exc, c.n, c.L, c.nw, c.prog->m_max, NT_EXC_WINDOWS, [](int) {});
+  if (c.rc.n_exc && !NT_DBG_NO_EXC_FIX) {
+    ne = lane_exc_windows(c, NT_EXC_WINDOWS, [](int) {});
     if (ne > NT_EXC_WINDOWS) ne = 0;
   }
   for (int k = 0; k <= ne; ++k) {
     int w = c.nw - 1;  // the last window after the exception windows
     if (k < ne) {
       int i = 0;
-      exc_windows(c.rc.exc_pos, (uint32_t)c.rc.n_exc, c.n, c.L, c.nw, c.prog->m_max, k + 1, [&](int x) {
+      lane_exc_windows(c, k + 1, [&](int x) {
         if (i++ == k) w = x;
       });
     }
@@ -1000,6 +1145,17 @@ static __device__ __forceinline__ void init_lane(Lane& c, const NtProgram* __res
     c.rc.n_exc = (int32_t)(e1 - e0);
     c.rc.exc_pos = B.exc_pos + e0;
     c.rc.exc_code = B.exc_code + e0;
+    if (e1 > e0) {
+      c.exc_lo = B.exc_pos[e0];
+      c.exc_hi = B.exc_pos[e1 - 1];
+      c.xcode = 0u;
+#pragma unroll
+      for (int k = 0; k < kExcLocal; ++k) {
+        const bool ok = e0 + (uint32_t)k < e1;
+        c.xpos[k] = ok ? B.exc_pos[e0 + k] : 0xFFFFFFFFu;
+        c.xcode |= (ok ? (uint32_t)B.exc_code[e0 + k] : 0u) << (8 * k);
+      }
+    }
   }
   c.prog = prog;
   c.n = (int)n32;
