@@ -16,6 +16,7 @@
 #include <dlfcn.h>
 #include <sys/stat.h>
 #include <unistd.h>
+#include <utime.h>
 
 #include <cstdio>
 #include <cstdlib>
@@ -264,6 +265,9 @@ bool cache_read(const std::string& path, std::vector<char>& code) {
     ok = std::fread(code.data(), 1, (size_t)n, f) == (size_t)n;
   }
   std::fclose(f);
+  // a hit marks the object as in use (tools/jit_cache_gc.sh drops the objects
+  // no prebuild touched)
+  if (ok) (void)utime(path.c_str(), nullptr);
   return ok;
 }
 
