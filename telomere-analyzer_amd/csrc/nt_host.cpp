@@ -338,10 +338,21 @@ int nt_create(int device, nt_ctx** out) {
 
 void nt_destroy(nt_ctx* ctx) {
   if (!ctx) return;
+  // NT_DESTROY_TIMES=1 (diagnostics): the teardown's phases on stderr
+  const bool tt = std::getenv("NT_DESTROY_TIMES") != nullptr;
+  double t0 = now_s();
+  auto lap = [&](const char* what) {
+    if (!tt) return;
+    const double t = now_s();
+    std::fprintf(stderr, "nt_destroy: %s %.4f s\n", what, t - t0);
+    t0 = t;
+  };
   if (ctx->cjit_build.valid()) ctx->cjit_build.wait();
+  lap("calling-kernel build");
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->call_stream) (void)hipStreamSynchronize(ctx->call_stream);
+  lap("streams");
   if (ctx->prog_dev) (void)hipFree(ctx->prog_dev);
   if (ctx->ev_scan) (void)hipEventDestroy(ctx->ev_scan);
   if (ctx->ev_call) (void)hipEventDestroy(ctx->ev_call);
@@ -351,7 +362,9 @@ void nt_destroy(nt_ctx* ctx) {
   for (auto& a : ctx->ev)
     for (hipEvent_t ev : a) (void)hipEventDestroy(ev);
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
+  lap("events and streams destroyed");
   delete ctx;
+  lap("buffers freed");
 }
 
 const char* nt_last_error(const nt_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }

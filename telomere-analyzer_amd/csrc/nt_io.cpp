@@ -47,6 +47,117 @@ static bool gz_failed(gzFile g) {
   return e != Z_OK && e != Z_STREAM_END;
 }
 
+// Inflated files and stream windows live in anonymous mappings that are
+// reused, not unmapped: freeing a gigabyte of pages (munmap) costs ~0.1 s of
+// kernel time and holds the process's mm lock, which the HIP runtime's own
+// calls wait on -- a 16-part fastq.gz run (16 GB inflated) spent 0.7 s of
+// reader time unmapping and its context teardown waited 0.3-0.7 s behind it
+// (2.6 s read wait and 0.3-0.6 s teardown with the unmaps, 1.9 s and 2 ms
+// without).  The process keeps up to NT_READER_POOL_GB (default 32) of them for
+// the next parts and the next reader; a buffer grows with mremap (the page
+// tables move, nothing is copied).
+struct MPool {
+  std::mutex mu;
+  std::vector<std::pair<char*, size_t>> free;
+  size_t bytes = 0, limit = 0;
+  MPool() {
+    const char* v = std::getenv("NT_READER_POOL_GB");
+    limit = (size_t)(v ? std::atof(v) : 32.0) << 30;
+  }
+  char* take(size_t want, size_t& cap) {
+    std::lock_guard<std::mutex> lk(mu);
+    size_t best = free.size();
+    for (size_t i = 0; i < free.size(); ++i)
+      if (free[i].second >= want && (best == free.size() || free[i].second < free[best].second)) best = i;
+    if (best == free.size() && !free.empty()) {  // none big enough: the biggest, grown by the caller
+      best = 0;
+      for (size_t i = 1; i < free.size(); ++i)
+        if (free[i].second > free[best].second) best = i;
+    }
+    if (best == free.size()) return nullptr;
+    char* p = free[best].first;
+    cap = free[best].second;
+    bytes -= cap;
+    free.erase(free.begin() + (ptrdiff_t)best);
+    return p;
+  }
+  void give(char* p, size_t cap) {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      if (bytes + cap <= limit) {
+        free.emplace_back(p, cap);
+        bytes += cap;
+        return;
+      }
+    }
+    constexpr size_t kStep = 256u << 20;  // (over the limit: unmapped in steps, the lock released between)
+    for (size_t off = 0; off < cap; off += kStep) munmap(p + off, std::min(kStep, cap - off));
+  }
+};
+static MPool& mpool() {
+  static MPool* p = new MPool;  // (never destroyed: the mappings go with the process)
+  return *p;
+}
+
+struct MBuf {
+  char* p = nullptr;
+  size_t n = 0, cap = 0;
+  MBuf() = default;
+  MBuf(const MBuf&) = delete;
+  MBuf& operator=(const MBuf&) = delete;
+  MBuf(MBuf&& o) noexcept { swap(o); }
+  MBuf& operator=(MBuf&& o) noexcept {
+    if (this != &o) {
+      release();
+      swap(o);
+    }
+    return *this;
+  }
+  ~MBuf() { release(); }
+  char* data() { return p; }
+  const char* data() const { return p; }
+  size_t size() const { return n; }
+  bool reserve(size_t want) {
+    if (want <= cap) return true;
+    const size_t c = (want + (2u << 20) - 1) & ~((size_t)(2u << 20) - 1);  // 2 MB steps
+    if (!p) p = mpool().take(c, cap);
+    if (c <= cap) return true;
+    void* q = p ? mremap(p, cap, c, MREMAP_MAYMOVE) : mmap(nullptr, c, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (q == MAP_FAILED) return false;
+    p = (char*)q;
+    cap = c;
+    return true;
+  }
+  bool resize(size_t m) {
+    if (!reserve(m)) return false;
+    n = m;
+    return true;
+  }
+  void swap(MBuf& o) {
+    std::swap(p, o.p);
+    std::swap(n, o.n);
+    std::swap(cap, o.cap);
+  }
+  void release() {
+    if (p) mpool().give(p, cap);
+    p = nullptr;
+    n = cap = 0;
+  }
+};
+
+// gzip's ISIZE (the uncompressed size mod 2^32 of the last member): a
+// capacity hint for a part inflated whole
+static size_t gz_isize_hint(const std::string& path) {
+  FILE* f = std::fopen(path.c_str(), "rb");
+  if (!f) return 0;
+  unsigned char b[4] = {0, 0, 0, 0};
+  size_t hint = 0;
+  if (std::fseek(f, -4, SEEK_END) == 0 && std::fread(b, 1, 4, f) == 4)
+    hint = (size_t)b[0] | ((size_t)b[1] << 8) | ((size_t)b[2] << 16) | ((size_t)b[3] << 24);
+  std::fclose(f);
+  return hint;
+}
+
 // Whole-file inflation of the next files of a multi-file input, ahead of the
 // parser: worker threads take files in order, at most `window` beyond the one
 // being parsed; the parser waits for its file's buffer.
@@ -54,7 +165,7 @@ struct Prefetcher {
   struct Slot {
     bool done = false, plain = false;  // plain: not gzip, the parser reads it itself (parallel pread)
     std::string err;
-    std::vector<char> data;
+    MBuf data;
   };
   std::vector<std::string> files_;  // the files in the order the parser takes them (the reader's plan)
   const std::vector<std::string>* files = nullptr;
@@ -94,8 +205,12 @@ struct Prefetcher {
       } else {
         gzbuffer(g, 1 << 20);
         size_t used = 0;
+        (void)sl.data.resize(gz_isize_hint((*files)[i]) + (4u << 20));  // (a hint: grows if it is short)
         for (;;) {
-          if (sl.data.size() - used < (4u << 20)) sl.data.resize(std::max<size_t>(8u << 20, sl.data.size() * 2));
+          if (sl.data.size() - used < (4u << 20) && !sl.data.resize(std::max<size_t>(8u << 20, sl.data.size() * 2))) {
+            sl.err = "out of memory inflating " + (*files)[i];
+            break;
+          }
           const int n = gzread(g, sl.data.data() + used, (unsigned)std::min<size_t>(sl.data.size() - used, 1u << 30));
           if (n < 0 || (n == 0 && gz_failed(g))) {
             sl.err = "read error in " + (*files)[i];
@@ -116,10 +231,10 @@ struct Prefetcher {
     }
   }
   // the inflated file i (waits for it); releases the window for one more file
-  bool take(size_t i, std::vector<char>& out, bool& plain, std::string& err) {
+  bool take(size_t i, MBuf& out, bool& plain, std::string& err) {
     std::unique_lock<std::mutex> lk(mu);
     consumed = i + 1;
-    for (; freed < i; ++freed) std::vector<char>().swap(slots[freed].data);  // passed over by a seek
+    for (; freed < i; ++freed) slots[freed].data.release();  // passed over by a seek
     cv.notify_all();
     cv.wait(lk, [&] { return slots[i].done; });
     if (!slots[i].err.empty()) {
@@ -129,7 +244,7 @@ struct Prefetcher {
     plain = slots[i].plain;
     if (plain) return true;
     out.swap(slots[i].data);
-    std::vector<char>().swap(slots[i].data);
+    slots[i].data.release();
     return true;
   }
   ~Prefetcher() {
@@ -147,7 +262,7 @@ struct Prefetcher {
 // that hold pointers into a buffer keep it alive (a chunk stays valid through
 // the next nt_reader_next call).
 struct RBuf {
-  std::vector<char> own;
+  MBuf own;
   void* map = nullptr;
   size_t map_len = 0;
   const char* data = nullptr;
@@ -322,7 +437,11 @@ bool more(nt_reader* r) {
   const size_t keep = r->end - r->pos;
   size_t cap = std::max(kWindow, 2 * keep);
   auto nb = std::make_shared<RBuf>();
-  nb->own.resize(cap);
+  if (!nb->own.resize(cap)) {
+    r->err = "out of memory reading " + r->files[r->cur_file];
+    r->src_eof = true;
+    return false;
+  }
   if (keep) std::memcpy(nb->own.data(), r->win->data + r->pos, keep);
   size_t got = keep;
   while (got < cap) {
