@@ -555,8 +555,6 @@ def run(input_path, save_path, patterns, fmt="fastq", nrec=10000, rc=False, min_
         stats["groups_rounds"] = g
     tc = time.time()
     rdr.close()
-    if os.environ.get("NT_DBG_CLOSE_SLEEP"):  # diagnostics: a pause before the context's teardown
-        time.sleep(float(os.environ["NT_DBG_CLOSE_SLEEP"]))
     tc2 = time.time()
     nt.close()
     if stats is not None:  # (inside "final")
