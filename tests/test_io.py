@@ -109,6 +109,28 @@ def test_reader_run_directory_inflated_ahead(tmp_path, monkeypatch, threads):
         _chunks(str(d), "fastq", 1000)
 
 
+def test_reader_parts_outgrow_the_isize_hint(tmp_path, monkeypatch):
+    """Parts inflated whole start at the size their gzip trailer (ISIZE) gives:
+    a multi-member part (bgzip-style, the trailer holds the LAST member's size)
+    and a part of 40 MB must grow past it; the mappings go back to the reader's
+    pool and serve the next reader in the process (read twice, same records)."""
+    monkeypatch.setenv("NT_READER_THREADS", "2")
+    rng = np.random.default_rng(9)
+    acgt = np.frombuffer(b"ACGT", np.uint8)
+    recs = [(f"m{i}", acgt[rng.integers(0, 4, int(rng.integers(50, 5000)))].tobytes().decode()) for i in range(400)]
+    d = tmp_path / "run"
+    d.mkdir()
+    with open(d / "part_00.fastq.gz", "wb") as f:  # 40 members, the last one tiny
+        for k in range(40):
+            sub = recs[10 * k:10 * k + 10] if k < 39 else recs[390:391]
+            f.write(gzip.compress("".join(f"@{n}\n{s}\n+\n{'I' * len(s)}\n" for n, s in sub).encode()))
+    big = [(f"b{i}", acgt[rng.integers(0, 4, 20000)].tobytes().decode()) for i in range(1000)]
+    _write_fastq(d / "part_01.fastq.gz", big, gz=True)
+    want = recs[:391] + big
+    for _ in range(2):
+        assert sum(_chunks(str(d), "fastq", 97), []) == want
+
+
 def test_reader_skips_dot_files(tmp_path):
     """dir(recursive = TRUE) leaves out names starting with '.' (all.files =
     FALSE, NanoTel.R:2176): AppleDouble '._*' parts, .DS_Store and hidden
