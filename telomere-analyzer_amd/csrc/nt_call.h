@@ -1018,6 +1018,9 @@ static __device__ __forceinline__ int lane_exc_windows(const Lane& c, int cap, F
 // counts are exact and only its last window is recounted.  One coverage site
 // for all of them (the windows in a rolled loop).
 static __device__ __forceinline__ void call_fix_windows(Lane& c, const uint32_t* __restrict__ thr, uint32_t thr_size) {
+#ifdef NT_DBG_NO_FIX  // timing experiments only (results wrong): no recounts at all
+  return;
+#endif
   if (c.nw <= 0) return;
   int ne = 0;
   if (c.rc.n_exc && !NT_DBG_NO_EXC_FIX) {
