@@ -1232,7 +1232,7 @@ __device__ __forceinline__ void tscan_bundles(const NtBatch& B, const NtOut& O, 
 
 
 // ======================================================================
-// Walker / writer waves (NT_TS_WS, the default).
+// Walker / writer waves (NT_TS_WS=1; off by default: measured no faster).
 //
 // On gfx9 a wave's vector-memory counter covers its loads AND its stores, in
 // issue order: once a wave has issued a store, every later wait for one of its
