@@ -134,6 +134,30 @@ def cpu_baseline(cfg, budget_s=12.0):
     return out
 
 
+class _ContigBuf:
+    """A device buffer from hipExtMallocWithFlags(hipDeviceMallocContiguous):
+    physically contiguous HBM, mapped with large pages.  The scans stream the
+    planes and the T-layout from 1,024 places at once; from torch's allocator
+    (hipMalloc) a box whose HBM is fragmented maps them with small pages and
+    the bundle scan ran 1.53 ms a range instead of 1.38 (same box, same data;
+    profiles/r04/contig/).  The library allocates its own buffers the same way."""
+
+    def __init__(self, nbytes):
+        import ctypes
+        self._hip = ctypes.CDLL("libamdhip64.so")
+        self._p = ctypes.c_void_p()
+        rc = self._hip.hipExtMallocWithFlags(ctypes.byref(self._p), ctypes.c_size_t(max(1, nbytes)), ctypes.c_uint(4))
+        if rc != 0:
+            raise RuntimeError(f"hipExtMallocWithFlags(contiguous, {nbytes}) failed: {rc}")
+
+    def data_ptr(self):
+        return self._p.value
+
+    def __del__(self):
+        if getattr(self, "_p", None) and self._p.value:
+            self._hip.hipFree(self._p)
+
+
 def exc_synth(n, read_len, frac, rank):
     """Exception lists for --n-frac: every round(1/frac)-th read carries one N
     (Biostrings code 15) at a seeded random position -> (exc_off [n+1],
@@ -245,12 +269,25 @@ def main():
     npass = nt.n_pass
     nblk = read_blocks(L)  # even block slot per read (16-byte segments)
     nw = window_count(L, 100)
-    planes = torch.empty(n * nblk * 2, dtype=torch.int32, device=dev)
+    # the batch's big buffers in contiguous HBM (_ContigBuf; NT_BENCH_CONTIG=0:
+    # torch's allocator), torch's when a contiguous allocation fails
+    contig = os.environ.get("NT_BENCH_CONTIG", "1") != "0"
+
+    def big_buffer(nbytes, dtype):
+        if contig:
+            try:
+                return _ContigBuf(nbytes)
+            except RuntimeError:
+                pass
+        return torch.empty(max(1, nbytes // torch.tensor([], dtype=dtype).element_size()), dtype=dtype, device=dev)
+
+    planes = big_buffer(n * nblk * 2 * 4, torch.int32)
     blk_off = torch.empty(n, dtype=torch.int64, device=dev)
     lens = torch.empty(n, dtype=torch.int32, device=dev)
     win_off = torch.empty(n, dtype=torch.int64, device=dev)
     rows = window_rows(nw)  # padded count rows (16-byte aligned, nt_common.h)
-    wc = torch.empty(n * rows * npass, dtype=torch.uint8 if nt.count_bytes == 1 else torch.int16, device=dev)
+    wc_bytes = n * rows * npass * nt.count_bytes
+    wc = big_buffer(wc_bytes, torch.uint8)
     start = torch.empty(n * 3, dtype=torch.int32, device=dev)
     end = torch.empty(n * 3, dtype=torch.int32, device=dev)
     dens = torch.empty(n * 3, dtype=torch.float64, device=dev)
@@ -277,7 +314,7 @@ def main():
     # a second output set and aux buffer.
     margin = 4 << 30
     aux_bytes = 64 * npass * (rows // 64 + 2) * n
-    out_bytes = sum(x.numel() * x.element_size() for x in (start, end, dens, flags, wc))
+    out_bytes = sum(x.numel() * x.element_size() for x in (start, end, dens, flags)) + wc_bytes
     want_pipe = not args.no_pipeline
     if nt.tscan and not args.per_read:
         lens_h = np.full(n, L, np.uint32)
@@ -308,7 +345,7 @@ def main():
             scan_path += "; " + cap_note
         bread = torch.from_numpy(plan.bnd_read.view(np.int32)).to(dev)
         bstripe = torch.from_numpy(plan.bnd_stripe.view(np.int64)).to(dev)
-        tpl = torch.empty(max(1, plan.tplane_bytes // 4), dtype=torch.int32, device=dev)
+        tpl = big_buffer(plan.tplane_bytes, torch.int32)
         # reads the plan leaves outside the bundles go to the per-read scan
         blist = torch.from_numpy(plan.list.view(np.int32)).to(dev) if len(plan.list) else None
         keep = [bread, bstripe, tpl, blist]
@@ -326,7 +363,7 @@ def main():
     pipelined = bundles is not None and want_pipe
     outs = [(start, end, dens, flags, wc)]
     if pipelined:
-        outs.append(tuple(torch.empty_like(x) for x in outs[0]))
+        outs.append(tuple(torch.empty_like(x) for x in outs[0][:4]) + (big_buffer(wc_bytes, torch.uint8),))
         nt.set_pipelined(True)
     k_step = [0]
 

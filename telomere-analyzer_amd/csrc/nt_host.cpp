@@ -126,6 +126,19 @@ struct HostBuf {
   }
 };
 
+// Device buffers in physically contiguous HBM (hipDeviceMallocContiguous),
+// hipMalloc when that fails: the scans stream the planes, the T-layout and the
+// counts from a thousand places at once, and on a box whose HBM is fragmented
+// plain hipMalloc memory is mapped with small pages -- the c50k bundle scan ran
+// 1.53 ms a range there instead of 1.38 (profiles/r04/contig/).  NT_DEV_CONTIG=0:
+// hipMalloc only.
+static bool dev_contig() {
+  static const bool on = [] {
+    const char* v = std::getenv("NT_DEV_CONTIG");
+    return !(v && v[0] == '0');
+  }();
+  return on;
+}
 struct DevBuf {
   void* p = nullptr;
   size_t cap = 0;
@@ -135,7 +148,13 @@ struct DevBuf {
     p = nullptr;
     cap = 0;
     const size_t want = std::max<size_t>(bytes, 256);
-    hipError_t e = hipMalloc(&p, want);
+    hipError_t e = hipErrorOutOfMemory;
+    if (want >= (64u << 20) && dev_contig()) e = hipExtMallocWithFlags(&p, want, hipDeviceMallocContiguous);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();  // (a failed contiguous request leaves the error state set)
+      p = nullptr;
+      e = hipMalloc(&p, want);
+    }
     if (e == hipSuccess) cap = want;
     return e;
   }
