@@ -273,12 +273,18 @@ def main():
     # torch's allocator), torch's when a contiguous allocation fails
     contig = os.environ.get("NT_BENCH_CONTIG", "1") != "0"
 
+    alloc_kinds = []
+
     def big_buffer(nbytes, dtype):
         if contig:
             try:
-                return _ContigBuf(nbytes)
+                b = _ContigBuf(nbytes)
+                alloc_kinds.append("contiguous")
+                return b
             except RuntimeError:
-                pass
+                alloc_kinds.append("hipMalloc (contiguous refused)")
+        else:
+            alloc_kinds.append("hipMalloc")
         return torch.empty(max(1, nbytes // torch.tensor([], dtype=dtype).element_size()), dtype=dtype, device=dev)
 
     planes = big_buffer(n * nblk * 2 * 4, torch.int32)
@@ -453,6 +459,7 @@ def main():
                        "patterns": cfg["patterns"], "subseq_length": 100, "min_density": 0.6,
                        "passes": npass, "telomeric_reads_rank0": telo, "scan_path": scan_path,
                        "pipelined": pipelined,
+                       "device_buffers": ", ".join(sorted(set(alloc_kinds))),
                        **({"reads_with_an_n": round(args.n_frac, 6)} if args.n_frac > 0 else {}),
                        "parallelism": f"dp{world} (read shards)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
