@@ -201,7 +201,36 @@ def _launch_ranks(n):
     return subprocess.run(cmd, env=env).returncode
 
 
+# Environment variables that change WHAT a step computes or measures: timing
+# builds and skipped kernels (results wrong), or a T-layout path that no longer
+# exists.  bench.py refuses to run with any of them (a stray variable must not
+# give a fast, wrong, credited number); every other NT_* knob in the
+# environment is recorded in the line (config.env_knobs).
+REFUSED_PREFIXES = ("NT_DBG_", "NT_TS_DBG")
+REFUSED_VARS = ("NT_JIT_OPTS", "NT_HOST_TLAYOUT", "NT_TS_WS")
+
+
+def refused_env(env=None):
+    """The refused variables set in env (os.environ), as 'NAME=value'."""
+    env = os.environ if env is None else env
+    bad = [k for k in env if k.startswith(REFUSED_PREFIXES) or k in REFUSED_VARS]
+    if env.get("NT_TSCAN", "1").startswith("0"):
+        bad.append("NT_TSCAN")
+    return sorted(f"{k}={env[k]}" for k in set(bad))
+
+
+def env_knobs(env=None):
+    """Every NT_* variable of the run (tuning knobs; none of them changes results)."""
+    env = os.environ if env is None else env
+    return {k: env[k] for k in sorted(env) if k.startswith("NT_")}
+
+
 def main():
+    bad = refused_env()
+    if bad:
+        print("bench.py: refusing to run with timing/debug variables set (they change what a step computes): "
+              + ", ".join(bad), file=sys.stderr)
+        sys.exit(2)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -305,60 +334,36 @@ def main():
     exc_h = exc_synth(n, L, args.n_frac, rank)
     exc_d = [torch.from_numpy(a.view(np.int32) if a.dtype == np.uint32 else a).to(dev) for a in exc_h] if exc_h else []
     exc_ptrs = [a.data_ptr() for a in exc_d] if exc_d else [0, 0, 0]
-    # the bundle layout (the reads transposed 32 to a bundle, the bundle scan's
-    # copy of them), built on the device before the timed region like the planes
+    # the bundles (reads grouped 32 to a bundle, scanned together from their
+    # own planes -- the batch holds one copy of the reads): the plan, built on
+    # the host from the lengths and block offsets as a product batch's is
     bundles, keep = None, []
     scan_path = "per-read"
     plan = None
-    cap_note = None
     # device memory: the planes, outputs and the library's aux buffer (8 np
-    # (rows/64 + 2) u64 a read, allocated at the first call) are resident; the
-    # bundle layout is a second copy of the reads (the calling kernel reads the
-    # per-read planes).  When both copies do not fit, the bundle scan takes the
-    # reads whose layout fits and the rest stay with the per-read scan (marked
-    # for it in the plan, as reads with non-ACGT letters are); pipelining needs
-    # a second output set and aux buffer.
+    # (rows/64 + 2) u64 a read, allocated at the first call) are resident;
+    # pipelining needs a second output set and aux buffer
     margin = 4 << 30
     aux_bytes = 64 * npass * (rows // 64 + 2) * n
     out_bytes = sum(x.numel() * x.element_size() for x in (start, end, dens, flags)) + wc_bytes
-    want_pipe = not args.no_pipeline
+    free, _ = torch.cuda.mem_get_info(dev)
+    want_pipe = not args.no_pipeline and 2 * aux_bytes + out_bytes + margin <= free
     if nt.tscan and not args.per_read:
         lens_h = np.full(n, L, np.uint32)
         # reads whose letters reach too many windows stay on the per-read scan
         marks = nt.exc_marks(lens_h, exc_h[0], exc_h[1]) if exc_h else None
-        plan = nt.bundle_plan(lens_h, marks)
-        free, _ = torch.cuda.mem_get_info(dev)
-        if plan.tplane_bytes + aux_bytes + margin > free:
-            per = plan.tplane_bytes / max(1, n)
-            k = int((free - aux_bytes - margin) / per) // 32 * 32 if free > aux_bytes + margin else 0
-            if k >= 32 * 128:  # at least two bundle ranges' worth
-                has_exc = np.zeros(n, np.uint8) if marks is None else marks.copy()
-                has_exc[k:] = 1
-                plan = nt.bundle_plan(lens_h, has_exc)
-                cap_note = (f"bundle layout for {k} of {n} reads (planes + layout beside the outputs fill "
-                            f"the GPU); the other {n - k} on the per-read scan")
-            else:
-                plan = None
-                scan_path = "per-read (bundle layout does not fit beside the planes)"
-        if plan is not None:
-            want_pipe = want_pipe and plan.tplane_bytes + 2 * aux_bytes + out_bytes + margin <= free
+        plan = nt.bundle_plan(lens_h, marks, blk_off=np.arange(n, dtype=np.uint64) * nblk)
     if plan is not None and plan.n_bundles == 0:
         plan = None
     if plan is not None:
         from nanotel_amd.api import DeviceBundles
         scan_path = "bundle" if len(plan.list) == 0 else f"bundle + per-read ({len(plan.list)} reads)"
-        if cap_note:
-            scan_path += "; " + cap_note
         bread = torch.from_numpy(plan.bnd_read.view(np.int32)).to(dev)
-        bstripe = torch.from_numpy(plan.bnd_stripe.view(np.int64)).to(dev)
-        tpl = big_buffer(plan.tplane_bytes, torch.int32)
         # reads the plan leaves outside the bundles go to the per-read scan
         blist = torch.from_numpy(plan.list.view(np.int32)).to(dev) if len(plan.list) else None
-        keep = [bread, bstripe, tpl, blist]
-        bundles = DeviceBundles(tpl.data_ptr(), bread.data_ptr(), bstripe.data_ptr(), plan.n_bundles,
-                                blist.data_ptr() if blist is not None else 0, len(plan.list), plan.tplane_bytes)
-        nt.bundle_layout_device(planes.data_ptr(), blk_off.data_ptr(), lens.data_ptr(), win_off.data_ptr(),
-                                n, n * rows, bundles)
+        keep = [bread, blist]
+        bundles = DeviceBundles(bread.data_ptr(), plan.n_bundles, blist.data_ptr() if blist is not None else 0,
+                                len(plan.list))
     torch.cuda.synchronize(dev)
 
     # Pipelined batches (nt_set_pipelined): a step returns with its last bundle
@@ -459,6 +464,7 @@ def main():
                        "patterns": cfg["patterns"], "subseq_length": 100, "min_density": 0.6,
                        "passes": npass, "telomeric_reads_rank0": telo, "scan_path": scan_path,
                        "pipelined": pipelined,
+                       "env_knobs": env_knobs(),
                        "device_buffers": ", ".join(sorted(set(alloc_kinds))),
                        **({"reads_with_an_n": round(args.n_frac, 6)} if args.n_frac > 0 else {}),
                        "parallelism": f"dp{world} (read shards)"},

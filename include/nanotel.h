@@ -52,7 +52,8 @@ extern "C" {
 /* summary flags per read */
 #define NT_ROW_TELOMERIC 0x01 /* row emitted: max telomere width >= 30 (NanoTel.R:1847) */
 #define NT_ROW_NA(p) (0x02 << (p)) /* pass p start == -1 -> NA columns (NanoTel.R:1926) */
-#define NT_ROW_ERR_ALIGN 0x10 /* blk_off[r] odd: read skipped (layout contract) */
+#define NT_ROW_ERR_ALIGN 0x10 /* layout contract: blk_off[r] odd, or a bundle's planes more than 2 GiB apart;
+                                 the read was skipped */
 #define NT_ROW_DONE 0x80
 
 typedef struct nt_ctx nt_ctx;
@@ -92,13 +93,15 @@ typedef struct {
   const uint8_t* exc_code;
   uint64_t n_reads;
   uint64_t n_windows;       /* sum of the window rows (win_counts has n_windows*n_pass entries) */
-  /* Bundle scan (optional): the reads transposed 32 to a bundle
-   * (nt_bundle_plan + nt_bundle_layout).  tplanes == NULL: every read takes the
+  /* Bundle scan (optional): reads grouped 32 to a bundle
+   * (nt_bundle_plan), scanned together from their own planes (no second copy
+   * of the reads).  bnd_read == NULL or n_bundles == 0: every read takes the
    * per-read scan.  Else the bundled reads take the bundle scan and the reads
-   * in list[0 .. n_list) the per-read scan (list may be NULL when n_list == 0). */
-  const uint32_t* tplanes;
+   * in list[0 .. n_list) the per-read scan (list may be NULL when n_list == 0).
+   * A bundle's reads must lie within 2 GiB of planes of each other (what
+   * nt_bundle_plan guarantees when given blk_off); the reads of a bundle that
+   * does not are returned with NT_ROW_ERR_ALIGN. */
   const uint32_t* bnd_read;   /* [n_bundles * 32] read of each slot, ~0u = empty */
-  const uint64_t* bnd_stripe; /* [n_bundles + 1] first stripe of each bundle */
   uint64_t n_bundles;
   const uint32_t* list;       /* reads outside the bundles */
   uint64_t n_list;
@@ -156,7 +159,7 @@ int nt_pack_reads(const char* const* seqs, const uint64_t* lens, uint64_t n_read
                   int32_t subseq_length, uint32_t* planes, uint64_t* blk_off, uint32_t* len,
                   uint64_t* win_off, uint32_t* exc_off, uint32_t* exc_pos, uint8_t* exc_code);
 
-/* --- bundle layout (the bundle scan's copy of the reads) ------------------- */
+/* --- bundles (the bundle scan's groups of reads) -------------------------- */
 /* Host: which reads with non-ACGT letters must stay on the per-read scan.
  * The bundle scan takes reads with exceptions too: the calling kernel recounts
  * the windows within (longest pattern - 1) of an exception exactly, as it
@@ -168,31 +171,18 @@ int nt_pack_reads(const char* const* seqs, const uint64_t* lens, uint64_t n_read
 int nt_exc_marks(nt_ctx* ctx, const uint32_t* len, const uint32_t* exc_off, const uint32_t* exc_pos,
                  uint64_t n_reads, uint8_t* has_exc);
 /* Host: group the reads of a batch 32 to a bundle (longest first; the compiled
- * program fixes the block size L).  has_exc (NULL = none) marks reads that
+ * program fixes the window size L).  has_exc (NULL = none) marks reads that
  * stay outside the bundles and go to the per-read scan: reads whose non-ACGT
  * letters reach too many windows (nt_exc_marks; marking every read with an
- * exception list is allowed too), or any the caller leaves there (e.g. to
- * bound the T-layout's memory when a batch's planes and its layout do not
- * both fit); so do the reads of any program the bundle scan does not cover
- * (then *n_bundles = 0).  A read with exceptions in a bundle needs the
- * batch's exception lists in the nt_batch of nt_scan_call.  Outputs:
- * bnd_read [ceil(n/32)*32], bnd_stripe [ceil(n/32)+1], list [n] (the reads
- * left out, in order), and the bytes of the T-layout buffer. */
-int nt_bundle_plan(nt_ctx* ctx, const uint32_t* len, const uint8_t* has_exc, uint64_t n_reads,
-                   uint32_t* bnd_read, uint64_t* bnd_stripe, uint64_t* n_bundles, uint32_t* list,
-                   uint64_t* n_list, uint64_t* tplane_bytes);
-/* Host (ingest): write the T-layout of the planned bundles into the host
- * buffer tplanes (tplane_bytes from the plan; every byte written) from host
- * planes packed by nt_pack_reads -- a 32 x 32 bit transpose per 32-base block
- * (AVX2), all host threads.  (nt_analyze_host builds its batches' T-layout on
- * the device with the transposer of nt_bundle_layout after the planes'
- * upload; NT_HOST_TLAYOUT=1 takes this host build instead.) */
-int nt_bundle_layout_host(const uint32_t* planes, const uint64_t* blk_off, const uint32_t* len,
-                          const uint32_t* bnd_read, const uint64_t* bnd_stripe, uint64_t n_bundles,
-                          int32_t subseq_length, uint32_t* tplanes, uint64_t tplane_bytes);
-/* Device: the same T-layout (bit for bit) from the batch's device planes, for
- * callers whose reads are already resident.  Asynchronous on the context stream. */
-int nt_bundle_layout(nt_ctx* ctx, const nt_batch* batch, uint32_t* tplanes, uint64_t tplane_bytes);
+ * exception list is allowed too), or any the caller leaves there; so do the
+ * reads of any program the bundle scan does not cover (then *n_bundles = 0).
+ * blk_off (NULL = the caller vouches for it): the batch's block offsets; a
+ * bundle whose reads' planes do not lie within 2 GiB of each other goes to the
+ * per-read scan whole.  A read with exceptions in a bundle needs the batch's
+ * exception lists in the nt_batch of nt_scan_call.  Outputs: bnd_read
+ * [ceil(n/32)*32], list [n] (the reads left out, in order). */
+int nt_bundle_plan(nt_ctx* ctx, const uint32_t* len, const uint64_t* blk_off, const uint8_t* has_exc,
+                   uint64_t n_reads, uint32_t* bnd_read, uint64_t* n_bundles, uint32_t* list, uint64_t* n_list);
 
 /* --- the hot path --------------------------------------------------------- */
 /* Asynchronous on the context stream.  max_len = longest read of the batch. */
@@ -211,7 +201,7 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
  * this only overlaps the device work of consecutive ones. */
 int nt_set_pipelined(nt_ctx* ctx, int on);
 /* Pipelined only: a call's INPUTS (planes, lengths, offsets, exception
- * lists, the T-layout and bundle lists) are read by its last calling kernel
+ * lists and bundle lists) are read by its last calling kernel
  * after nt_scan_call returns, so they must not be overwritten (or freed) until
  * that calling is done.  nt_wait_call(ctx, back) makes the context stream wait
  * for the calling of the call `back` calls before the latest one (0 = the
@@ -267,7 +257,7 @@ int nt_analyze_host(nt_ctx* ctx, const char* const* seqs, const uint64_t* lens, 
                     void* win_counts, uint32_t* hits);
 
 /* Host-path phase times of the context's nt_analyze_host calls (seconds,
- * cumulative): [0] layout of the batch, [1] 2-bit packing, [2] T-layout,
+ * cumulative): [0] layout of the batch, [1] 2-bit packing, [2] bundle plan,
  * [3] uploads enqueued, [4] device work + downloads, [5] row checks. */
 int nt_host_times(const nt_ctx* ctx, double* t6);
 

@@ -195,7 +195,7 @@ static int rng_cmp(const void* a, const void* b) {
  * ranges dropped (union() uses drop.empty.ranges=TRUE). */
 static void rl_reduce(rlist* l) {
   int64_t w = 0;
-  qsort(l->v, (size_t)l->n, sizeof(rng), rng_cmp);
+  if (l->n > 1) qsort(l->v, (size_t)l->n, sizeof(rng), rng_cmp); /* (qsort of NULL, 0 is UB) */
   for (int64_t i = 0; i < l->n; i++) {
     rng r = l->v[i];
     if (r.e < r.s) continue;

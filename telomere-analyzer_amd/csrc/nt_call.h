@@ -201,12 +201,6 @@ struct Pos {
 constexpr int kTmRegs = NT_CALL_TM_LDS ? NT_CALL_TM_WORDS : 8;  // bitmask words held per lane
 
 constexpr int kExcLocal = 4;
-#ifndef NT_DBG_NO_EXC_FIX  // timing experiments only (results wrong): no exception-window recounts
-#define NT_DBG_NO_EXC_FIX 0
-#endif
-#ifndef NT_DBG_NO_EXC_PATCH  // timing experiments only (results wrong): neighbourhoods ignore exceptions
-#define NT_DBG_NO_EXC_PATCH 0
-#endif
 
 // Per-lane state of one read-pass.
 struct Lane {
@@ -256,7 +250,7 @@ __device__ __forceinline__ void patch_words(const Lane& c, int64_t hb, const uin
   const int64_t xlo = hb > 0 ? hb : 0;
   int64_t xhi = shi + m - 1;
   if (xhi > n - 1) xhi = n - 1;
-  if (xlo > xhi || xhi < (int64_t)c.exc_lo || xlo > (int64_t)c.exc_hi || NT_DBG_NO_EXC_PATCH) return;
+  if (xlo > xhi || xhi < (int64_t)c.exc_lo || xlo > (int64_t)c.exc_hi) return;
   const bool cached = rc.n_exc <= kExcLocal;
   auto exc_at = [&](int32_t i) -> int64_t {  // position of exception i
     uint32_t xi = 0u;
@@ -1018,12 +1012,9 @@ static __device__ __forceinline__ int lane_exc_windows(const Lane& c, int cap, F
 // counts are exact and only its last window is recounted.  One coverage site
 // for all of them (the windows in a rolled loop).
 static __device__ __forceinline__ void call_fix_windows(Lane& c, const uint32_t* __restrict__ thr, uint32_t thr_size) {
-#ifdef NT_DBG_NO_FIX  // timing experiments only (results wrong): no recounts at all
-  return;
-#endif
   if (c.nw <= 0) return;
   int ne = 0;
-  if (c.rc.n_exc && !NT_DBG_NO_EXC_FIX) {
+  if (c.rc.n_exc) {
     ne = lane_exc_windows(c, NT_EXC_WINDOWS, [](int) {});
     if (ne > NT_EXC_WINDOWS) ne = 0;
   }
@@ -1057,17 +1048,11 @@ static __device__ __forceinline__ void call_fix_windows(Lane& c, const uint32_t*
 static __device__ __forceinline__ void call_pass(Lane& c, int& out_s, int& out_e, double& out_d, uint32_t& err) {
   tm_preload(c);
   Pos tp = find_telo_position(c, 3, 2.0);
-#ifndef NT_DBG_NO_ACC
   // get_accurate_* neighbourhoods fetched with the wrapper's density loads
   // (one memory round trip less); refetched if the wrapper re-runs the call
   NbB5 fs, fe;
   if (NT_CALL_ACC_EARLY) accurate_fetch(c, tp.s, tp.e, fs, fe);
-#endif
-#ifdef NT_DBG_NO_WRAP
-  const double telo_density = 1.0;
-#else
   const double telo_density = sub_density(c, tp.s, tp.e);
-#endif
   const int num_rows = (tp.e - tp.s + 1) / c.L;
   bool refetch = !NT_CALL_ACC_EARLY;
   if (telo_density < 0.85 && num_rows > 5) {
@@ -1076,15 +1061,9 @@ static __device__ __forceinline__ void call_pass(Lane& c, int& out_s, int& out_e
     tp = find_telo_position(c, min_rows, min_density);
     refetch = true;
   }
-#ifdef NT_DBG_NO_ACC  // timing experiments only (wrong results)
-  (void)refetch;
-  const int s_acc = tp.s;
-  int e_acc = tp.e;
-#else
   if (refetch) accurate_fetch(c, tp.s, tp.e, fs, fe);
   int s_acc, e_acc;
   accurate_both(c, tp.s, tp.e, fs, fe, s_acc, e_acc);
-#endif
   if (s_acc > e_acc) e_acc = s_acc;
   tp = Pos{s_acc, e_acc};
   if (tp.e - tp.s + 1 < 100) {
@@ -1096,11 +1075,7 @@ static __device__ __forceinline__ void call_pass(Lane& c, int& out_s, int& out_e
       tp = find_left_telo(c);
     }
   }
-#ifdef NT_DBG_NO_EXT
-  if (false) {
-#else
   if (!c.prog->legacy_no_ext) {
-#endif
     // both sides' plane windows in one batch, then the step walks in registers
     const int ei = tp.e + 1, si = tp.s - 1;
     Pw<5> wr, wl;
@@ -1118,11 +1093,7 @@ static __device__ __forceinline__ void call_pass(Lane& c, int& out_s, int& out_e
   if (tp.e < tp.s - 1) { err |= NT_FLAG_ERR_WIDTH; out_s = -1; out_e = -1; out_d = 0.0; return; }
   out_s = tp.s;
   out_e = tp.e;
-#ifdef NT_DBG_NO_FINAL
-  out_d = 0.5;
-#else
   out_d = sub_density(c, tp.s, tp.e);
-#endif
 }
 
 // The lane of read r, pass p.
@@ -1178,6 +1149,17 @@ static __device__ __forceinline__ void init_lane(Lane& c, const NtProgram* __res
   c.raw = p == 0 && prog->raw_p1;
 }
 
+// A bundled read the bundle scan did not scan: its bundle's planes span more
+// than 2 GiB (nt_tscan.h kTsSpanError in its first checkpoint, which is
+// otherwise 0).  Reported as a layout-contract error, as an odd blk_off is.
+static __device__ __forceinline__ bool bundle_span_error(const NtProgram* __restrict__ prog, const NtBatch& B,
+                                                         const uint64_t* __restrict__ tmask, uint64_t r) {
+  const int np = prog->n_pass;
+  const int nw = (int)split_window_count((int)B.len[r], prog->L);
+  const uint32_t* ck = reinterpret_cast<const uint32_t*>(tmask + aux_base(B.win_off[r], r, np) + (uint64_t)np * aux_nmw(nw));
+  return ck[0] == 0xFFFFFFFFu;
+}
+
 // The per-pass split (kPass >= 0): a lane per read, this pass's start / end /
 // density; an error is left in end (-2: find_right_telo on a 0-row table, -3:
 // a negative width) and the flags are made by nt_call_combine_kernel after
@@ -1191,11 +1173,15 @@ static __device__ __forceinline__ void run_pass(const NtProgram* __restrict__ pr
   for (uint64_t idx = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; idx < total; idx += stride) {
     const uint64_t r = B.list ? (uint64_t)B.list[idx] : idx;
     if (r == 0xFFFFFFFFull || (B.blk_off[r] & 1u)) continue;
+    if (fix_last && bundle_span_error(prog, B, tmask, r)) {  // left to nt_call_combine_kernel (end -4)
+      O.start[r * 3 + kPass] = -1;
+      O.end[r * 3 + kPass] = -4;
+      O.density[r * 3 + kPass] = 0.0;
+      continue;
+    }
     Lane c;
     init_lane(c, prog, B, O, tmask, r, kPass, tm_lds, pw_lds);
-#ifndef NT_DBG_NO_FIXLAST
     if (fix_last) call_fix_windows(c, thr, thr_size);
-#endif
     int s = -1, e = -1;
     double d = 0.0;
     uint32_t flags = 0u;
@@ -1237,12 +1223,11 @@ static __device__ __forceinline__ void run(const NtProgram* __restrict__ prog, N
     bool align = false;
     if (in) {
       align = (B.blk_off[r] & 1u) != 0;  // the scan skipped this read (layout contract)
+      if (!align && fix_last) align = bundle_span_error(prog, B, tmask, r);
       if (!align && p < np) {
         Lane c;
         init_lane(c, prog, B, O, tmask, r, p, tm_lds, pw_lds);
-#ifndef NT_DBG_NO_FIXLAST  // timing experiments only (wrong results for bundled reads)
         if (fix_last) call_fix_windows(c, thr, thr_size);
-#endif
         call_pass(c, s, e, d, flags);
         if (s == -1) flags |= 1u << (NT_FLAG_NA_SHIFT + p);
         w = e - s + 1;

@@ -126,13 +126,9 @@ NT_HOSTDEV inline int exc_windows(const uint32_t* pos, uint32_t n_exc, int n, in
   return cnt;
 }
 
-// T-layout ("bundles", the bundle scan's copy of the reads, nt_tscan.h):
-//   reads grouped NT_BUNDLE to a bundle, slots sorted by length (non-increasing;
-//   read index ~0u = empty slot).  Bundle b's positions are cut into blocks of
-//   L = subseq_length positions, 64 blocks to a STRIPE; stripe g holds T*64
-//   16-byte words (T = ceil(L/2)): word t*64 + l = {lo, hi of position q,
-//   lo, hi of position q+1} of block l, q = block start + 2t, bit s = slot s.
-//   Bundle b owns stripes [bnd_stripe[b], bnd_stripe[b+1]).
+// Bundles (the bundle scan, nt_tscan.h): reads grouped NT_BUNDLE to a
+//   bundle, slots sorted by length (non-increasing; read index ~0u = empty
+//   slot), scanned together from their own planes: bnd_read[b * NT_BUNDLE + s].
 #define NT_BUNDLE 32
 
 struct NtBatch {
@@ -147,10 +143,8 @@ struct NtBatch {
   // per-read scan (scan_reads): the reads it scans, list[i] (nullptr: all n_reads)
   const uint32_t* list;
   uint64_t n_list;
-  // bundle scan (nt_tscan.h); tplanes == nullptr: no bundles
-  const uint32_t* tplanes;     // 16-byte words, see above
+  // bundle scan (nt_tscan.h); n_bundles == 0: no bundles
   const uint32_t* bnd_read;    // [n_bundles * NT_BUNDLE]
-  const uint64_t* bnd_stripe;  // [n_bundles + 1]
   uint64_t n_bundles;
 };
 

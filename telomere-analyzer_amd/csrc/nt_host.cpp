@@ -36,8 +36,6 @@ int nt_dev_scan_blocks_per_cu(int single, int one, int m6, int lds, size_t lds_b
 hipError_t nt_dev_launch_call(const NtProgram* prog, const NtBatch* B, const NtOut* O,
                               const uint64_t* tmask, const uint32_t* thr, uint32_t thr_size, int fix_last,
                               int long_tvr, int call_grid, hipStream_t stream);
-hipError_t nt_dev_launch_bundle(const NtBatch* B, uint64_t n_stripes, uint32_t* tp, int L, uint32_t div_m,
-                                uint32_t div_s, hipStream_t stream, int cu_count);
 hipError_t nt_dev_launch_synth(const NtSynth* S, uint32_t* planes, uint64_t n_reads,
                                hipStream_t stream);
 hipError_t nt_dev_launch_filter(const NtProgram* prog, const NtBatch* B, uint8_t* keep,
@@ -48,6 +46,7 @@ hipError_t nt_dev_launch_uniform_layout(uint64_t n_reads, uint64_t nblk, uint64_
 }
 
 int nt_jit_blocks_per_cu(void* fn, size_t lds_bytes);
+int nt_jit_block_threads(void* fn);
 bool nt_jit_get(int device, const NtProgram& P, void* fn[4], void** tfn, std::string& err);
 bool nt_tscan_eligible(const NtProgram& P);
 hipError_t nt_tjit_launch(void* fn, int grid, hipStream_t stream, const NtBatch* B, const NtOut* O,
@@ -217,10 +216,10 @@ struct nt_ctx {
   DevBuf planes, blk_off, len, win_off, exc_off, exc_pos, exc_code;
   DevBuf wc, start, end, dens, flags, hits, scratch, tmask, thr, queue;
   DevBuf tmask_alt;  // the odd calls' aux buffer in pipelined mode
-  DevBuf tplanes, bnd_read, bnd_stripe, list;  // upload_reads' bundle layout
-  HostBuf h_planes, h_meta, h_tplanes;  // upload_reads staging
+  DevBuf bnd_read, list;  // upload_reads' bundles
+  HostBuf h_planes, h_meta;  // upload_reads staging
   // host-path phase times (s, cumulative; nt_host_times): layout, pack,
-  // T-layout, uploads, the device work and downloads, the row checks
+  // bundle plan, uploads, the device work and downloads, the row checks
   double host_t[6] = {};
 };
 
@@ -514,14 +513,14 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
   const int m6 = (single && P.pat[0].m == 6) ? 1 : 0;
   // the bundle scan takes the bundled reads when the program has one and no
   // hit counters are asked for (a parity/debug output of the per-read scan)
-  const bool tscan = ctx->tjit_fn && batch->tplanes && batch->n_bundles && !out->hits;
+  const bool tscan = ctx->tjit_fn && batch->bnd_read && batch->n_bundles && !out->hits;
   // the bundle scan stores 8 window counts at once: padded rows (nt_common.h) from a 16-byte aligned base
   if (tscan && (reinterpret_cast<uintptr_t>(out->win_counts) & 15))
     return fail(ctx, NT_E_ARG, "win_counts must be 16-byte aligned for the bundle scan");
   NtBatch B{batch->planes, batch->blk_off, batch->len, batch->win_off,
             batch->exc_off, batch->exc_pos, batch->exc_code, batch->n_reads,
             tscan ? batch->list : nullptr, tscan ? batch->n_list : 0,
-            tscan ? batch->tplanes : nullptr, batch->bnd_read, batch->bnd_stripe, tscan ? batch->n_bundles : 0};
+            batch->bnd_read, tscan ? batch->n_bundles : 0};
   if (tscan && batch->n_list && !batch->list) return fail(ctx, NT_E_ARG, "n_list > 0 without a list");
   const uint64_t n_scan = tscan ? batch->n_list : batch->n_reads;  // reads of the per-read scan
   NtOut O{out->win_counts, out->start, out->end, out->density, out->flags, out->hits};
@@ -645,9 +644,6 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
     (void)hipEventRecord(ev[0], ctx->stream);
   }
   if ((e = hipMemsetAsync(queue, 0, nqueue * NT_QUEUE_WORDS * 8, ctx->stream)) != hipSuccess) return hip_fail(ctx, e, "hipMemsetAsync(queue)");
-  // fault isolation (debugging): NT_DBG_SKIP_SCAN / NT_DBG_SKIP_CALL launch only the other kernel
-  const bool dbg_skip_scan = std::getenv("NT_DBG_SKIP_SCAN") != nullptr;
-  const bool dbg_skip_call = std::getenv("NT_DBG_SKIP_CALL") != nullptr;
   if (tscan) {
     // the bundle scan first: one wave per bundle, exactly the resident blocks
     // (one per CU while a calling kernel runs beside it: room for its waves)
@@ -677,11 +673,11 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
     for (uint64_t k = 0; k < tsub; ++k) {
       const uint64_t b0 = bb[k], b1 = bb[k + 1];
       if (b1 == b0) continue;
-      NtBatch Bt = B;  // bundles [b0, b1): bnd_stripe stays absolute
+      NtBatch Bt = B;  // bundles [b0, b1)
       Bt.bnd_read += NT_BUNDLE * b0;
-      Bt.bnd_stripe += b0;
       Bt.n_bundles = b1 - b0;
-      const uint64_t tgrid = std::max<uint64_t>(1, std::min<uint64_t>((Bt.n_bundles + 3) / 4, (uint64_t)ctx->cu_count * tbpc));
+      const uint64_t wpb = (uint64_t)std::max(1, nt_jit_block_threads(ctx->tjit_fn) / 64);  // a wave per bundle
+      const uint64_t tgrid = std::max<uint64_t>(1, std::min<uint64_t>((Bt.n_bundles + wpb - 1) / wpb, (uint64_t)ctx->cu_count * tbpc));
       const int pe = ev ? ctx->ev_nt[ctx->n_ev - 1] : 0;  // event pair of this launch
       if (ev) (void)hipEventRecord(ev[3 + 2 * pe], ctx->stream);
       e = nt_tjit_launch(ctx->tjit_fn, (int)tgrid, ctx->stream, &Bt, &O, tmask,
@@ -702,8 +698,7 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
           return hip_fail(ctx, e, "stream dependency");
         cs = ctx->call_stream;
       }
-      if (!dbg_skip_call &&
-          (e = launch_call(ctx, cfn, &Bc, &O, tmask, 1, cs)) != hipSuccess)
+      if ((e = launch_call(ctx, cfn, &Bc, &O, tmask, 1, cs)) != hipSuccess)
         return hip_fail(ctx, e, "launch nt_call_kernel");
     }
   }
@@ -743,37 +738,19 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
     const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((ns + 3) / 4, (uint64_t)ctx->cu_count * bpc));
     const QueuePlan qp = queue_plan(std::max<uint64_t>(ns, 1), batch->n_windows * (uint64_t)L / batch->n_reads, grid * 4);
     const uint32_t claim = qp.claim, nstatic = qp.nstatic;
-    // NT_DBG_CHECK_PLANES=<planes in 16-byte segments> (debugging, with the
-    // scan JIT-built with -DNT_DBG_CHECK=1): address checks, report on stderr
-    uint64_t* dbg = nullptr;
-    if (const char* v = std::getenv("NT_DBG_CHECK_PLANES")) {
-      if (hipMalloc(&dbg, 9 * 8) == hipSuccess) {
-        const uint64_t h[9] = {std::strtoull(v, nullptr, 10), batch->n_windows * (uint64_t)np, tmw, 0, 0, 0, 0, 0, 0};
-        (void)hipMemcpy(dbg, h, sizeof h, hipMemcpyHostToDevice);
-      }
-    }
     // the per-read scan beside the bundle scan (its list reads): one more
     // timed launch of the scan kernels (nt_kernel_times)
     const int pe = (ev && tscan && n_scan > 0) ? ctx->ev_nt[ctx->n_ev - 1] : -1;
     if (pe >= 0) (void)hipEventRecord(ev[3 + 2 * pe], ctx->stream);
-    if (dbg_skip_scan || n_scan == 0 || !lds_fits)
+    if (n_scan == 0 || !lds_fits)
       e = hipSuccess;
     else if (ctx->jit)
       e = nt_jit_launch(jit_lds, (int)grid, lds_bytes, ctx->stream, ctx->prog_dev,
                         (const uint32_t*)ctx->thr.p, &Bk, &Ok, tmk, q, 0u, (uint32_t)len_cap, claim, nstatic, ww_lds,
-                        (uint32_t*)dbg);
+                        nullptr);
     else
       e = nt_dev_launch(ctx->prog_dev, (const uint32_t*)ctx->thr.p, &Bk, &Ok, tmk, q, 0u, (uint32_t)len_cap, claim, nstatic,
                         single, one, m6, 1, ww_lds, nullptr, (int)grid, ctx->stream);
-    if (dbg && e == hipSuccess) {
-      uint64_t h[9];
-      (void)hipStreamSynchronize(ctx->stream);
-      (void)hipMemcpy(h, dbg, sizeof h, hipMemcpyDeviceToHost);
-      std::fprintf(stderr, "NT_DBG_CHECK: %llu violations; first kind %llu index %llu read %llu limit %llu\n",
-                   (unsigned long long)h[4], (unsigned long long)h[5], (unsigned long long)h[6],
-                   (unsigned long long)h[7], (unsigned long long)h[8]);
-      (void)hipFree(dbg);
-    }
     if (e != hipSuccess) return hip_fail(ctx, e, "launch nt_scan_kernel<lds>");
     if (two && n_scan > 0) {
       if (ctx->jit)
@@ -791,11 +768,10 @@ int nt_scan_call(nt_ctx* ctx, const nt_batch* batch, const nt_out* out, uint64_t
     }
     if (tscan) {
       // the reads of the per-read scan (the bundled ones are called above)
-      if (n_scan > 0 && !dbg_skip_call) e = launch_call(ctx, cfn, &Bk, &Ok, tmk, 0, ctx->stream);
+      if (n_scan > 0) e = launch_call(ctx, cfn, &Bk, &Ok, tmk, 0, ctx->stream);
     } else if (nsub == 1) {
       if (ev) (void)hipEventRecord(ev[1], ctx->stream);
-      e = dbg_skip_call ? hipSuccess
-                        : launch_call(ctx, cfn, &Bk, &Ok, tmk, 0, ctx->stream);
+      e = launch_call(ctx, cfn, &Bk, &Ok, tmk, 0, ctx->stream);
     } else {
       // calling kernel of this sub-batch on the call stream, after its scan
       if ((e = hipEventRecord(ctx->ev_scan, ctx->stream)) != hipSuccess ||
@@ -835,45 +811,51 @@ static void exc_marks(const NtProgram& P, const uint32_t* len, const uint32_t* e
   });
 }
 
-// Bundles of the bundle scan: the eligible reads (no non-ACGT letter, the
-// program covered by nt_tscan.h) sorted by length, longest first (ties in
-// input order), 32 to a bundle; a bundle's T-layout is ceil(ceil(n_max / L) /
-// 64) stripes of ceil(L/2) * 64 16-byte words, and must stay below 2^31 bytes
-// (the scan's buffer offsets): reads longer than that stay out.
-int nt_bundle_plan(nt_ctx* ctx, const uint32_t* len, const uint8_t* has_exc, uint64_t n_reads,
-                   uint32_t* bnd_read, uint64_t* bnd_stripe, uint64_t* n_bundles, uint32_t* list,
-                   uint64_t* n_list, uint64_t* tplane_bytes) {
-  if (!ctx || !n_bundles || !n_list || !tplane_bytes || (n_reads && (!len || !bnd_read || !bnd_stripe || !list)))
-    return NT_E_ARG;
+// Bundles of the bundle scan: the eligible reads (no non-ACGT letter beyond
+// NT_EXC_WINDOWS windows, the program covered by nt_tscan.h) sorted by length,
+// longest first (ties in input order), 32 to a bundle.  The scan addresses a
+// bundle's planes from its lowest read's with 32-bit offsets: with blk_off
+// given, a bundle whose reads' planes span more than kBundleSpan bytes goes to
+// the per-read scan whole (the host path's batches are far smaller).
+static constexpr uint64_t kBundleSpan = 0x7FFFFFF0ull;  // nt_tscan.h kTsMaxSpan
+
+int nt_bundle_plan(nt_ctx* ctx, const uint32_t* len, const uint64_t* blk_off, const uint8_t* has_exc,
+                   uint64_t n_reads, uint32_t* bnd_read, uint64_t* n_bundles, uint32_t* list, uint64_t* n_list) {
+  if (!ctx || !n_bundles || !n_list || (n_reads && (!len || !bnd_read || !list))) return NT_E_ARG;
   if (!ctx->compiled) return fail(ctx, NT_E_STATE, "nt_compile() not called");
-  const uint64_t L = (uint64_t)ctx->prog.L, T = (L + 1) / 2;
-  const uint64_t stripe_bytes = T * 64 * 16;
-  const uint64_t max_stripes = ((1ull << 31) - 1) / stripe_bytes;
   const bool ok = nt_tscan_eligible(ctx->prog);
   std::vector<uint32_t> in;
   in.reserve(n_reads);
-  uint64_t nl = 0;
+  std::vector<uint8_t> out(n_reads, 0);  // reads left to the per-read scan
   for (uint64_t r = 0; r < n_reads; ++r) {
-    const uint64_t st = ((len[r] + L - 1) / L + 63) / 64;
-    if (ok && len[r] > 0 && !(has_exc && has_exc[r]) && st <= max_stripes) in.push_back((uint32_t)r);
-    else list[nl++] = (uint32_t)r;
+    if (ok && len[r] > 0 && !(has_exc && has_exc[r])) in.push_back((uint32_t)r);
+    else out[r] = 1;
   }
   std::stable_sort(in.begin(), in.end(), [&](uint32_t a, uint32_t b) { return len[a] > len[b]; });
-  const uint64_t nb = (in.size() + NT_BUNDLE - 1) / NT_BUNDLE;
-  uint64_t g = 0;
-  for (uint64_t b = 0; b < nb; ++b) {
-    bnd_stripe[b] = g;
-    for (uint64_t s = 0; s < NT_BUNDLE; ++s) {
-      const uint64_t i = b * NT_BUNDLE + s;
-      bnd_read[i] = i < in.size() ? in[i] : 0xFFFFFFFFu;
+  const uint64_t ng = (in.size() + NT_BUNDLE - 1) / NT_BUNDLE;
+  uint64_t nb = 0;
+  for (uint64_t g = 0; g < ng; ++g) {
+    const uint64_t i0 = g * NT_BUNDLE, i1 = std::min<uint64_t>(in.size(), i0 + NT_BUNDLE);
+    if (blk_off) {  // the bundle's planes within kBundleSpan bytes
+      uint64_t lo = ~0ull, hi = 0;
+      for (uint64_t i = i0; i < i1; ++i) {
+        lo = std::min(lo, blk_off[in[i]]);
+        hi = std::max(hi, blk_off[in[i]] + read_blocks(len[in[i]]));
+      }
+      if ((hi - lo) * 8 > kBundleSpan) {
+        for (uint64_t i = i0; i < i1; ++i) out[in[i]] = 1;
+        continue;
+      }
     }
-    const uint64_t nmax = len[in[b * NT_BUNDLE]];
-    g += ((nmax + L - 1) / L + 63) / 64;
+    for (uint64_t s = 0; s < NT_BUNDLE; ++s)
+      bnd_read[nb * NT_BUNDLE + s] = i0 + s < i1 ? in[i0 + s] : 0xFFFFFFFFu;
+    ++nb;
   }
-  bnd_stripe[nb] = g;
+  uint64_t nl = 0;
+  for (uint64_t r = 0; r < n_reads; ++r)
+    if (out[r]) list[nl++] = (uint32_t)r;
   *n_bundles = nb;
   *n_list = nl;
-  *tplane_bytes = g * stripe_bytes;
   return NT_OK;
 }
 
@@ -887,22 +869,6 @@ int nt_exc_marks(nt_ctx* ctx, const uint32_t* len, const uint32_t* exc_off, cons
     exc_marks(ctx->prog, len, exc_off, exc_pos, n_reads, has_exc);
   }
   return NT_OK;
-}
-
-int nt_bundle_layout(nt_ctx* ctx, const nt_batch* batch, uint32_t* tplanes, uint64_t tplane_bytes) {
-  if (!ctx || !batch || (batch->n_bundles && !tplanes)) return NT_E_ARG;
-  if (!ctx->compiled) return fail(ctx, NT_E_STATE, "nt_compile() not called");
-  if (batch->n_bundles == 0) return NT_OK;
-  (void)hipSetDevice(ctx->device);
-  if (ctx->prog.L > 170) return fail(ctx, NT_E_ARG, "bundle layout: subseq_length > 170 has no bundle scan");
-  // the kernel writes every word of every stripe (zeros past the reads)
-  const uint64_t stripe_bytes = (uint64_t)((ctx->prog.L + 1) / 2) * 64 * 16;
-  if (tplane_bytes % stripe_bytes) return fail(ctx, NT_E_ARG, "tplane_bytes is not a whole number of stripes");
-  NtBatch B{batch->planes, batch->blk_off, batch->len, batch->win_off, nullptr, nullptr, nullptr, batch->n_reads,
-            nullptr, 0, tplanes, batch->bnd_read, batch->bnd_stripe, batch->n_bundles};
-  hipError_t e = nt_dev_launch_bundle(&B, tplane_bytes / stripe_bytes, tplanes, ctx->prog.L, ctx->prog.div32_m,
-                                      ctx->prog.div32_s, ctx->stream, ctx->cu_count);
-  return e == hipSuccess ? NT_OK : hip_fail(ctx, e, "launch nt_bundle_kernel");
 }
 
 int nt_call_jit_state(const nt_ctx* ctx) { return ctx ? ctx->cjit_last : 0; }
@@ -998,11 +964,6 @@ int64_t nt_kernel_times(nt_ctx* ctx, double* scan_ms, double* call_ms) {
 
 // Pack a host chunk (2-bit planes + exception lists, --rc fused) and upload
 // it to the context's device buffers; B describes the device batch.
-static bool host_tlayout() {
-  const char* v = std::getenv("NT_HOST_TLAYOUT");
-  return v && v[0] == '1';
-}
-
 static int upload_reads(nt_ctx* ctx, const char* const* seqs, const uint64_t* lens, uint64_t n_reads,
                         nt_batch* B, uint64_t* max_len, bool want_bundles) {
   const int L = ctx->prog.L;
@@ -1091,55 +1052,26 @@ static int upload_reads(nt_ctx* ctx, const char* const* seqs, const uint64_t* le
     // the exception lists are pageable vectors: finish their copies before they go
     if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess) return hip_fail(ctx, e, "hipStreamSynchronize");
   }
-  // the bundle layout of the batch (bundle scan): built on the host from the
-  // packed planes (ingest) and uploaded beside them
-  uint64_t nb = 0, nl = 0, tpb = 0;
+  // the batch's bundles (bundle scan): the plan, uploaded beside the planes
+  // (the scan reads the reads from the planes themselves)
+  uint64_t nb = 0, nl = 0;
   std::vector<uint32_t> h_bread, h_list;
-  std::vector<uint64_t> h_bstripe;
   if (ctx->tjit_fn && want_bundles) {
     // reads with non-ACGT letters join the bundles unless their exceptions
     // reach more than NT_EXC_WINDOWS windows (nt_common.h)
     std::vector<uint8_t> hx(n_reads, 0);
     if (te) exc_marks(ctx->prog, h_len, h_eoff.data(), h_epos.data(), n_reads, hx.data());
     h_bread.resize((n_reads + NT_BUNDLE - 1) / NT_BUNDLE * NT_BUNDLE + NT_BUNDLE);
-    h_bstripe.resize((n_reads + NT_BUNDLE - 1) / NT_BUNDLE + 2);
     h_list.resize(n_reads + 1);
-    int rc = nt_bundle_plan(ctx, h_len, hx.data(), n_reads, h_bread.data(), h_bstripe.data(), &nb, h_list.data(),
-                            &nl, &tpb);
+    int rc = nt_bundle_plan(ctx, h_len, h_blk, hx.data(), n_reads, h_bread.data(), &nb, h_list.data(), &nl);
     if (rc) return rc;
     h_bread.resize(nb * NT_BUNDLE);
-    h_bstripe.resize(nb + 1);
     h_list.resize(nl);
+    lap(2);
   }
   if (nb) {
-    lap(3);
     NT_UP(bnd_read, h_bread);
-    NT_UP(bnd_stripe, h_bstripe);
     if (nl) { NT_UP(list, h_list); }
-    if (host_tlayout()) {
-      // NT_HOST_TLAYOUT=1: the T-layout built on the host and uploaded beside
-      // the planes (round 3; twice the upload bytes, 98 ms of host time per 8
-      // Gbases on a 16-core share -- the end-to-end bound)
-      if ((e = ctx->h_tplanes.ensure(tpb)) != hipSuccess) return hip_fail(ctx, e, "hipHostMalloc(tplanes)");
-      int rc = nt_bundle_layout_host(hp, h_blk, h_len, h_bread.data(), h_bstripe.data(), nb, L,
-                                     (uint32_t*)ctx->h_tplanes.p, tpb);
-      if (rc) return fail(ctx, rc, "nt_bundle_layout_host");
-      lap(2);
-      NT_UP_PTR(tplanes, ctx->h_tplanes.p, tpb);
-    } else {
-      // the device transposer from the uploaded planes (about 1 ms per 8 Gbases
-      // of GPU time; nt_bundle_layout), on the context stream before the scan
-      if ((e = ctx->tplanes.ensure(tpb)) != hipSuccess) return hip_fail(ctx, e, "hipMalloc(tplanes)");
-      const uint64_t stripe_bytes = (uint64_t)((L + 1) / 2) * 64 * 16;
-      NtBatch Bt{(const uint32_t*)ctx->planes.p, (const uint64_t*)ctx->blk_off.p, (const uint32_t*)ctx->len.p,
-                 (const uint64_t*)ctx->win_off.p, nullptr, nullptr, nullptr, n_reads, nullptr, 0,
-                 (const uint32_t*)ctx->tplanes.p, (const uint32_t*)ctx->bnd_read.p,
-                 (const uint64_t*)ctx->bnd_stripe.p, nb};
-      e = nt_dev_launch_bundle(&Bt, tpb / stripe_bytes, (uint32_t*)ctx->tplanes.p, L, ctx->prog.div32_m,
-                               ctx->prog.div32_s, ctx->stream, ctx->cu_count);
-      if (e != hipSuccess) return hip_fail(ctx, e, "launch nt_bundle_kernel");
-      lap(2);
-    }
     // the vectors are pageable: finish their copies before they go
     if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess) return hip_fail(ctx, e, "hipStreamSynchronize");
   }
@@ -1150,9 +1082,7 @@ static int upload_reads(nt_ctx* ctx, const char* const* seqs, const uint64_t* le
                 te ? (const uint32_t*)ctx->exc_off.p : nullptr,
                 te ? (const uint32_t*)ctx->exc_pos.p : nullptr,
                 te ? (const uint8_t*)ctx->exc_code.p : nullptr, n_reads, tw,
-                nb ? (const uint32_t*)ctx->tplanes.p : nullptr,
-                nb ? (const uint32_t*)ctx->bnd_read.p : nullptr,
-                nb ? (const uint64_t*)ctx->bnd_stripe.p : nullptr, nb,
+                nb ? (const uint32_t*)ctx->bnd_read.p : nullptr, nb,
                 nl && nb ? (const uint32_t*)ctx->list.p : nullptr, nb ? nl : 0};
   lap(3);
   *max_len = ml;
@@ -1176,7 +1106,7 @@ int nt_filter_call(nt_ctx* ctx, const nt_batch* batch, uint8_t* keep) {
   (void)hipSetDevice(ctx->device);
   NtBatch B{batch->planes, batch->blk_off, batch->len, batch->win_off,
             batch->exc_off, batch->exc_pos, batch->exc_code, batch->n_reads,
-            nullptr, 0, nullptr, nullptr, nullptr, 0};
+            nullptr, 0, nullptr, 0};
   const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((batch->n_reads + 255) / 256, (uint64_t)ctx->cu_count * 16));
   const hipError_t e = nt_dev_launch_filter(ctx->prog_dev, &B, keep, filter_threshold(ctx->prog.min_density),
                                             ctx->prog.right_edge, (int)grid, ctx->stream);

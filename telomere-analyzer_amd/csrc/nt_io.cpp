@@ -53,7 +53,7 @@ static bool gz_failed(gzFile g) {
 // calls wait on -- a 16-part fastq.gz run (16 GB inflated) spent 0.7 s of
 // reader time unmapping and its context teardown waited 0.3-0.7 s behind it
 // (2.6 s read wait and 0.3-0.6 s teardown with the unmaps, 1.9 s and 2 ms
-// without).  The process keeps up to NT_READER_POOL_GB (default 32) of them for
+// without).  The process keeps up to NT_READER_POOL_GB (default 32 / local ranks) of them for
 // the next parts and the next reader; a buffer grows with mremap (the page
 // tables move, nothing is copied).
 struct MPool {
@@ -61,8 +61,12 @@ struct MPool {
   std::vector<std::pair<char*, size_t>> free;
   size_t bytes = 0, limit = 0;
   MPool() {
+    // default 32 GB a node: one process per GPU splits it over the local ranks
+    double gb = 32.0;
+    if (const char* w = std::getenv("LOCAL_WORLD_SIZE"))
+      if (std::atoi(w) > 1) gb /= std::atoi(w);
     const char* v = std::getenv("NT_READER_POOL_GB");
-    limit = (size_t)(v ? std::atof(v) : 32.0) << 30;
+    limit = (size_t)((v ? std::atof(v) : gb) * (double)(1ull << 30));
   }
   char* take(size_t want, size_t& cap) {
     std::lock_guard<std::mutex> lk(mu);
@@ -300,6 +304,11 @@ struct nt_reader {
   size_t fq_i = 0;
   uint64_t fq_scan = 0;
   int fq_mode = 0;
+  // the next slice's byte cap: 1 GB when reading on, kSliceSeek after a seek
+  // that left the index (a rank's block may be far smaller than a slice:
+  // indexing 1 GB of other ranks' records per seek undid the sharding), then
+  // doubling
+  uint64_t fq_slice = 0;
   // the current file's bytes: a mapping of the whole plain file, a whole gzip
   // part inflated ahead (Prefetcher), or windows of a gzip stream (serial inflate)
   gzFile gz = nullptr;
@@ -346,6 +355,11 @@ constexpr size_t kWindow = 64u << 20;  // gzip stream window / index slice (grow
 unsigned host_threads() {
   unsigned nt = std::thread::hardware_concurrency();
   nt = std::max(1u, std::min(nt == 0 ? 1u : nt, 16u));
+  // one process per GPU: the ranks of a node share its cores
+  if (const char* w = std::getenv("LOCAL_WORLD_SIZE")) {
+    const int k = atoi(w);
+    if (k > 1) nt = std::max(1u, nt / (unsigned)k);
+  }
   if (const char* v = std::getenv("NT_READER_PARSE_THREADS")) nt = (unsigned)std::max(1, atoi(v));
   return nt;
 }
@@ -482,10 +496,13 @@ void start(nt_reader* r) {
 }
 
 // the FASTQ fast path's state for a new position of the open file
-void fq_reset(nt_reader* r, uint64_t pos, bool mapped) {
+constexpr uint64_t kSliceMax = 1ull << 30, kSliceSeek = 16ull << 20;
+
+void fq_reset(nt_reader* r, uint64_t pos, bool mapped, uint64_t slice = kSliceMax) {
   r->fq.clear();
   r->fq_i = 0;
   r->fq_scan = pos;
+  r->fq_slice = slice;
   const char* v = std::getenv("NT_READER_FQ_FAST");  // 0: the line parser for FASTQ too
   const bool off = v && v[0] == '0';
   r->fq_mode = (r->format == 1 && mapped && !off) ? 1 : 0;
@@ -770,8 +787,9 @@ int fq_index_slice(nt_reader* r) {
   const size_t n = r->end;
   const size_t a = skip_blank(d, n, r->fq_scan);
   if (a >= n) return 0;
-  constexpr size_t kSlice = 1ull << 30;
-  const size_t b = std::min(n, a + kSlice);
+  const size_t slice = r->fq_slice ? r->fq_slice : kSliceMax;
+  r->fq_slice = std::min<uint64_t>(kSliceMax, 2 * slice);
+  const size_t b = std::min(n, a + slice);
   const unsigned nt = (b - a) >= (8u << 20) ? host_threads() : 1u;
   struct Part {
     std::vector<nt_reader::FqRec> recs;
@@ -1234,10 +1252,25 @@ int nt_reader_seek(nt_reader* r, int mode, uint64_t a, uint64_t b) {
   }
   if (mode == 0) {
     if (off > r->end) return NT_E_ARG;
+    if (r->fq_mode == 1 && r->fq_i < r->fq.size() && off >= r->fq[r->fq_i].hdr && off < r->fq_scan) {
+      // a forward seek inside the indexed slice: keep the index, move to the
+      // record that starts there (the records are in file order)
+      size_t lo = r->fq_i, hi = r->fq.size();
+      while (lo < hi) {
+        const size_t mid = (lo + hi) / 2;
+        if (r->fq[mid].hdr < off) lo = mid + 1;
+        else hi = mid;
+      }
+      if (lo < r->fq.size() && r->fq[lo].hdr == off) {
+        r->fq_i = lo;
+        r->pos = off;
+        return NT_OK;
+      }
+    }
     r->pos = r->scan = off;
     r->nl.clear();
     r->nl_i = 0;
-    fq_reset(r, off, r->win && r->win->map != nullptr);
+    fq_reset(r, off, r->win && r->win->map != nullptr, kSliceSeek);
     return NT_OK;
   }
   std::vector<uint64_t> lens;

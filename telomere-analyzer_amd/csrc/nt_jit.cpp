@@ -57,6 +57,18 @@ struct CallEntry {
 };
 std::map<std::string, CallEntry> g_ccache;
 
+// NT_JIT_OPTS (extra hiprtc options, e.g. -D switches of timing experiments)
+// is honoured only by a tuning build of the library (make EXTRA=-DNT_TUNING_BUILD):
+// the product library compiles every kernel as shipped, whatever the
+// environment says.
+const char* jit_opts() {
+#ifdef NT_TUNING_BUILD
+  return std::getenv("NT_JIT_OPTS");
+#else
+  return nullptr;
+#endif
+}
+
 // eq: the code-equality truth tables (fixed=TRUE, the edge steps) instead of the scan's
 std::string pat_type(const NtPat& P, bool eq = false) {
   std::string s = "nt::CtPat<" + std::to_string(P.m);
@@ -116,30 +128,19 @@ std::string jit_source(const NtProgram& P) {
   if (nt_tscan_eligible(P)) {
     s += "using TPats = nt::CtList<" + pats + ">;\nusing TTvrs = nt::CtList<" + tvrs + ">;\n";
     s += "using TJit = nt::TProg<TPats, TTvrs, " + std::to_string(P.L) + ">;\n";
+    // one wave per bundle; as many waves a workgroup (at most 4, one per
+    // SIMD) as their LDS (slots, output rows, the half-stripe buffer) fits in
+    // the CU's 160 KB; ~420 registers a lane: one wave per SIMD
     s += R"(
-#ifndef NT_TSCAN_WAVES_EU
-#define NT_TSCAN_WAVES_EU 2
-#endif
-#if NT_TS_WS  // 4 walker waves + 1 writer wave (nt_tscan.h)
-extern "C" __global__ void __launch_bounds__(320) __attribute__((amdgpu_waves_per_eu(NT_TSCAN_WAVES_EU)))
+constexpr int kTsW = nt::ts_lds_words<TJit::kNP, TJit::kL>();
+constexpr int kTsNW = 40960 / kTsW < 4 ? 40960 / kTsW : 4;
+static_assert(kTsNW >= 1, "bundle-scan LDS");
+extern "C" __global__ void __launch_bounds__(kTsNW * 64) __attribute__((amdgpu_waves_per_eu(1)))
 nt_tscan_jit(NtBatch B, NtOut O, uint64_t* __restrict__ tmask, unsigned long long* __restrict__ queue,
              uint32_t thr_full) {
-  __shared__ uint32_t tsl[nt::ts_ws_lds_words<TJit::kNP>()];
-  nt::tscan_bundles_ws<TJit, TPats, TTvrs>(B, O, tmask, queue, thr_full, tsl);
+  __shared__ uint32_t tsl[kTsNW * kTsW];
+  nt::tscan_bundles<TJit, TPats, TTvrs>(B, O, tmask, queue, thr_full, tsl + (threadIdx.x >> 6) * kTsW);
 }
-#else
-#ifndef NT_TS_DBG_THREADS  // timing experiments: a block of more waves, the extra ones idle
-#define NT_TS_DBG_THREADS 256
-#endif
-extern "C" __global__ void __launch_bounds__(NT_TS_DBG_THREADS) __attribute__((amdgpu_waves_per_eu(NT_TSCAN_WAVES_EU)))
-nt_tscan_jit(NtBatch B, NtOut O, uint64_t* __restrict__ tmask, unsigned long long* __restrict__ queue,
-             uint32_t thr_full) {
-  constexpr int kW = nt::ts_lds_words<TJit::kNP>();
-  __shared__ uint32_t tsl[4 * kW];
-  if (threadIdx.x >= 256) return;
-  nt::tscan_bundles<TJit, TPats, TTvrs>(B, O, tmask, queue, thr_full, tsl + (threadIdx.x >> 6) * kW);
-}
-#endif
 )";
   }
   s += R"(
@@ -297,8 +298,8 @@ bool get_code(const std::string& arch, const std::string& src, std::vector<char>
               bool fresh = false, std::string* cpath_out = nullptr) {
   const char* hdrs[] = {kJitCommon, kJitDevice, kJitScan, kJitTScan, kJitCall};
   const char* names[] = {"nt_common.h", "nt_device.h", "nt_scan.h", "nt_tscan.h", "nt_call.h"};
-  std::vector<std::string> extra;  // NT_JIT_OPTS: extra compiler options (tuning experiments)
-  if (const char* v = std::getenv("NT_JIT_OPTS")) {
+  std::vector<std::string> extra;  // NT_JIT_OPTS: extra compiler options (tuning builds only)
+  if (const char* v = jit_opts()) {
     std::string t;
     for (const char* p = v;; ++p) {
       if (*p == ' ' || *p == 0) {
@@ -421,7 +422,7 @@ bool nt_jit_get(int device, const NtProgram& P, void* fn[4], void** tfn, std::st
     return false;
   }
   const std::string src = jit_source(P);
-  const char* xo = std::getenv("NT_JIT_OPTS");
+  const char* xo = jit_opts();
   const std::string key = std::to_string(device) + "\n" + (xo ? xo : "") + "\n" + src;
   std::lock_guard<std::mutex> lk(g_mu);
   auto it = g_cache.find(key);
@@ -447,6 +448,8 @@ static int jit_threads(void* fn) {
     return 256;
   return v;
 }
+
+int nt_jit_block_threads(void* fn) { return jit_threads(fn); }
 
 hipError_t nt_tjit_launch(void* fn, int grid, hipStream_t stream, const NtBatch* B, const NtOut* O,
                           uint64_t* tmask, unsigned long long* queue, uint32_t thr_full) {
@@ -486,7 +489,7 @@ void* nt_cjit_get(int device, const NtProgram& P, std::string& err) {
     return nullptr;
   }
   const std::string src = call_source(P);
-  const char* xo = std::getenv("NT_JIT_OPTS");
+  const char* xo = jit_opts();
   const std::string key = std::to_string(device) + "\n" + (xo ? xo : "") + "\n" + src;
   {
     std::lock_guard<std::mutex> lk(g_mu);

@@ -65,7 +65,9 @@ __global__ void __launch_bounds__(256) nt_call_combine_kernel(NtBatch B, NtOut O
   for (uint64_t idx = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; idx < total; idx += stride) {
     const uint64_t r = B.list ? (uint64_t)B.list[idx] : idx;
     if (r == 0xFFFFFFFFull) continue;
-    if (B.blk_off[r] & 1u) {  // the scan skipped this read (layout contract)
+    bool span = false;  // a pass left -4: the bundle scan skipped the read (nt_call.h bundle_span_error)
+    for (int p = 0; p < np; ++p) span = span || O.end[r * 3 + p] == -4;
+    if ((B.blk_off[r] & 1u) || span) {  // the scan skipped this read (layout contract)
       for (int p = 0; p < 3; ++p) {
         O.start[r * 3 + p] = -1;
         O.end[r * 3 + p] = -1;
@@ -132,109 +134,6 @@ nt_layout_kernel(uint64_t n_reads, uint64_t nblk, uint64_t read_len, uint64_t nw
     blk_off[r] = r * nblk;
     len[r] = (uint32_t)read_len;
     win_off[r] = r * nw;
-  }
-}
-
-// ================================================================ bundles
-//
-// The T-layout of the bundle scan (nt_common.h) from the per-read planes: one
-// workgroup per bundle, its half stripes in turn (32 blocks = 32 L positions =
-// L plane words of each of the bundle's 32 reads).  The half stripe's words
-// of the 32 reads come into LDS by coalesced loads; then per step every lane
-// takes one {lo, hi} word of its read (lanes 0-31: word w of slot s, lanes
-// 32-63: word w + 1; the 4 waves every 4th step), masked past the read end,
-// and two 32 x 32 bit transposes inside each half wave turn
-// them into the 32-slot columns of 32 positions; these go to an LDS copy of
-// the half stripe's T-layout rows (row t: 32 words of 16 bytes, 8-byte halves
-// by position parity), written out as whole 512-byte row runs.  Every word of
-// every stripe is written (zeros past the reads): no memset first.
-constexpr int kBndRowWords = 132;  // LDS row stride (words): 128 + 4 spreads the banks
-
-__global__ void __launch_bounds__(256)
-nt_bundle_kernel(NtBatch B, uint32_t* __restrict__ tp, int L, uint32_t div_m, uint32_t div_s) {
-  extern __shared__ uint32_t lds[];
-  const int T = (L + 1) / 2;
-  const int R = 2 * L + 2;                // words per read in the input copy (bank spread)
-  uint32_t* in = lds;                     // [32][R]: the half stripe's plane words of each read
-  uint32_t* rows = lds + NT_BUNDLE * R;   // [T][kBndRowWords]: its T-layout rows
-  uint32_t* meta = rows + T * kBndRowWords;  // [32][4]: len, block offset lo / hi of each slot
-  const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x >> 6;
-  const int s = lane & 31, hh = lane >> 5;
-  const BitTr bt(lane);
-  for (uint64_t b = blockIdx.x; b < B.n_bundles; b += gridDim.x) {
-    const uint32_t r = B.bnd_read[b * NT_BUNDLE + s];
-    const int64_t len = r != 0xFFFFFFFFu ? (int64_t)B.len[r] : 0;
-    const uint64_t g0 = uniform_u64(B.bnd_stripe[b]), g1 = uniform_u64(B.bnd_stripe[b + 1]);
-    if (threadIdx.x < NT_BUNDLE) {
-      const uint64_t bo = r != 0xFFFFFFFFu ? B.blk_off[r] : 0ull;
-      *reinterpret_cast<uint4*>(meta + 4 * s) = make_uint4((uint32_t)len, (uint32_t)bo, (uint32_t)(bo >> 32), 0u);
-    }
-    __syncthreads();
-    // 1. a half stripe's words [w0, w0 + L) of the 32 reads, coalesced (8
-    // bytes a thread), into registers -- the next half stripe's while this
-    // one is transposed -- then into LDS
-    constexpr int kMaxE = (NT_BUNDLE * 170 + 255) / 256;  // L <= 170 (nt_tscan_eligible)
-    uint2 v[kMaxE];
-    auto fetch = [&](uint64_t uu) {
-      const uint64_t wu = (uint64_t)L * uu;
-#pragma unroll
-      for (int k = 0; k < kMaxE; ++k) {
-        const uint32_t e = threadIdx.x + 256u * k;
-        v[k] = make_uint2(0u, 0u);
-        if (e < (uint32_t)(NT_BUNDLE * L)) {
-          const uint32_t rs = __umulhi(e, div_m) >> div_s, wd = e - rs * (uint32_t)L;
-          const uint4 m = *reinterpret_cast<const uint4*>(meta + 4 * rs);
-          if (32 * (int64_t)(wu + wd) < (int64_t)m.x)  // (empty slots have len 0)
-            v[k] = reinterpret_cast<const uint2*>(B.planes)[(((uint64_t)m.z << 32) | m.y) + wu + wd];
-        }
-      }
-    };
-    const uint64_t nu = 2 * (g1 - g0);  // half stripes of the bundle
-    fetch(0);
-    for (uint64_t u = 0; u < nu; ++u) {
-      const uint64_t G = g0 + (u >> 1);
-      const int h = (int)(u & 1);
-      const uint64_t w0 = (uint64_t)L * u;  // first plane word of the half stripe
-#pragma unroll
-      for (int k = 0; k < kMaxE; ++k) {
-        const uint32_t e = threadIdx.x + 256u * k;
-        if (e < (uint32_t)(NT_BUNDLE * L)) {
-          const uint32_t rs = __umulhi(e, div_m) >> div_s, wd = e - rs * (uint32_t)L;
-          *reinterpret_cast<uint2*>(in + rs * R + 2 * wd) = v[k];
-        }
-      }
-      if ((L & 1) && threadIdx.x < 32)  // odd L: the last row's second half holds no position
-        *reinterpret_cast<uint2*>(rows + (T - 1) * kBndRowWords + 4 * s + 2) = make_uint2(0u, 0u);
-      __syncthreads();
-      if (u + 1 < nu) fetch(u + 1);  // in flight during the transposes and the stores
-      // 2. wave wv takes the steps wv, wv + 4, ... (step = 2 words: lanes 0-31
-      // the first, 32-63 the second): lane 32 hh + i gets the 32-read columns
-      // of position 32 wl + i
-      for (int w = 2 * wv; w < L; w += 8) {
-        const int wl = w + hh;
-        uint2 v = make_uint2(0u, 0u);
-        if (wl < L) {
-          v = *reinterpret_cast<const uint2*>(in + s * R + 2 * wl);
-          const int64_t nb = len - 32 * (int64_t)(w0 + wl);  // valid bases of the word
-          const uint32_t m = nb >= 32 ? ~0u : nb <= 0 ? 0u : ((1u << nb) - 1u);
-          v.x &= m;
-          v.y &= m;
-        }
-        const uint32_t cl = half_bit_transpose(v.x, lane, bt), ch = half_bit_transpose(v.y, lane, bt);
-        if (wl < L) {
-          const uint32_t p = 32u * (uint32_t)wl + (uint32_t)s;  // position in the half stripe
-          const uint32_t l = __umulhi(p, div_m) >> div_s, o = p - l * (uint32_t)L;
-          *reinterpret_cast<uint2*>(rows + (o >> 1) * kBndRowWords + 4 * l + 2 * (o & 1)) = make_uint2(cl, ch);
-        }
-      }
-      __syncthreads();
-      // 3. rows t: 32 words of 16 bytes at word (G T + t) 64 + 32 h + l
-      uint4* out = reinterpret_cast<uint4*>(tp) + G * (uint64_t)T * kWave + 32 * h;
-      for (int t = threadIdx.x >> 5; t < T; t += 8)
-        out[(uint64_t)t * kWave + s] = *reinterpret_cast<const uint4*>(rows + t * kBndRowWords + 4 * s);
-      __syncthreads();
-    }
-    __syncthreads();  // meta is rewritten for the next bundle
   }
 }
 
@@ -416,17 +315,6 @@ hipError_t nt_dev_launch_call(const NtProgram* prog, const NtBatch* B, const NtO
 
 hipError_t nt_dev_launch_combine(const NtBatch* B, const NtOut* O, int np, int grid, hipStream_t stream) {
   hipLaunchKernelGGL(nt::nt_call_combine_kernel, dim3(grid), dim3(256), 0, stream, *B, *O, np);
-  return hipGetLastError();
-}
-
-hipError_t nt_dev_launch_bundle(const NtBatch* B, uint64_t n_stripes, uint32_t* tp, int L, uint32_t div_m,
-                                uint32_t div_s, hipStream_t stream, int cu_count) {
-  // one workgroup per bundle (its half stripes in turn), a grid-stride loop over them
-  uint64_t grid = n_stripes ? B->n_bundles : 0;
-  if (grid > (uint64_t)cu_count * 16) grid = (uint64_t)cu_count * 16;
-  if (grid == 0) return hipSuccess;
-  const size_t lds = ((size_t)((L + 1) / 2) * nt::kBndRowWords + (size_t)NT_BUNDLE * (2 * L + 2) + 4 * NT_BUNDLE) * 4;
-  hipLaunchKernelGGL(nt::nt_bundle_kernel, dim3((uint32_t)grid), dim3(256), lds, stream, *B, tp, L, div_m, div_s);
   return hipGetLastError();
 }
 

@@ -1,7 +1,6 @@
 // nt_pack.cpp -- the host-only half of the C-ABI (no HIP): pattern parsing and
 // the program (A1, extract_patterns NanoTel.R:2322-2334), the 2-bit packer
-// with the reverse complement fused (A14, NanoTel.R:2219-2221), the bundle
-// T-layout builder, serials and row order (A15, NanoTel.R:2050-2070,
+// with the reverse complement fused (A14, NanoTel.R:2219-2221), serials and row order (A15, NanoTel.R:2050-2070,
 // 2234-2258), the summary columns (NanoTel.R:1820-1837, 1926-1974) and the
 // host twin of the synthetic-read generator.  Built into libnanotel.so and,
 // with the reader and the oracle, into the sanitizer test driver
@@ -110,45 +109,6 @@ static const bool g_avx2 = __builtin_cpu_supports("avx2");
 
 inline bool pack32(const unsigned char* p, uint32_t& lo, uint32_t& hi) {
   return g_avx2 ? pack32_avx2(p, lo, hi) : pack32_scalar(p, lo, hi);
-}
-
-// 32 x 32 bit transpose: y[i] bit s = x[s] bit i (32 reads' plane words of
-// one 32-base block -> the T-layout words of its 32 positions, bit s = slot s).
-// AVX2: a byte transpose of the 32 rows into 4 registers (register b, byte s
-// = byte b of x[s]: in-lane byte shuffle, dword permute, 64-bit 4x4 transpose),
-// then bit k of every byte by one shift + movemask per output word.
-__attribute__((target("avx2"))) static void transpose32_avx2(const uint32_t* x, uint32_t* y) {
-  const __m256i bsh = _mm256_setr_epi8(0, 4, 8, 12, 1, 5, 9, 13, 2, 6, 10, 14, 3, 7, 11, 15,
-                                       0, 4, 8, 12, 1, 5, 9, 13, 2, 6, 10, 14, 3, 7, 11, 15);
-  const __m256i dperm = _mm256_setr_epi32(0, 4, 1, 5, 2, 6, 3, 7);
-  __m256i B[4];
-  for (int g = 0; g < 4; ++g) {
-    // lane h, dword b = byte b of rows 8g+4h .. 8g+4h+3; then qword b = byte b of rows 8g .. 8g+7
-    const __m256i a = _mm256_shuffle_epi8(_mm256_loadu_si256((const __m256i*)(x + 8 * g)), bsh);
-    B[g] = _mm256_permutevar8x32_epi32(a, dperm);
-  }
-  const __m256i t0 = _mm256_unpacklo_epi64(B[0], B[1]), t1 = _mm256_unpackhi_epi64(B[0], B[1]);
-  const __m256i t2 = _mm256_unpacklo_epi64(B[2], B[3]), t3 = _mm256_unpackhi_epi64(B[2], B[3]);
-  const __m256i Y[4] = {_mm256_permute2x128_si256(t0, t2, 0x20), _mm256_permute2x128_si256(t1, t3, 0x20),
-                        _mm256_permute2x128_si256(t0, t2, 0x31), _mm256_permute2x128_si256(t1, t3, 0x31)};
-  for (int b = 0; b < 4; ++b) {
-    y[8 * b + 7] = (uint32_t)_mm256_movemask_epi8(Y[b]);
-    y[8 * b + 6] = (uint32_t)_mm256_movemask_epi8(_mm256_slli_epi16(Y[b], 1));
-    y[8 * b + 5] = (uint32_t)_mm256_movemask_epi8(_mm256_slli_epi16(Y[b], 2));
-    y[8 * b + 4] = (uint32_t)_mm256_movemask_epi8(_mm256_slli_epi16(Y[b], 3));
-    y[8 * b + 3] = (uint32_t)_mm256_movemask_epi8(_mm256_slli_epi16(Y[b], 4));
-    y[8 * b + 2] = (uint32_t)_mm256_movemask_epi8(_mm256_slli_epi16(Y[b], 5));
-    y[8 * b + 1] = (uint32_t)_mm256_movemask_epi8(_mm256_slli_epi16(Y[b], 6));
-    y[8 * b + 0] = (uint32_t)_mm256_movemask_epi8(_mm256_slli_epi16(Y[b], 7));
-  }
-}
-
-static void transpose32_scalar(const uint32_t* x, uint32_t* y) {
-  for (int i = 0; i < 32; ++i) {
-    uint32_t w = 0;
-    for (int s = 0; s < 32; ++s) w |= ((x[s] >> i) & 1u) << s;
-    y[i] = w;
-  }
 }
 
 // number of non-A/C/G/T bytes in s[0, n)
@@ -372,63 +332,6 @@ int64_t pack_one(const unsigned char* s, uint64_t n, int rc, uint32_t* out, uint
 }
 
 
-// The T-layout of one bundle on the host (nt_common.h): stripes [g0, g0 +
-// nst) of tp, every word written (zeros past a read's end and in the unused
-// half of the last row when L is odd).  Block w of the 32 slots' plane words
-// -> 32 positions; position p = block k = p / L (stripe k / 64, lane k % 64),
-// offset o = p % L (row o / 2, half o % 2).
-static void tlayout_bundle(const uint32_t* planes, const uint64_t* blk_off, const uint32_t* len,
-                           const uint32_t* slots, uint64_t g0, uint64_t nst, uint32_t L, uint32_t* tp) {
-  const uint64_t T = (L + 1) / 2;
-  uint32_t* base = tp + g0 * T * 64 * 4;
-  std::memset(base, 0, nst * T * 64 * 16);
-  uint64_t n_max = 0;
-  const uint32_t* pl[NT_BUNDLE];
-  uint64_t ln[NT_BUNDLE];
-  for (int s = 0; s < NT_BUNDLE; ++s) {
-    const uint32_t r = slots[s];
-    ln[s] = r != 0xFFFFFFFFu ? len[r] : 0;
-    pl[s] = r != 0xFFFFFFFFu ? planes + 2 * blk_off[r] : nullptr;
-    n_max = std::max(n_max, ln[s]);
-  }
-  n_max = std::min<uint64_t>(n_max, nst * 64 * L);
-  alignas(32) uint32_t xl[32], xh[32], yl[32], yh[32];
-  uint64_t k = 0, o = 0;  // block and offset of position 32 w
-  for (uint64_t w = 0; 32 * w < n_max; ++w) {
-    for (int s = 0; s < NT_BUNDLE; ++s) {
-      const int64_t nb = (int64_t)ln[s] - 32 * (int64_t)w;  // valid bases of the word
-      const uint32_t m = nb >= 32 ? ~0u : nb <= 0 ? 0u : ((1u << nb) - 1u);
-      xl[s] = m ? pl[s][2 * w] & m : 0u;
-      xh[s] = m ? pl[s][2 * w + 1] & m : 0u;
-    }
-    if (g_avx2) {
-      transpose32_avx2(xl, yl);
-      transpose32_avx2(xh, yh);
-    } else {
-      transpose32_scalar(xl, yl);
-      transpose32_scalar(xh, yh);
-    }
-    const int np = (int)std::min<uint64_t>(32, n_max - 32 * w);
-    uint64_t kk = k, oo = o;
-    for (int i = 0; i < np; ++i) {
-      uint32_t* q = base + (((kk >> 6) * T + (oo >> 1)) * 64 + (kk & 63)) * 4 + 2 * (oo & 1);
-      q[0] = yl[i];
-      q[1] = yh[i];
-      if (++oo == L) {
-        oo = 0;
-        ++kk;
-      }
-    }
-    o += 32;
-    while (o >= L) {
-      o -= L;
-      ++k;
-    }
-  }
-}
-
-
-
 NtSynth to_synth(const nt_synth_params* sp) {
   NtSynth S;
   S.seed = sp->seed;
@@ -639,23 +542,6 @@ int nt_pack_reads(const char* const* seqs, const uint64_t* lens, uint64_t n_read
   return bad.load() ? NT_E_LETTER : NT_OK;
 }
 
-
-int nt_bundle_layout_host(const uint32_t* planes, const uint64_t* blk_off, const uint32_t* len,
-                          const uint32_t* bnd_read, const uint64_t* bnd_stripe, uint64_t n_bundles,
-                          int32_t subseq_length, uint32_t* tplanes, uint64_t tplane_bytes) {
-  if (n_bundles == 0) return NT_OK;
-  if (!planes || !blk_off || !len || !bnd_read || !bnd_stripe || !tplanes) return NT_E_ARG;
-  if (subseq_length < 1 || subseq_length > 170) return NT_E_ARG;
-  const uint64_t L = (uint64_t)subseq_length, T = (L + 1) / 2;
-  if (bnd_stripe[n_bundles] * T * 64 * 16 > tplane_bytes) return NT_E_ARG;
-  for (uint64_t b = 0; b < n_bundles; ++b)
-    if (bnd_stripe[b + 1] < bnd_stripe[b]) return NT_E_ARG;
-  parallel_for(n_bundles, [&](uint64_t b) {
-    tlayout_bundle(planes, blk_off, len, bnd_read + NT_BUNDLE * b, bnd_stripe[b], bnd_stripe[b + 1] - bnd_stripe[b],
-                   (uint32_t)L, tplanes);
-  });
-  return NT_OK;
-}
 
 int64_t nt_assign_serials(const uint8_t* is_telo, uint64_t n, double* serial_start_io,
                           double* max_serial_io, double* serial_out, int64_t* order_out) {

@@ -55,9 +55,9 @@ class NtBatch(ctypes.Structure):
         ("planes", ctypes.c_void_p), ("blk_off", ctypes.c_void_p), ("len", ctypes.c_void_p),
         ("win_off", ctypes.c_void_p), ("exc_off", ctypes.c_void_p), ("exc_pos", ctypes.c_void_p),
         ("exc_code", ctypes.c_void_p), ("n_reads", ctypes.c_uint64), ("n_windows", ctypes.c_uint64),
-        # bundle scan (optional): the T-layout and its bundles, the reads left to the per-read scan
-        ("tplanes", ctypes.c_void_p), ("bnd_read", ctypes.c_void_p), ("bnd_stripe", ctypes.c_void_p),
-        ("n_bundles", ctypes.c_uint64), ("list", ctypes.c_void_p), ("n_list", ctypes.c_uint64),
+        # bundle scan (optional): the bundles' reads, the reads left to the per-read scan
+        ("bnd_read", ctypes.c_void_p), ("n_bundles", ctypes.c_uint64), ("list", ctypes.c_void_p),
+        ("n_list", ctypes.c_uint64),
     ]
 
 
@@ -98,10 +98,7 @@ SIGNATURES = {
     "nt_pack_reads": (ctypes.c_int, [_P, _P, ctypes.c_uint64, ctypes.c_int32, ctypes.c_int32, _P, _P,
                                      _P, _P, _P, _P, _P]),
     "nt_exc_marks": (ctypes.c_int, [_P, _P, _P, _P, ctypes.c_uint64, _P]),
-    "nt_bundle_plan": (ctypes.c_int, [_P, _P, _P, ctypes.c_uint64, _P, _P, _U64P, _P, _U64P, _U64P]),
-    "nt_bundle_layout_host": (ctypes.c_int, [_P, _P, _P, _P, _P, ctypes.c_uint64, ctypes.c_int32, _P,
-                                             ctypes.c_uint64]),
-    "nt_bundle_layout": (ctypes.c_int, [_P, ctypes.POINTER(NtBatch), _P, ctypes.c_uint64]),
+    "nt_bundle_plan": (ctypes.c_int, [_P, _P, _P, _P, ctypes.c_uint64, _P, _U64P, _P, _U64P]),
     "nt_scan_call": (ctypes.c_int, [_P, ctypes.POINTER(NtBatch), ctypes.POINTER(NtOut), ctypes.c_uint64]),
     "nt_set_profiling": (ctypes.c_int, [_P, ctypes.c_int]),
     "nt_kernel_times": (ctypes.c_int64, [_P, ctypes.POINTER(ctypes.c_double),

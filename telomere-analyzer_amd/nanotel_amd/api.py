@@ -255,7 +255,7 @@ class NanoTel:
                          bundles=None):
         """Device-resident hot path: all pointer arguments are device pointers
         (ints); n_windows = sum of the window rows (window_rows).  bundles: a DeviceBundles
-        (bundle_plan + bundle_layout_device) or None (per-read scan only).
+        (a bundle_plan's lists on the device) or None (per-read scan only).
         Asynchronous on the context stream (see set_stream)."""
         B = self._batch(planes, blk_off, lengths, win_off, n_reads, n_windows, exc_off, exc_pos, exc_code,
                         bundles)
@@ -268,8 +268,8 @@ class NanoTel:
         b = bundles
         return NtBatch(planes, blk_off, lengths, win_off, exc_off or None, exc_pos or None,
                        exc_code or None, int(n_reads), int(n_windows),
-                       b.tplanes if b else None, b.bnd_read if b else None, b.bnd_stripe if b else None,
-                       b.n_bundles if b else 0, (b.list or None) if b else None, b.n_list if b else 0)
+                       b.bnd_read if b else None, b.n_bundles if b else 0, (b.list or None) if b else None,
+                       b.n_list if b else 0)
 
     def exc_marks(self, lengths, exc_off, exc_pos):
         """nt_exc_marks on host arrays: uint8 per read, 1 = its non-ACGT letters
@@ -283,31 +283,23 @@ class NanoTel:
                                   ln.size, out.ctypes.data), self._h)
         return out[:ln.size]
 
-    def bundle_plan(self, lengths, has_exc=None):
-        """nt_bundle_plan on host arrays: returns a BundlePlan (numpy arrays)."""
+    def bundle_plan(self, lengths, has_exc=None, blk_off=None):
+        """nt_bundle_plan on host arrays: returns a BundlePlan (numpy arrays).
+        blk_off (the batch's block offsets; None = the caller vouches that
+        every bundle's planes lie within 2 GiB): bundles spread wider go to the
+        per-read scan."""
         ln = np.ascontiguousarray(lengths, np.uint32)
         n = ln.size
         nbmax = (n + 31) // 32
         bread = np.zeros(max(1, nbmax * 32), np.uint32)
-        bstripe = np.zeros(nbmax + 1, np.uint64)
         lst = np.zeros(max(1, n), np.uint32)
         hx = None if has_exc is None else np.ascontiguousarray(has_exc, np.uint8)
-        nb, nl, tpb = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
-        _check(lib().nt_bundle_plan(self._h, ln.ctypes.data, None if hx is None else hx.ctypes.data, n,
-                                    bread.ctypes.data, bstripe.ctypes.data, ctypes.byref(nb), lst.ctypes.data,
-                                    ctypes.byref(nl), ctypes.byref(tpb)), self._h)
-        return BundlePlan(bread[:nb.value * 32], bstripe[:nb.value + 1], lst[:nl.value], tpb.value)
-
-    def bundle_layout_host(self, planes, blk_off, lengths, plan):
-        """nt_bundle_layout_host: the T-layout of a BundlePlan (host numpy
-        planes / blk_off / lengths as from nt_pack_reads) -> uint32 array."""
-        return bundle_layout_host(planes, blk_off, lengths, plan, self.subseq_length)
-
-    def bundle_layout_device(self, planes, blk_off, lengths, win_off, n_reads, n_windows, bundles):
-        """nt_bundle_layout: write bundles.tplanes (device) from the per-read planes."""
-        B = self._batch(planes, blk_off, lengths, win_off, n_reads, n_windows, bundles=bundles)
-        _check(lib().nt_bundle_layout(self._h, ctypes.byref(B), bundles.tplanes, int(bundles.tplane_bytes)),
-               self._h)
+        bo = None if blk_off is None else np.ascontiguousarray(blk_off, np.uint64)
+        nb, nl = ctypes.c_uint64(), ctypes.c_uint64()
+        _check(lib().nt_bundle_plan(self._h, ln.ctypes.data, None if bo is None else bo.ctypes.data,
+                                    None if hx is None else hx.ctypes.data, n, bread.ctypes.data, ctypes.byref(nb),
+                                    lst.ctypes.data, ctypes.byref(nl)), self._h)
+        return BundlePlan(bread[:nb.value * 32], lst[:nl.value])
 
     def synth_device(self, sp, n_reads, planes_ptr):
         _check(lib().nt_synth_device(self._h, ctypes.byref(sp), int(n_reads), planes_ptr), self._h)
@@ -318,34 +310,19 @@ class NanoTel:
 
 
 class BundlePlan:
-    """Host result of nt_bundle_plan: bnd_read (n_bundles*32 u32), bnd_stripe
-    (n_bundles+1 u64), list (the reads left to the per-read scan), tplane_bytes."""
+    """Host result of nt_bundle_plan: bnd_read (n_bundles*32 u32, ~0 = empty
+    slot) and list (the reads left to the per-read scan)."""
 
-    def __init__(self, bnd_read, bnd_stripe, lst, tplane_bytes):
-        self.bnd_read, self.bnd_stripe, self.list, self.tplane_bytes = bnd_read, bnd_stripe, lst, tplane_bytes
-        self.n_bundles = len(bnd_stripe) - 1 if len(bnd_stripe) else 0
+    def __init__(self, bnd_read, lst):
+        self.bnd_read, self.list = bnd_read, lst
+        self.n_bundles = len(bnd_read) // 32
 
 
 class DeviceBundles:
-    """Device pointers (ints) of a bundle layout for scan_call_device."""
+    """Device pointers (ints) of a BundlePlan for scan_call_device."""
 
-    def __init__(self, tplanes, bnd_read, bnd_stripe, n_bundles, lst, n_list, tplane_bytes):
-        self.tplanes, self.bnd_read, self.bnd_stripe, self.n_bundles = tplanes, bnd_read, bnd_stripe, n_bundles
-        self.list, self.n_list, self.tplane_bytes = lst, n_list, tplane_bytes
-
-
-def bundle_layout_host(planes, blk_off, lengths, plan, subseq_length):
-    """nt_bundle_layout_host (no device): host T-layout of `plan`'s bundles."""
-    pl = np.ascontiguousarray(planes, np.uint32)
-    bo = np.ascontiguousarray(blk_off, np.uint64)
-    ln = np.ascontiguousarray(lengths, np.uint32)
-    br = np.ascontiguousarray(plan.bnd_read, np.uint32)
-    bs = np.ascontiguousarray(plan.bnd_stripe, np.uint64)
-    out = np.empty(max(1, plan.tplane_bytes // 4), np.uint32)
-    _check(lib().nt_bundle_layout_host(pl.ctypes.data, bo.ctypes.data, ln.ctypes.data, br.ctypes.data,
-                                       bs.ctypes.data, plan.n_bundles, int(subseq_length), out.ctypes.data,
-                                       int(plan.tplane_bytes)))
-    return out[:plan.tplane_bytes // 4]
+    def __init__(self, bnd_read, n_bundles, lst, n_list):
+        self.bnd_read, self.n_bundles, self.list, self.n_list = bnd_read, n_bundles, lst, n_list
 
 
 def jit_prebuild(patterns, tvr_patterns=None, subseq_length=100, min_density=0.6, check_right_edge=False,

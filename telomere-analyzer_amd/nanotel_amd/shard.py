@@ -245,7 +245,16 @@ def ingest_plan(rdr, nrec, rank, world, device=None, log=None):
         return IngestPlan(reason="one rank" if world <= 1 else "NT_SHARD_INGEST=0")
     from ._lib import NanoTelError
     files = rdr.files()
-    plain, total_bytes = rdr.layout()
+    # the layout (a stat of every file) can fail on one rank only: its failure
+    # goes through the same flag exchange as the reads below, so that no rank
+    # waits in a collective the failing one never joins
+    lay_err, plain, total_bytes = None, False, 0
+    try:
+        plain, total_bytes = rdr.layout()
+    except (NanoTelError, OSError) as ex:
+        lay_err = ex
+    if _all_sum(np.array([1 if lay_err is not None else 0], np.int64), device)[0]:
+        raise lay_err if lay_err is not None else RuntimeError("NanoTel: another rank failed to read the input")
     if plain:
         a, b = total_bytes * rank // world, total_bytes * (rank + 1) // world
         row, err = np.zeros((world, 4), np.int64), None

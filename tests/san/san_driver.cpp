@@ -1,7 +1,7 @@
 // san_driver.cpp -- the host code that parses untrusted input and packs it,
 // built with AddressSanitizer + UndefinedBehaviorSanitizer (tests/san/Makefile,
 // run by tests/test_sanitizers.py): the FASTA/FASTQ(.gz) reader (nt_io.cpp),
-// the 2-bit packer with --rc and IUPAC exceptions, the host T-layout builder,
+// the 2-bit packer with --rc and IUPAC exceptions,
 // serials / row columns (nt_pack.cpp) and the CPU oracle
 // (oracle/nanotel_oracle.c, test infrastructure).  Every check is against an
 // independent plain restatement; any sanitizer report aborts the run.
@@ -164,7 +164,7 @@ static int code2(char c) {
   return -1;
 }
 
-static void test_packer_and_tlayout(std::mt19937_64& g) {
+static void test_packer(std::mt19937_64& g) {
   std::vector<std::string> seqs;
   for (int i = 0; i < 200; ++i) seqs.push_back(rand_seq(g, 1 + g() % 7000, i % 5 ? "ACGTacgt" : "ACGTNRYKMacgtn"));
   std::vector<const char*> ptr;
@@ -191,37 +191,6 @@ static void test_packer_and_tlayout(std::mt19937_64& g) {
         const uint64_t w = 2 * (blk[r] + p / 32);
         const int got = (int)((planes[w] >> (p % 32)) & 1u) | (int)(((planes[w + 1] >> (p % 32)) & 1u) << 1);
         CHECK(got == c);
-      }
-    if (rc) continue;
-    // the host T-layout of bundles of the reads without exceptions, L = 37
-    std::vector<uint32_t> in;
-    for (uint64_t r = 0; r < n; ++r)
-      if (eoff[r + 1] == eoff[r]) in.push_back((uint32_t)r);
-    std::stable_sort(in.begin(), in.end(), [&](uint32_t a, uint32_t b) { return lens[a] > lens[b]; });
-    const uint64_t L = 37, T = (L + 1) / 2, nb = (in.size() + 31) / 32;
-    std::vector<uint32_t> bread(nb * 32, 0xFFFFFFFFu);
-    std::vector<uint64_t> bstripe(nb + 1);
-    uint64_t gs = 0;
-    for (uint64_t b = 0; b < nb; ++b) {
-      bstripe[b] = gs;
-      for (uint64_t s = 0; s < 32 && b * 32 + s < in.size(); ++s) bread[b * 32 + s] = in[b * 32 + s];
-      gs += ((lens[in[b * 32]] + L - 1) / L + 63) / 64;
-    }
-    bstripe[nb] = gs;
-    std::vector<uint32_t> tp(gs * T * 64 * 4 + 4, 0xDEADBEEFu);
-    CHECK(nt_bundle_layout_host(planes.data(), blk.data(), len.data(), bread.data(), bstripe.data(), nb, (int)L,
-                                tp.data(), gs * T * 64 * 16) == 0);
-    CHECK(tp[gs * T * 64 * 4] == 0xDEADBEEFu);  // nothing past the buffer
-    for (uint64_t b = 0; b < nb; ++b)
-      for (uint64_t s = 0; s < 32; ++s) {
-        const uint32_t r = bread[b * 32 + s];
-        if (r == 0xFFFFFFFFu) continue;
-        for (uint64_t p = 0; p < lens[r]; p += 1 + g() % 7) {
-          const uint64_t k = p / L, o = p % L;
-          const uint64_t idx = ((bstripe[b] + k / 64) * T + o / 2) * 64 + k % 64;
-          const int got = (int)((tp[4 * idx + 2 * (o & 1)] >> s) & 1u) | (int)(((tp[4 * idx + 2 * (o & 1) + 1] >> s) & 1u) << 1);
-          CHECK(got == code2(seqs[r][p]));
-        }
       }
   }
 }
@@ -288,7 +257,7 @@ int main(int argc, char** argv) {
   if (argc < 2) return 2;
   std::mt19937_64 g(20261017);
   test_reader(g, argv[1]);
-  test_packer_and_tlayout(g);
+  test_packer(g);
   test_serials_rows(g);
   test_oracle(g);
   std::printf("san_driver: %s (%d failed checks)\n", g_fail ? "FAIL" : "OK", g_fail);

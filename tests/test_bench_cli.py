@@ -24,3 +24,21 @@ def test_bench_rejects_zero_gpus():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "0"], timeout=60,
                        capture_output=True, text=True)
     assert r.returncode != 0
+
+
+def test_bench_refuses_debug_environment():
+    """Timing builds and skipped kernels change what a step computes: bench.py
+    exits non-zero before touching the GPU when any such variable is set
+    (VERDICT r4 item 6), and records the other NT_* knobs in its line."""
+    sys.path.insert(0, ROOT)
+    import bench
+    for var, val in (("NT_DBG_SKIP_CALL", "1"), ("NT_JIT_OPTS", "-DNT_TS_DBG_NOWALK=1"), ("NT_TSCAN", "0"),
+                     ("NT_HOST_TLAYOUT", "1"), ("NT_TS_DBG_NOOUT", "1")):
+        env = dict(os.environ, **{var: val})
+        assert bench.refused_env(env) == [f"{var}={val}"]
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "1", "--warmup", "0"],
+                           env=env, timeout=60, capture_output=True, text=True)
+        assert r.returncode == 2 and var in r.stderr, (var, r.returncode, r.stderr[-400:])
+    clean = {k: v for k, v in os.environ.items() if not k.startswith("NT_")}
+    assert bench.refused_env(clean) == []
+    assert bench.env_knobs(dict(clean, NT_TSUB="2", NT_JIT_CACHE="/x")) == {"NT_JIT_CACHE": "/x", "NT_TSUB": "2"}

@@ -628,21 +628,17 @@ def test_device_resident_path_matches_host_path(jit):
 
 
 def _device_bundles(nt, t, n, read_len, has_exc=None):
-    """The bench's bundle layout of a device batch (host plan, device transpose);
-    has_exc: reads left to the per-read scan (their list goes with the bundles)."""
+    """The bench's bundles of a device batch (host plan from the lengths and
+    block offsets); has_exc: reads left to the per-read scan (their list goes
+    with the bundles)."""
     import torch
     from nanotel_amd.api import DeviceBundles
-    plan = nt.bundle_plan(np.full(n, read_len, np.uint32), has_exc)
-    d = dict(bnd_read=torch.from_numpy(plan.bnd_read.view(np.int32)).cuda(),
-             bnd_stripe=torch.from_numpy(plan.bnd_stripe.view(np.int64)).cuda(),
-             tplanes=torch.empty(max(1, plan.tplane_bytes // 4), dtype=torch.int32, device="cuda"))
+    plan = nt.bundle_plan(np.full(n, read_len, np.uint32), has_exc, blk_off=t["blk_off"].cpu().numpy().view(np.uint64))
+    d = dict(bnd_read=torch.from_numpy(plan.bnd_read.view(np.int32)).cuda())
     nl = len(plan.list)
     if nl:
         d["list"] = torch.from_numpy(plan.list.view(np.int32)).cuda()
-    b = DeviceBundles(d["tplanes"].data_ptr(), d["bnd_read"].data_ptr(), d["bnd_stripe"].data_ptr(),
-                      plan.n_bundles, d["list"].data_ptr() if nl else 0, nl, plan.tplane_bytes)
-    nt.bundle_layout_device(t["planes"].data_ptr(), t["blk_off"].data_ptr(), t["lens"].data_ptr(),
-                            t["win_off"].data_ptr(), n, n * t["rows"], b)
+    b = DeviceBundles(d["bnd_read"].data_ptr(), plan.n_bundles, d["list"].data_ptr() if nl else 0, nl)
     nt.synchronize()
     return b, d
 
@@ -810,26 +806,22 @@ def test_pipelined_calls_with_rewritten_inputs(back):
             run(t, b, o)
             nt.synchronize()
             refs.append(o)
-        # the input sets the caller rewrites: planes and T-layout (the uniform
-        # layout and the bundle lists are the same for every batch here)
+        # the input sets the caller rewrites: the planes (the uniform layout and
+        # the bundle lists are the same for every batch here)
         sets = []
         for _ in range(back + 1):
-            t0, _, k0 = batches[0]
+            t0, b0, _ = batches[0]
             x = dict(t0)
             x["planes"] = torch.empty_like(t0["planes"])
-            tpl = torch.empty_like(k0["tplanes"])
-            xb = DeviceBundles(tpl.data_ptr(), k0["bnd_read"].data_ptr(), k0["bnd_stripe"].data_ptr(),
-                               batches[0][1].n_bundles, 0, 0, batches[0][1].tplane_bytes)
-            sets.append((x, xb, tpl))
+            sets.append((x, b0))
         order = [0, 1, 2, 0, 2, 1]
         outs = [{k: torch.full_like(batches[i][0][k], 0x55) for k in keys} for i in order]
         nt.set_pipelined(True)
         for c, (i, o) in enumerate(zip(order, outs)):
-            x, xb, tpl = sets[c % len(sets)]
+            x, xb = sets[c % len(sets)]
             if c >= len(sets):
                 nt.wait_call(back)  # the calling that still reads this set
             x["planes"].copy_(batches[i][0]["planes"])
-            tpl.copy_(batches[i][2]["tplanes"])
             run(x, xb, o)
         nt.join()
         nt.synchronize()
@@ -900,35 +892,25 @@ def test_full_size_bundle_scan_equals_per_read_scan(cfg):
     torch.cuda.empty_cache()
 
 
-@pytest.mark.parametrize("read_len", [50000, 10000, 6450, 3001])
-def test_host_tlayout_matches_device(read_len):
-    # the T-layout the host path uploads (nt_bundle_layout_host, built at
-    # ingest) and the one the bench builds on the device (nt_bundle_layout)
-    # are the same bits, so the bench's timed step is the product's device work
-    from nanotel_amd import synth_params
-    n = 160  # 5 bundles
-    nt = _nt(patterns="TTAGGG")
-    t = _device_batch(nt, synth_params(read_len=read_len, first_read=read_len), n, read_len)
-    b, d = _device_bundles(nt, t, n, read_len)
-    plan = nt.bundle_plan(np.full(n, read_len, np.uint32))
-    host = nt.bundle_layout_host(t["planes"].cpu().numpy().view(np.uint32),
-                                 t["blk_off"].cpu().numpy().view(np.uint64),
-                                 t["lens"].cpu().numpy().view(np.uint32), plan)
-    dev = d["tplanes"].cpu().numpy().view(np.uint32)[:plan.tplane_bytes // 4]
-    assert host.shape == dev.shape
-    assert np.array_equal(host, dev), np.flatnonzero(host != dev)[:8]
-
-
-def test_host_tlayout_matches_device_mixed_lengths():
-    # ragged bundles (lengths sorted within a bundle, ends inside words),
-    # L = 37 (odd: the last row's second half holds no position)
+@pytest.mark.parametrize("L", [37, 100, 50])
+def test_bundle_scan_ragged_packed_batch(L):
+    # ragged bundles from the host packer (lengths sorted within a bundle, read
+    # ends inside plane words, bundles whose reads lie anywhere in the batch),
+    # odd L (the second half window one position short): the bundle scan
+    # against the per-read scan of the same device batch on every output
     import ctypes
     import torch
     from nanotel_amd import _lib
     from nanotel_amd.api import DeviceBundles
-    rng = np.random.default_rng(5)
-    seqs = [bytes(rng.choice(list(b"ACGT"), int(rng.integers(1, 12000))).tolist()) for _ in range(150)]
-    L = 37
+    rng = np.random.default_rng(5 + L)
+    seqs = []
+    for i in range(150):
+        n_i = int(rng.integers(1, 12000))
+        s_i = bytearray(rng.choice(list(b"ACGT"), n_i).tolist())
+        if i % 3 == 0 and n_i > 3000:  # a telomeric tract somewhere
+            a0 = int(rng.integers(0, n_i - 2000))
+            s_i[a0:a0 + 1800] = (b"TTAGGG" * 300)[:1800]
+        seqs.append(bytes(s_i))
     lib = _lib.lib()
     n = len(seqs)
     ptrs = (ctypes.c_char_p * n)(*seqs)
@@ -941,36 +923,69 @@ def test_host_tlayout_matches_device_mixed_lengths():
     assert lib.nt_pack_reads(ctypes.cast(ptrs, ctypes.c_void_p), lens.ctypes.data, n, 0, L, planes.ctypes.data,
                              blk.ctypes.data, ln.ctypes.data, wo.ctypes.data, None, None, None) == 0
     nt = _nt(patterns="TTAGGG", subseq_length=L)
-    plan = nt.bundle_plan(ln)
-    host = nt.bundle_layout_host(planes, blk, ln, plan)
-    dp = torch.from_numpy(planes.view(np.int32)).cuda()
-    dblk = torch.from_numpy(blk.view(np.int64)).cuda()
-    dln = torch.from_numpy(ln.view(np.int32)).cuda()
-    dwo = torch.from_numpy(wo.view(np.int64)).cuda()
+    assert nt.tscan
+    plan = nt.bundle_plan(ln, blk_off=blk)
+    assert plan.n_bundles == 5 and len(plan.list) == 0
+    dev = {k: torch.from_numpy(v).cuda() for k, v in (("planes", planes.view(np.int32)), ("blk", blk.view(np.int64)),
+                                                    ("ln", ln.view(np.int32)), ("wo", wo.view(np.int64)))}
     br = torch.from_numpy(plan.bnd_read.view(np.int32)).cuda()
-    bs = torch.from_numpy(plan.bnd_stripe.view(np.int64)).cuda()
-    tp = torch.full((plan.tplane_bytes // 4,), -1, dtype=torch.int32, device="cuda")
-    bb = DeviceBundles(tp.data_ptr(), br.data_ptr(), bs.data_ptr(), plan.n_bundles, 0, 0, plan.tplane_bytes)
-    nt.bundle_layout_device(dp.data_ptr(), dblk.data_ptr(), dln.data_ptr(), dwo.data_ptr(), n, int(tw.value), bb)
-    nt.synchronize()
-    dev = tp.cpu().numpy().view(np.uint32)
-    assert np.array_equal(host, dev), np.flatnonzero(host != dev)[:8]
+    bb = DeviceBundles(br.data_ptr(), plan.n_bundles, 0, 0)
+    nwc = int(tw.value) * nt.n_pass
+    outs = []
+    for bundles in (None, bb):
+        o = dict(start=torch.full((n * 3,), 7, dtype=torch.int32, device="cuda"),
+                 end=torch.full((n * 3,), 7, dtype=torch.int32, device="cuda"),
+                 dens=torch.full((n * 3,), 7.0, dtype=torch.float64, device="cuda"),
+                 flags=torch.zeros(n, dtype=torch.uint8, device="cuda"),
+                 wc=torch.full((nwc,), 0x55, dtype=torch.uint8, device="cuda"))
+        nt.scan_call_device(dev["planes"].data_ptr(), dev["blk"].data_ptr(), dev["ln"].data_ptr(),
+                            dev["wo"].data_ptr(), n, int(tw.value), int(ml.value), o["start"].data_ptr(),
+                            o["end"].data_ptr(), o["dens"].data_ptr(), o["flags"].data_ptr(), o["wc"].data_ptr(),
+                            bundles=bundles)
+        nt.synchronize()
+        outs.append({k: v.cpu().numpy() for k, v in o.items()})
+    ref, got = outs
+    for k in ("start", "end", "flags"):
+        assert np.array_equal(got[k], ref[k]), (k, np.flatnonzero(got[k] != ref[k])[:8])
+    assert np.array_equal(got["dens"].view(np.uint64), ref["dens"].view(np.uint64))
+    # every window count of every read and pass (padding windows excluded)
+    for r in range(n):
+        nw = int(lib.nt_window_count(int(ln[r]), L))
+        rows = int(lib.nt_window_rows(nw))
+        for p in range(nt.n_pass):
+            o = int(wo[r]) * nt.n_pass + p * rows
+            assert np.array_equal(got["wc"][o:o + nw], ref["wc"][o:o + nw]), (r, p)
+    assert int(((ref["flags"] & 1) != 0).sum()) > 5
 
 
-# BASELINE.json configs[2], [3] (10M x 50 kb, bundle scan: planes 125 GB + the
-# T-layout 128 GB resident) and one GPU's shard of configs[4] (12.5M x 50 kb,
-# 156 GB of planes, per-read scan): the bench's full-size batches, sampled
-# against the oracle on reads regenerated on the host (nt_synth_ascii) --
-# the first and last reads (the last bundles: block offsets past 2^31,
-# T-layout words past 2^32) and reads spread over the whole batch; every row
-# field and every window count of every pass (NanoTel.R:717-766, 1080-1155).
+def test_bundle_plan_keeps_bundles_compact():
+    # nt_bundle_plan with blk_off: a bundle whose reads' planes lie more than
+    # 2 GiB apart goes to the per-read scan whole; the others stay bundles
+    nt = _nt(patterns="TTAGGG")
+    n = 96
+    ln = np.full(n, 50000, np.uint32)
+    blk = np.arange(n, dtype=np.uint64) * 1564
+    blk[40] = np.uint64(1) << 29  # 4 GiB: read 40's bundle (reads 32-63) spans too far
+    plan = nt.bundle_plan(ln, blk_off=blk)
+    assert plan.n_bundles == 2
+    assert np.array_equal(plan.list, np.arange(32, 64, dtype=np.uint32))
+    assert set(plan.bnd_read.tolist()) == set(range(32)) | set(range(64, 96))
+    plan = nt.bundle_plan(ln)  # no blk_off: the caller vouches
+    assert plan.n_bundles == 3 and len(plan.list) == 0
+
+
+# BASELINE.json configs[2], [3] (10M x 50 kb) and one GPU's shard of
+# configs[4] (12.5M x 50 kb, 156 GB of planes resident), bundle scan, and the
+# shard on the per-read scan: the bench's full-size batches, sampled against
+# the oracle on reads regenerated on the host (nt_synth_ascii) -- the first
+# and last reads (the last bundles: block offsets past 2^31) and reads spread
+# over the whole batch; every row field and every window count of every pass
+# (NanoTel.R:717-766, 1080-1155).
 FULL_CONFIGS = {  # patterns, TVRs, reads, variant rate, bundle path, read length
     "c3": ("YYAGGG", None, 10_000_000, 0.05, True, 50_000),
     "c4": ("TTAGGG TCAGGG", "TGAGGG TTGGGG", 10_000_000, 0.05, True, 50_000),
-    "c5_shard": ("TTAGGG", None, 12_500_000, 0.0, False, 50_000),
-    # the shard as bench.py runs it: the bundle copy for the reads whose copy fits
-    # beside the planes, the rest marked for the per-read scan (has_exc)
-    "c5_capped": ("TTAGGG", None, 12_500_000, 0.0, "capped", 50_000),
+    "c5": ("TTAGGG", None, 12_500_000, 0.0, True, 50_000),
+    "c5_per_read": ("TTAGGG", None, 12_500_000, 0.0, False, 50_000),
     "c10k": ("TTAGGG", None, 1_000_000, 0.0, True, 10_000),
 }
 
@@ -986,18 +1001,7 @@ def test_full_size_config_sampled_vs_oracle(name):
     t = _device_batch(nt, sp, n, read_len, hits=False)
     b = keep = None
     extra = np.zeros(0, np.int64)
-    if bundle == "capped":
-        torch.cuda.empty_cache()
-        free = torch.cuda.mem_get_info()[0]
-        aux = 64 * nt.n_pass * (t["rows"] // 64 + 2) * n
-        per = nt.bundle_plan(np.full(n, read_len, np.uint32)).tplane_bytes / n
-        k = int((free - aux - (4 << 30)) / per) // 32 * 32
-        assert 32 * 128 <= k < n, k
-        has_exc = np.zeros(n, np.uint8)
-        has_exc[k:] = 1
-        b, keep = _device_bundles(nt, t, n, read_len, has_exc)
-        extra = np.arange(k - 64, k + 64)  # both sides of the bundled / per-read boundary
-    elif bundle:
+    if bundle:
         b, keep = _device_bundles(nt, t, n, read_len)
     nt.scan_call_device(t["planes"].data_ptr(), t["blk_off"].data_ptr(), t["lens"].data_ptr(),
                         t["win_off"].data_ptr(), n, n * t["rows"], read_len, t["start"].data_ptr(),
@@ -1042,15 +1046,13 @@ def test_odd_block_offset_is_reported():
 @pytest.mark.parametrize("path", ["jit", "aot", "bundle"])
 def test_offsets_beyond_32_bits(path):
     # Batches of 10M x 50 kb reads have block offsets >= 2^31 and window
-    # offsets >= 2^32 (a sign-extended 32-bit block offset once faulted there),
-    # and their T-layout word offsets pass 2^32.  Reproduced without
-    # allocating them: the planes / window-count / T-layout base pointers are
-    # shifted down by exactly the offsets added to blk_off / win_off /
-    # bnd_stripe.  Bundle path: the bundle scan reads the shifted T-layout, the
-    # calling kernel the shifted planes.
+    # offsets >= 2^32 (a sign-extended 32-bit block offset once faulted there).
+    # Reproduced without allocating them: the planes / window-count base
+    # pointers are shifted down by exactly the offsets added to blk_off /
+    # win_off.  Bundle path: the bundle scan's descriptor base is its lowest
+    # read's planes, 2^34 bytes past the shifted base.
     import torch
     from nanotel_amd import synth_params
-    from nanotel_amd.api import DeviceBundles
     n, read_len = 64 if path != "bundle" else 96, 50000
     nt = _nt(jit=path != "aot", patterns="TTAGGG")
     t = _device_batch(nt, synth_params(read_len=read_len, first_read=77), n, read_len)
@@ -1063,13 +1065,7 @@ def test_offsets_beyond_32_bits(path):
     blk, win = t["blk_off"] + boff, t["win_off"] + woff
     bundles, keep = None, None
     if path == "bundle":
-        b, keep = _device_bundles(nt, t, n, read_len)
-        stripe_bytes = 50 * 64 * 16
-        soff = (1 << 35) // stripe_bytes + 1  # stripes: T-layout offsets past 2^35 bytes (2^33 words)
-        bs = keep["bnd_stripe"] + soff
-        bundles = DeviceBundles(b.tplanes - soff * stripe_bytes, b.bnd_read, bs.data_ptr(), b.n_bundles, 0, 0,
-                                b.tplane_bytes)
-        keep["bs_shift"] = bs
+        bundles, keep = _device_bundles(nt, t, n, read_len)
     nt.scan_call_device(t["planes"].data_ptr() - boff * 8, blk.data_ptr(), t["lens"].data_ptr(), win.data_ptr(),
                         n, woff + n * t["rows"], read_len, t["start"].data_ptr(), t["end"].data_ptr(),
                         t["dens"].data_ptr(), t["flags"].data_ptr(), t["wc"].data_ptr() - woff * nt.n_pass * nt.count_bytes,

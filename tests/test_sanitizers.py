@@ -1,6 +1,6 @@
 """AddressSanitizer + UndefinedBehaviorSanitizer over the host code that parses
 untrusted input (the FASTA/FASTQ(.gz) reader), the 2-bit packer, the host
-T-layout builder, serials / summary columns, and the CPU oracle (SURVEY §5:
+serials / summary columns, and the CPU oracle (SURVEY §5:
 race detection / sanitizers).  Builds tests/san/san_driver (g++ -fsanitize)
 and runs it; any sanitizer report fails the test."""
 import os

@@ -11,22 +11,13 @@ cat > "$out/t.hip" <<EOT
 using PatL = nt::CtList<$pats>;
 using TvrL = nt::CtList<$tvrs>;
 using JitT = nt::TProg<PatL, TvrL, $L>;
-#if NT_TS_WS
-extern "C" __global__ void __launch_bounds__(320) __attribute__((amdgpu_waves_per_eu(${WAVES:-2})))
-nt_tscan_jit(NtBatch B, NtOut O, uint64_t* __restrict__ tmask,
-             unsigned long long* __restrict__ queue, uint32_t thr_full) {
-  __shared__ uint32_t tsl[nt::ts_ws_lds_words<JitT::kNP>()];
-  nt::tscan_bundles_ws<JitT, PatL, TvrL>(B, O, tmask, queue, thr_full, tsl);
-}
-#else
 extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(${WAVES:-2})))
 nt_tscan_jit(NtBatch B, NtOut O, uint64_t* __restrict__ tmask,
              unsigned long long* __restrict__ queue, uint32_t thr_full) {
-  constexpr int kW = nt::ts_lds_words<JitT::kNP>();
+  constexpr int kW = nt::ts_lds_words<JitT::kNP, JitT::kL>();
   __shared__ uint32_t tsl[4 * kW];
   nt::tscan_bundles<JitT, PatL, TvrL>(B, O, tmask, queue, thr_full, tsl + (threadIdx.x >> 6) * kW);
 }
-#endif
 EOT
 cd "$out"
 /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off ${ISA_DEFS:-} -I"$here/telomere-analyzer_amd/csrc" \
