@@ -12,7 +12,11 @@ N GPUs: one process per GPU (torch.distributed, RCCL), each rank scans its own
 shard of reads (first_read = rank * reads) -> weak scaling, no data-path
 collective.  value = bases of all ranks / max-over-ranks time.
 
-python bench.py --gpus N --steps K --warmup W [--config c50k|c10k]
+python bench.py --gpus N --steps K --warmup W [--config c5|c50k|c10k|c3|c4]
+
+The default workload is c5: the 12.5M-read (50 kb) per-GPU shard of
+BASELINE.json configs[4] (100M reads over 8 GPUs), TTAGGG -- the
+configuration the headline metric is quoted on.
 """
 import argparse
 import json
@@ -43,7 +47,7 @@ CONFIGS = {
     "c4": dict(reads=10_000_000, read_len=50_000, patterns="TTAGGG TCAGGG", tvr="TGAGGG TTGGGG", rc=False,
                variant=0.05, desc="10M synthetic 50 kb reads / GPU, TTAGGG TCAGGG + TVR TGAGGG TTGGGG, P1+P2+P3"),
     # BASELINE.json configs[4]: 100M x 50 kb over 8 GPUs = 12.5M reads (625 Gbases,
-    # 156 GB of planes) resident per GPU, one launch per step
+    # 156 GB of planes) resident per GPU; the default workload
     "c5": dict(reads=12_500_000, read_len=50_000, patterns="TTAGGG", tvr=None, rc=False, variant=0.0,
                desc="12.5M synthetic 50 kb reads / GPU (100M over 8 GPUs), TTAGGG, P1 + P2"),
 }
@@ -137,7 +141,7 @@ def cpu_baseline(cfg, budget_s=12.0):
 class _ContigBuf:
     """A device buffer from hipExtMallocWithFlags(hipDeviceMallocContiguous):
     physically contiguous HBM, mapped with large pages.  The scans stream the
-    planes and the T-layout from 1,024 places at once; from torch's allocator
+    per-read planes from 1,024 places at once; from torch's allocator
     (hipMalloc) a box whose HBM is fragmented maps them with small pages and
     the bundle scan ran 1.53 ms a range instead of 1.38 (same box, same data;
     profiles/r04/contig/).  The library allocates its own buffers the same way."""
@@ -202,8 +206,8 @@ def _launch_ranks(n):
 
 
 # Environment variables that change WHAT a step computes or measures: timing
-# builds and skipped kernels (results wrong), or a T-layout path that no longer
-# exists.  bench.py refuses to run with any of them (a stray variable must not
+# builds and skipped kernels (results wrong), or paths (the T-layout copy, the
+# walker/writer split) that no longer exist.  bench.py refuses to run with any of them (a stray variable must not
 # give a fast, wrong, credited number); every other NT_* knob in the
 # environment is recorded in the line (config.env_knobs).
 REFUSED_PREFIXES = ("NT_DBG_", "NT_TS_DBG")
@@ -235,7 +239,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--config", default="c50k", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default="c5", choices=sorted(CONFIGS))
     ap.add_argument("--reads", type=int, default=0, help="override reads per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--per-read", action="store_true", help="per-read scan only (no bundle layout)")

@@ -382,6 +382,12 @@ int nt_synth_device(nt_ctx* ctx, const nt_synth_params* sp, uint64_t n_reads, ui
 int nt_uniform_layout_device(nt_ctx* ctx, uint64_t n_reads, uint64_t read_len, int32_t subseq_length,
                              uint64_t* blk_off_dev, uint32_t* len_dev, uint64_t* win_off_dev);
 int nt_synth_ascii(const nt_synth_params* sp, uint64_t read_index, char* out);
+/* --rc for a device-resident batch: planes_out read r = reverseComplement of
+ * planes_in read r (NanoTel.R:2219-2221), the same blk_off / len; out of place,
+ * asynchronous on the context stream.  Reads must be A/C/G/T only (a batch with
+ * non-ACGT letters takes the host packer, nt_pack_reads rc = 1). */
+int nt_rc_device(nt_ctx* ctx, const uint32_t* planes_in, uint32_t* planes_out, const uint64_t* blk_off_dev,
+                 const uint32_t* len_dev, uint64_t n_reads);
 
 #ifdef __cplusplus
 }

@@ -38,6 +38,8 @@ hipError_t nt_dev_launch_call(const NtProgram* prog, const NtBatch* B, const NtO
                               int long_tvr, int call_grid, hipStream_t stream);
 hipError_t nt_dev_launch_synth(const NtSynth* S, uint32_t* planes, uint64_t n_reads,
                                hipStream_t stream);
+hipError_t nt_dev_launch_rc(const uint32_t* in, uint32_t* out, const uint64_t* blk_off, const uint32_t* len,
+                            uint64_t n_reads, int cu_count, hipStream_t stream);
 hipError_t nt_dev_launch_filter(const NtProgram* prog, const NtBatch* B, uint8_t* keep,
                                 uint32_t thr_count, int right_edge, int grid, hipStream_t stream);
 hipError_t nt_dev_launch_uniform_layout(uint64_t n_reads, uint64_t nblk, uint64_t read_len,
@@ -1204,6 +1206,15 @@ int nt_synth_device(nt_ctx* ctx, const nt_synth_params* sp, uint64_t n_reads, ui
   const NtSynth S = to_synth(sp);
   hipError_t e = nt_dev_launch_synth(&S, planes_dev, n_reads, ctx->stream);
   return e == hipSuccess ? NT_OK : hip_fail(ctx, e, "launch nt_synth_kernel");
+}
+
+int nt_rc_device(nt_ctx* ctx, const uint32_t* planes_in, uint32_t* planes_out, const uint64_t* blk_off_dev,
+                 const uint32_t* len_dev, uint64_t n_reads) {
+  if (!ctx || (n_reads && (!planes_in || !planes_out || !blk_off_dev || !len_dev))) return NT_E_ARG;
+  if (planes_in == planes_out && n_reads) return fail(ctx, NT_E_ARG, "nt_rc_device is out of place");
+  (void)hipSetDevice(ctx->device);
+  const hipError_t e = nt_dev_launch_rc(planes_in, planes_out, blk_off_dev, len_dev, n_reads, ctx->cu_count, ctx->stream);
+  return e == hipSuccess ? NT_OK : hip_fail(ctx, e, "launch nt_rc_kernel");
 }
 
 int nt_uniform_layout_device(nt_ctx* ctx, uint64_t n_reads, uint64_t read_len, int32_t subseq_length,

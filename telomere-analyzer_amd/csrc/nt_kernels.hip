@@ -137,6 +137,42 @@ nt_layout_kernel(uint64_t n_reads, uint64_t nblk, uint64_t read_len, uint64_t nw
   }
 }
 
+// ================================================================ --rc
+//
+// reverseComplement(dna_reads) (NanoTel.R:2219-2221) of a device-resident
+// batch: out read r = the reverse complement of in read r, same block
+// offsets (out of place; the host path fuses it into the packer instead).
+// One wave per read (grid-stride), a lane per output plane word: new word j
+// = positions 32 j .. 32 j + 31 = old positions n - 1 - 32 j - i, i.e. the
+// 32 old bits from e = n - 32 j - 32 (a funnel of two old words, zero before
+// the read), bit-reversed; the complement flips both plane bits (A 00 <-> T
+// 11, C 01 <-> G 10).  Batches with non-ACGT letters take the host packer.
+__global__ void __launch_bounds__(256)
+nt_rc_kernel(const uint2* __restrict__ in, uint2* __restrict__ out, const uint64_t* __restrict__ blk_off,
+             const uint32_t* __restrict__ len, uint64_t n_reads) {
+  const int lane = threadIdx.x & 63;
+  for (uint64_t r = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < n_reads; r += (uint64_t)gridDim.x * 4) {
+    const int64_t n = len[r];
+    const uint64_t bo = blk_off[r];
+    const int64_t W = (n + 31) >> 5, WB = 2 * ((n + 63) >> 6);  // words of the read, of its blocks
+    for (int64_t j = lane; j < WB; j += 64) {
+      const int64_t e = n - 32 * j - 32;
+      const int64_t k = e >> 5;  // arithmetic: -1 for the last word of a read not a multiple of 32
+      const uint32_t sh = (uint32_t)(e & 31);
+      uint2 v = make_uint2(0u, 0u);  // the block padding past the read: zero, as the packer leaves it
+      if (j < W) {
+        const uint2 a = k >= 0 ? in[bo + k] : make_uint2(0u, 0u);
+        const uint2 b = k + 1 < W ? in[bo + k + 1] : make_uint2(0u, 0u);
+        const uint32_t lo = __builtin_amdgcn_alignbit(b.x, a.x, sh), hi = __builtin_amdgcn_alignbit(b.y, a.y, sh);
+        const int64_t m = n - 32 * j;  // positions of the word inside the read
+        const uint32_t keep = m >= 32 ? 0xFFFFFFFFu : (1u << m) - 1u;
+        v = make_uint2(~__builtin_bitreverse32(lo) & keep, ~__builtin_bitreverse32(hi) & keep);
+      }
+      out[bo + j] = v;
+    }
+  }
+}
+
 // ============================================================== filter
 //
 // --use_filter (filter_reads / filter_density, NanoTel.R:2083-2163): one lane
@@ -315,6 +351,16 @@ hipError_t nt_dev_launch_call(const NtProgram* prog, const NtBatch* B, const NtO
 
 hipError_t nt_dev_launch_combine(const NtBatch* B, const NtOut* O, int np, int grid, hipStream_t stream) {
   hipLaunchKernelGGL(nt::nt_call_combine_kernel, dim3(grid), dim3(256), 0, stream, *B, *O, np);
+  return hipGetLastError();
+}
+
+hipError_t nt_dev_launch_rc(const uint32_t* in, uint32_t* out, const uint64_t* blk_off, const uint32_t* len,
+                            uint64_t n_reads, int cu_count, hipStream_t stream) {
+  uint64_t grid = (n_reads + 3) / 4;
+  if (grid > (uint64_t)cu_count * 32) grid = (uint64_t)cu_count * 32;
+  if (grid == 0) return hipSuccess;
+  hipLaunchKernelGGL(nt::nt_rc_kernel, dim3((uint32_t)grid), dim3(256), 0, stream, reinterpret_cast<const uint2*>(in),
+                     reinterpret_cast<uint2*>(out), blk_off, len, n_reads);
   return hipGetLastError();
 }
 

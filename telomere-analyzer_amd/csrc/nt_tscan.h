@@ -932,10 +932,14 @@ __device__ __forceinline__ void tscan_bundles(const NtBatch& B, const NtOut& O, 
     }
     uint4 pf[St::kPer];  // the next half stripe's units
     auto fetch = [&](int hs) {
-      const uint32_t so = (uint32_t)(St::first_word(hs) * 8);  // (negative for hs 0: the range check zeroes it)
+      // (half stripe 0 starts 2 words before the reads: the range check does
+      // not wrap voffset + soffset, so that offset goes into voffset, where a
+      // slot at the descriptor base wraps past the range and loads zeros)
+      const int fw = St::first_word(hs);
+      const uint32_t so = fw < 0 ? 0u : (uint32_t)(fw * 8), vd = fw < 0 ? (uint32_t)(-fw * 8) : 0u;
 #pragma unroll
       for (int k = 0; k < St::kPer; ++k) {
-        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, vu[k], so, 0);
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, vu[k] - vd, so, 0);
         pf[k] = make_uint4(v[0], v[1], v[2], v[3]);
       }
     };
@@ -965,7 +969,8 @@ __device__ __forceinline__ void tscan_bundles(const NtBatch& B, const NtOut& O, 
           for (int t = 0; t < 8; ++t) x[t] = (uint32_t)__shfl_xor((int)acc[p][t], 32, kWave);
           bitsliced_add(acc[p], x);
 #pragma unroll
-          for (int t = 0; t < 8; ++t) oacc[p][t] = mh == (hs & 1) ? acc[p][t] : oacc[p][t];
+          for (int t = 0; t < 8; ++t)  // (an even half stripe clears the second half: none follows the last)
+            oacc[p][t] = mh == (hs & 1) ? acc[p][t] : ((hs & 1) ? oacc[p][t] : 0u);
         }
       }
       wave_sync();  // every lane's reads of the buffer are done before the next half stripe's writes

@@ -137,6 +137,7 @@ SIGNATURES = {
     "nt_reader_seek": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64]),
     "nt_reader_stats": (ctypes.c_int, [_P, _U64P]),
     "nt_synth_device": (ctypes.c_int, [_P, ctypes.POINTER(NtSynthParams), ctypes.c_uint64, _P]),
+    "nt_rc_device": (ctypes.c_int, [_P, _P, _P, _P, _P, ctypes.c_uint64]),
     "nt_uniform_layout_device": (ctypes.c_int, [_P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int32,
                                                 _P, _P, _P]),
     "nt_synth_ascii": (ctypes.c_int, [ctypes.POINTER(NtSynthParams), ctypes.c_uint64, ctypes.c_char_p]),

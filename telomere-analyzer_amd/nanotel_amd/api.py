@@ -304,6 +304,11 @@ class NanoTel:
     def synth_device(self, sp, n_reads, planes_ptr):
         _check(lib().nt_synth_device(self._h, ctypes.byref(sp), int(n_reads), planes_ptr), self._h)
 
+    def rc_device(self, planes_in, planes_out, blk_off_ptr, len_ptr, n_reads):
+        """nt_rc_device: planes_out = the reverse complement of every read of
+        planes_in (device pointers, same layout; A/C/G/T reads)."""
+        _check(lib().nt_rc_device(self._h, planes_in, planes_out, blk_off_ptr, len_ptr, int(n_reads)), self._h)
+
     def uniform_layout_device(self, n_reads, read_len, blk_off_ptr, len_ptr, win_off_ptr):
         _check(lib().nt_uniform_layout_device(self._h, int(n_reads), int(read_len), self.subseq_length,
                                               blk_off_ptr, len_ptr, win_off_ptr), self._h)

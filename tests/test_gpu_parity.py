@@ -958,6 +958,50 @@ def test_bundle_scan_ragged_packed_batch(L):
     assert int(((ref["flags"] & 1) != 0).sum()) > 5
 
 
+def test_rc_device_matches_host_packer():
+    # nt_rc_device (the --rc transform of a device-resident batch) against the
+    # host packer's fused reverse complement (nt_pack_reads rc = 1) on every
+    # plane word of ragged reads: lengths around word and block boundaries,
+    # the padding words of each read's blocks zero
+    import ctypes
+    import torch
+    from nanotel_amd import _lib
+    rng = np.random.default_rng(77)
+    lens_l = [1, 2, 31, 32, 33, 63, 64, 65, 95, 96, 97, 127, 128, 129, 1000, 4095, 4096, 4097, 50000]
+    lens_l += [int(x) for x in rng.integers(1, 20000, 45)]
+    seqs = [bytes(rng.choice(list(b"ACGT"), n).tolist()) for n in lens_l]
+    lib = _lib.lib()
+    n = len(seqs)
+    ptrs = (ctypes.c_char_p * n)(*seqs)
+    lens = np.array(lens_l, np.uint64)
+    tb, tw, te, ml, bad = (ctypes.c_uint64() for _ in range(5))
+    assert lib.nt_pack_count(ctypes.cast(ptrs, ctypes.c_void_p), lens.ctypes.data, n, 100, ctypes.byref(tb),
+                             ctypes.byref(tw), ctypes.byref(te), ctypes.byref(ml), ctypes.byref(bad)) == 0
+    packed = []
+    for rc in (0, 1):
+        planes = np.full(2 * tb.value + 2, 0x5A5A5A5A, np.uint32)
+        blk, ln, wo = np.zeros(n, np.uint64), np.zeros(n, np.uint32), np.zeros(n, np.uint64)
+        assert lib.nt_pack_reads(ctypes.cast(ptrs, ctypes.c_void_p), lens.ctypes.data, n, rc, 100,
+                                 planes.ctypes.data, blk.ctypes.data, ln.ctypes.data, wo.ctypes.data,
+                                 None, None, None) == 0
+        packed.append((planes, blk, ln))
+    (fwd, blk, ln), (want, blk1, _) = packed
+    assert np.array_equal(blk, blk1)
+    nt = _nt(patterns="TTAGGG")
+    d_in = torch.from_numpy(fwd.view(np.int32)).cuda()
+    d_out = torch.full_like(d_in, 0x3C3C3C3C)
+    d_blk = torch.from_numpy(blk.view(np.int64)).cuda()
+    d_len = torch.from_numpy(ln.view(np.int32)).cuda()
+    nt.rc_device(d_in.data_ptr(), d_out.data_ptr(), d_blk.data_ptr(), d_len.data_ptr(), n)
+    nt.synchronize()
+    got = d_out.cpu().numpy().view(np.uint32)
+    for r in range(n):
+        w0 = 2 * int(blk[r])
+        nwd = 2 * 2 * ((int(ln[r]) + 63) // 64)  # uint32 words of the read's blocks (lo, hi pairs)
+        assert np.array_equal(got[w0:w0 + nwd], want[w0:w0 + nwd]), (r, int(ln[r]))
+    nt.close()
+
+
 def test_bundle_plan_keeps_bundles_compact():
     # nt_bundle_plan with blk_off: a bundle whose reads' planes lie more than
     # 2 GiB apart goes to the per-read scan whole; the others stay bundles
@@ -981,13 +1025,38 @@ def test_bundle_plan_keeps_bundles_compact():
 # and last reads (the last bundles: block offsets past 2^31) and reads spread
 # over the whole batch; every row field and every window count of every pass
 # (NanoTel.R:717-766, 1080-1155).
-FULL_CONFIGS = {  # patterns, TVRs, reads, variant rate, bundle path, read length
-    "c3": ("YYAGGG", None, 10_000_000, 0.05, True, 50_000),
-    "c4": ("TTAGGG TCAGGG", "TGAGGG TTGGGG", 10_000_000, 0.05, True, 50_000),
-    "c5": ("TTAGGG", None, 12_500_000, 0.0, True, 50_000),
-    "c5_per_read": ("TTAGGG", None, 12_500_000, 0.0, False, 50_000),
-    "c10k": ("TTAGGG", None, 1_000_000, 0.0, True, 10_000),
+#
+# c3 is --rc: the reads are generated as they arrive (rc_layout: the telomere
+# is the reverse complement, at the far end) and turned into scan orientation
+# by the device reverse complement (nt_rc_device, chunks of 1M reads through a
+# scratch buffer) before the scan; the oracle reverse-complements its copy of
+# every sampled read (NanoTel.R:2219-2221).
+FULL_CONFIGS = {  # patterns, TVRs, reads, variant rate, bundle path, read length, --rc
+    "c3": ("YYAGGG", None, 10_000_000, 0.05, True, 50_000, True),
+    "c4": ("TTAGGG TCAGGG", "TGAGGG TTGGGG", 10_000_000, 0.05, True, 50_000, False),
+    "c5": ("TTAGGG", None, 12_500_000, 0.0, True, 50_000, False),
+    "c5_per_read": ("TTAGGG", None, 12_500_000, 0.0, False, 50_000, False),
+    "c10k": ("TTAGGG", None, 1_000_000, 0.0, True, 10_000, False),
 }
+
+
+def _rc_device_batch(nt, t, n, read_len, chunk=1_000_000):
+    """Reverse-complement every read of a uniform device batch in place, in
+    chunks through a scratch buffer (nt_rc_device is out of place)."""
+    import torch
+    from nanotel_amd import read_blocks
+    wpr = read_blocks(read_len) * 2  # int32 plane words a read
+    tmp = torch.empty(min(n, chunk) * wpr, dtype=torch.int32, device="cuda")
+    for r0 in range(0, n, chunk):
+        m = min(chunk, n - r0)
+        # the kernel writes read r at planes_out + blk_off[r] words: shift the
+        # scratch base back by the chunk's first read
+        nt.rc_device(t["planes"].data_ptr(), tmp.data_ptr() - r0 * wpr * 4, t["blk_off"].data_ptr() + 8 * r0,
+                     t["lens"].data_ptr() + 4 * r0, m)
+        nt.synchronize()
+        t["planes"][r0 * wpr:(r0 + m) * wpr].copy_(tmp[:m * wpr])
+    torch.cuda.synchronize()
+    del tmp
 
 
 @pytest.mark.timeout(600)
@@ -995,10 +1064,12 @@ FULL_CONFIGS = {  # patterns, TVRs, reads, variant rate, bundle path, read lengt
 def test_full_size_config_sampled_vs_oracle(name):
     import torch
     from nanotel_amd import synth_params, synth_read_ascii
-    pats, tvr, n, var, bundle, read_len = FULL_CONFIGS[name]
-    nt = _nt(patterns=pats, tvr_patterns=tvr)
-    sp = synth_params(read_len=read_len, first_read=0, variant_rate=var)
+    pats, tvr, n, var, bundle, read_len, rc = FULL_CONFIGS[name]
+    nt = _nt(patterns=pats, tvr_patterns=tvr, rc=rc)
+    sp = synth_params(read_len=read_len, first_read=0, variant_rate=var, rc_layout=rc)
     t = _device_batch(nt, sp, n, read_len, hits=False)
+    if rc:
+        _rc_device_batch(nt, t, n, read_len)
     b = keep = None
     extra = np.zeros(0, np.int64)
     if bundle:
@@ -1025,7 +1096,7 @@ def test_full_size_config_sampled_vs_oracle(name):
     del t, keep, it
     torch.cuda.empty_cache()
     seqs = [synth_read_ascii(sp, int(i)) for i in idx]
-    compare(nt, res, oracle_rows(seqs, pats, tvr=tvr, want_hits=False), check_hits=False)
+    compare(nt, res, oracle_rows(seqs, pats, tvr=tvr, rc=rc, want_hits=False), check_hits=False)
     assert res["telomeric"].sum() > idx.size // 4 and n_telo > n // 4
     nt.close()
 
