@@ -641,14 +641,16 @@ __device__ __forceinline__ void transpose32(uint32_t (&a)[32]) {
 // The half-stripe buffer: the planes of a bundle's 32 reads over a half
 // stripe (32 windows = 32 L positions = L plane words a read) plus a margin
 // of plane words on each side (the walks' halos and the 32-position ranges'
-// overhang), staged in LDS: slot s's words are row s, kTsRow words of 8 bytes.
+// overhang), staged in LDS: slot s's words are row s, kRow words of 8 bytes.
 // Row word j of half stripe hs is plane word hs L - 2 - (hs L & 1) + j of the
-// read (even, so that the 16-byte loads that fill it are aligned).
+// read (even, so that the 16-byte loads that fill it are aligned).  A row is
+// filled by kLoads 16-byte buffer loads straight into LDS (lane u = unit u of
+// the row's 64-unit piece c; the LDS address is the load's base + 16 lane).
 template <int kL>
 struct TsStage {
   static constexpr int kRow = 2 * ((kL + 7) / 2);         // plane words a row (>= L + 6, even)
-  static constexpr int kUnits = NT_BUNDLE * kRow / 2;     // 16-byte units of the buffer
-  static constexpr int kPer = (kUnits + kWave - 1) / kWave;  // of them a lane loads
+  static constexpr int kRowUnits = kRow / 2;              // 16-byte units a row
+  static constexpr int kLoads = (kRowUnits + kWave - 1) / kWave;  // loads a row
   static constexpr int kWords = NT_BUNDLE * kRow * 2;     // uint32 words of LDS
   __device__ __forceinline__ static int first_word(int hs) { return (hs * kL - 2) & ~1; }
 };
@@ -660,10 +662,13 @@ struct TsStage {
 // = 0 .. kN - 1 is position (32 hs + l) L + h L0 - kLam + i.  Per range of 32
 // positions: the pieces at the lane's bit offset of plane words (q, q + 1) of
 // every slot (LDS reads, v_alignbit), two 32 x 32 bit transposes in the
-// lane's registers, and the range's steps of the pipe.  Position -1 of the
-// first window (Biostrings' out-of-bound start) is masked in the prologue;
-// the read ends are not (the calling kernel recounts every read's last
-// window, see the header).
+// lane's registers, and the range's steps of the pipe.  The pieces of range
+// r + 1 are cut before range r is walked, so that the buffer is free once the
+// last range's are: issue() then starts the next half stripe's loads into it,
+// which land while the lane walks (for L <= 116, kNR = 2: the whole walk).
+// Position -1 of the first window (Biostrings' out-of-bound start) is masked
+// in the prologue; the read ends are not (the calling kernel recounts every
+// read's last window, see the header).
 template <class TP, class Pats, class Tvrs>
 struct TWalkerL {
   static constexpr int kL = TP::kL, kLam = TP::kLam;
@@ -671,25 +676,40 @@ struct TWalkerL {
   static constexpr int kN = kL0 + 2 * kLam;        // steps of a half-window walk
   static constexpr int kNR = (kN + 31) / 32;       // ranges of 32 positions
   static constexpr int kPro = 2 * kLam;            // prologue steps (no counts)
+  static constexpr int kIssueAt = kNR >= 2 ? kNR - 2 : 0;  // the range walked after the buffer's last read
   using St = TsStage<kL>;
   typename TPipeSel<TP, Pats, Tvrs>::type pp;
+
+  // range r's pieces of every slot: rows from the lane's word w (LDS)
+  template <int r>
+  __device__ __forceinline__ static void cut(const uint2* __restrict__ row, uint32_t sh, uint32_t (&lo)[32],
+                                             uint32_t (&hi)[32]) {
+#pragma unroll
+    for (int s = 0; s < NT_BUNDLE; ++s) {
+      const uint2 a = row[s * St::kRow + r], b = row[s * St::kRow + r + 1];
+      lo[s] = __builtin_amdgcn_alignbit(b.x, a.x, sh);
+      hi[s] = __builtin_amdgcn_alignbit(b.y, a.y, sh);
+    }
+  }
 
   // one half stripe: the counts of the lane's half window into acc.  buf: the
   // staged rows; w: the lane's first plane word, relative to the row start;
   // sh: its bit offset; first: the lane walks position -1 of the read;
-  // cmask: 0 when the lane's last counted step is past its window (odd L, h = 1)
+  // cmask: 0 when the lane's last counted step is past its window (odd L, h = 1);
+  // issue(): called once the buffer has been read
+  template <class Issue>
   __device__ __forceinline__ void walk(const uint2* __restrict__ buf, int w, uint32_t sh, bool first, uint32_t cmask,
-                                       uint32_t (&acc)[3][8]) {
+                                       uint32_t (&acc)[3][8], Issue&& issue) {
     pp.init();
+    const uint2* row = buf + w;
+    uint32_t plo[kNR][32], phi[kNR][32];
+    cut<0>(row, sh, plo[0], phi[0]);
     static_for<0, kNR>([&](auto ri) {
       constexpr int r = decltype(ri)::value;
-      uint32_t lo[32], hi[32];
-#pragma unroll
-      for (int s = 0; s < NT_BUNDLE; ++s) {
-        const uint2 a = buf[s * St::kRow + w + r], b = buf[s * St::kRow + w + r + 1];
-        lo[s] = __builtin_amdgcn_alignbit(b.x, a.x, sh);
-        hi[s] = __builtin_amdgcn_alignbit(b.y, a.y, sh);
-      }
+      if constexpr (r + 1 < kNR) cut<r + 1>(row, sh, plo[r + 1], phi[r + 1]);
+      if constexpr (r == kIssueAt) issue();
+      uint32_t (&lo)[32] = plo[r];
+      uint32_t (&hi)[32] = phi[r];
       transpose32(lo);
       transpose32(hi);
       // the range's steps in runs of at most 16 (the prologue's apart)
@@ -920,27 +940,32 @@ __device__ __forceinline__ void tscan_bundles(const NtBatch& B, const NtOut& O, 
     const int nst = (nhs + 1) / 2;                // output stripes of 64 windows
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint32_t*>(B.planes) + base * 2ull, (short)0, (int)(uint32_t)((top - base) * 8ull), 0x00020000);
-    // this lane's 16-byte units of the buffer: unit u = lane + 64 k = words
-    // (2 (u % kRow/2), +1) of slot u / (kRow/2); voffset = the slot's planes
-    // + the unit's place in the row (the half stripe's first word: soffset)
-    uint32_t vu[St::kPer];
-#pragma unroll
-    for (int k = 0; k < St::kPer; ++k) {
-      const int u = lane + kWave * k;
-      const int s = u / (St::kRow / 2), j = u % (St::kRow / 2);
-      vu[k] = u < St::kUnits ? sl[s].pad + 16u * (uint32_t)j : 0x80000000u;
-    }
-    uint4 pf[St::kPer];  // the next half stripe's units
+    // the buffer's loads: row s piece c <- 16-byte units 64 c + lane of slot s
+    // (lanes past the row's end idle), voffset = the slot's planes (bytes from
+    // the descriptor base, lane s of pad_v) + the unit, soffset = the half
+    // stripe's first word (half stripe 0 starts 2 words before the reads: the
+    // range check does not wrap voffset + soffset, so that offset goes into
+    // voffset, where a slot at the descriptor base wraps past the range and
+    // loads zeros)
+    const uint32_t pad_v = sl[lane & (NT_BUNDLE - 1)].pad;
+    // the buffer's LDS address, provably wave-uniform (the loads' M0)
+    const uint32_t stage_lds = (uint32_t)__builtin_amdgcn_readfirstlane(
+        (int)(uint32_t)(unsigned long)(__attribute__((address_space(3))) void*)stage);
     auto fetch = [&](int hs) {
-      // (half stripe 0 starts 2 words before the reads: the range check does
-      // not wrap voffset + soffset, so that offset goes into voffset, where a
-      // slot at the descriptor base wraps past the range and loads zeros)
       const int fw = St::first_word(hs);
-      const uint32_t so = fw < 0 ? 0u : (uint32_t)(fw * 8), vd = fw < 0 ? (uint32_t)(-fw * 8) : 0u;
+      const uint32_t so = fw < 0 ? 0u : (uint32_t)(fw * 8);
+      const uint32_t vl = 16u * (uint32_t)lane - (fw < 0 ? (uint32_t)(-fw * 8) : 0u);
 #pragma unroll
-      for (int k = 0; k < St::kPer; ++k) {
-        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, vu[k] - vd, so, 0);
-        pf[k] = make_uint4(v[0], v[1], v[2], v[3]);
+      for (int c = 0; c < St::kLoads; ++c) {
+        if (kWave * c + lane < St::kRowUnits) {
+#pragma unroll
+          for (int s = 0; s < NT_BUNDLE; ++s) {
+            const uint32_t pad = (uint32_t)__builtin_amdgcn_readlane((int)pad_v, s);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                rs, (__attribute__((address_space(3))) void*)(unsigned long)(stage_lds + 8u * (s * St::kRow + 2 * kWave * c)),
+                16, pad + 1024u * c + vl, so, 0, 0);
+          }
+        }
       }
     };
     fetch(0);
@@ -950,18 +975,20 @@ __device__ __forceinline__ void tscan_bundles(const NtBatch& B, const NtOut& O, 
 #pragma unroll
       for (int t = 0; t < 8; ++t) oacc[p][t] = 0u;
     for (int hs = 0; hs < nhs; ++hs) {
-      // ---- stage this half stripe, fetch the next
-#pragma unroll
-      for (int k = 0; k < St::kPer; ++k)
-        if (lane + kWave * k < St::kUnits) reinterpret_cast<uint4*>(stage)[lane + kWave * k] = pf[k];
-      if (hs + 1 < nhs) fetch(hs + 1);
-      wave_sync();
-      // ---- walk the half windows, add the halves
+      // ---- this half stripe's rows have landed (the loads write LDS and count as vmcnt)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // ---- walk the half windows (the next half stripe's loads start once
+      // the buffer has been read), add the halves
       {
-        const int w = wq - St::first_word(hs) + hs * kL;  // the lane's first word in the row
+        int w = wq - St::first_word(hs) + hs * kL;  // the lane's first word in the row
+        asm volatile("" : "+v"(w));  // (the row addresses are cut per half stripe, not held in registers)
         uint32_t acc[3][8];
         Wk wk;
-        wk.walk(stage, w, sh, hs == 0 && lane == 0, cmask, acc);
+        wk.walk(stage, w, sh, hs == 0 && lane == 0, cmask, acc, [&]() {
+          // (every read of the buffer has returned before a load may write it)
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          if (hs + 1 < nhs) fetch(hs + 1);
+        });
 #pragma unroll
         for (int p = 0; p < kNP; ++p) {
           uint32_t x[8];
@@ -973,7 +1000,6 @@ __device__ __forceinline__ void tscan_bundles(const NtBatch& B, const NtOut& O, 
             oacc[p][t] = mh == (hs & 1) ? acc[p][t] : ((hs & 1) ? oacc[p][t] : 0u);
         }
       }
-      wave_sync();  // every lane's reads of the buffer are done before the next half stripe's writes
       if (!(hs & 1) && hs + 1 < nhs) continue;
       const int st = hs >> 1;
       uint32_t (&acc)[3][8] = oacc;

@@ -11,12 +11,13 @@ cat > "$out/t.hip" <<EOT
 using PatL = nt::CtList<$pats>;
 using TvrL = nt::CtList<$tvrs>;
 using JitT = nt::TProg<PatL, TvrL, $L>;
-extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(${WAVES:-2})))
+constexpr int kTsW = nt::ts_lds_words<JitT::kNP, JitT::kL>();
+constexpr int kTsNW = 40960 / kTsW < 4 ? 40960 / kTsW : 4;
+extern "C" __global__ void __launch_bounds__(kTsNW * 64) __attribute__((amdgpu_waves_per_eu(1)))
 nt_tscan_jit(NtBatch B, NtOut O, uint64_t* __restrict__ tmask,
              unsigned long long* __restrict__ queue, uint32_t thr_full) {
-  constexpr int kW = nt::ts_lds_words<JitT::kNP, JitT::kL>();
-  __shared__ uint32_t tsl[4 * kW];
-  nt::tscan_bundles<JitT, PatL, TvrL>(B, O, tmask, queue, thr_full, tsl + (threadIdx.x >> 6) * kW);
+  __shared__ uint32_t tsl[kTsNW * kTsW];
+  nt::tscan_bundles<JitT, PatL, TvrL>(B, O, tmask, queue, thr_full, tsl + (threadIdx.x >> 6) * kTsW);
 }
 EOT
 cd "$out"
