@@ -682,14 +682,34 @@ struct TWalkerL {
 
   // range r's pieces of every slot: rows from the lane's word w (LDS)
   template <int r>
-  __device__ __forceinline__ static void cut(const uint2* __restrict__ row, uint32_t sh, uint32_t (&lo)[32],
+  __device__ __forceinline__ static void cut(const uint2* row, uint32_t sh, uint32_t (&lo)[32],
                                              uint32_t (&hi)[32]) {
+    // (volatile: one ds_read_b64 a word -- two accesses of 32 lanes, 256 B a
+    // clock -- where the compiler would pair a word with its neighbour into a
+    // ds_read2_b64, which the LDS serves at half that rate)
+    typedef const volatile __attribute__((address_space(3))) uint64_t lds_u64;
+    lds_u64* vr = (lds_u64*)(row);
 #pragma unroll
     for (int s = 0; s < NT_BUNDLE; ++s) {
-      const uint2 a = row[s * St::kRow + r], b = row[s * St::kRow + r + 1];
-      lo[s] = __builtin_amdgcn_alignbit(b.x, a.x, sh);
-      hi[s] = __builtin_amdgcn_alignbit(b.y, a.y, sh);
+      const uint64_t a = vr[s * St::kRow + r], b = vr[s * St::kRow + r + 1];
+      lo[s] = __builtin_amdgcn_alignbit((uint32_t)b, (uint32_t)a, sh);
+      hi[s] = __builtin_amdgcn_alignbit((uint32_t)(b >> 32), (uint32_t)(a >> 32), sh);
     }
+  }
+
+  // the first run (of the at most 4 a range's steps split into: prologue /
+  // counted, 16 steps at most) of range r that has steps
+  template <int r>
+  static constexpr int first_run() {
+    const int a = 32 * r, b = 32 * r + 32 < kN ? 32 * r + 32 : kN;
+    for (int q = 0; q < 4; ++q) {
+      const int m0 = a + 16 * (q >> 1), m1 = a + 16 * (q >> 1) + 16 < b ? a + 16 * (q >> 1) + 16 : b;
+      const bool pro = !(q & 1);
+      const int u0 = pro ? m0 : (m0 > kPro ? m0 : kPro);
+      const int u1 = pro ? (m1 < kPro ? m1 : kPro) : m1;
+      if (u1 > u0) return q;
+    }
+    return 0;
   }
 
   // one half stripe: the counts of the lane's half window into acc.  buf: the
@@ -698,7 +718,7 @@ struct TWalkerL {
   // cmask: 0 when the lane's last counted step is past its window (odd L, h = 1);
   // issue(): called once the buffer has been read
   template <class Issue>
-  __device__ __forceinline__ void walk(const uint2* __restrict__ buf, int w, uint32_t sh, bool first, uint32_t cmask,
+  __device__ __forceinline__ void walk(const uint2* buf, int w, uint32_t sh, bool first, uint32_t cmask,
                                        uint32_t (&acc)[3][8], Issue&& issue) {
     pp.init();
     const uint2* row = buf + w;
@@ -707,7 +727,6 @@ struct TWalkerL {
     static_for<0, kNR>([&](auto ri) {
       constexpr int r = decltype(ri)::value;
       if constexpr (r + 1 < kNR) cut<r + 1>(row, sh, plo[r + 1], phi[r + 1]);
-      if constexpr (r == kIssueAt) issue();
       uint32_t (&lo)[32] = plo[r];
       uint32_t (&hi)[32] = phi[r];
       transpose32(lo);
@@ -734,6 +753,9 @@ struct TWalkerL {
           pp.bc[1].pin();
           if constexpr (TP::kNP == 3) pp.bc[2].pin();
           __builtin_amdgcn_sched_barrier(0);
+          // the buffer's last reads returned under this run: start the next
+          // half stripe's loads into it
+          if constexpr (q == first_run<r>() && r == kIssueAt) issue();
         }
       });
     });
@@ -955,16 +977,19 @@ __device__ __forceinline__ void tscan_bundles(const NtBatch& B, const NtOut& O, 
       const int fw = St::first_word(hs);
       const uint32_t so = fw < 0 ? 0u : (uint32_t)(fw * 8);
       const uint32_t vl = 16u * (uint32_t)lane - (fw < 0 ? (uint32_t)(-fw * 8) : 0u);
+      // (the slots' offsets are read with every lane active: a lane the load's
+      // mask leaves out has no defined value to read)
+      uint32_t pad[NT_BUNDLE];
+#pragma unroll
+      for (int s = 0; s < NT_BUNDLE; ++s) pad[s] = (uint32_t)__builtin_amdgcn_readlane((int)pad_v, s);
 #pragma unroll
       for (int c = 0; c < St::kLoads; ++c) {
         if (kWave * c + lane < St::kRowUnits) {
 #pragma unroll
-          for (int s = 0; s < NT_BUNDLE; ++s) {
-            const uint32_t pad = (uint32_t)__builtin_amdgcn_readlane((int)pad_v, s);
+          for (int s = 0; s < NT_BUNDLE; ++s)
             __builtin_amdgcn_raw_ptr_buffer_load_lds(
                 rs, (__attribute__((address_space(3))) void*)(unsigned long)(stage_lds + 8u * (s * St::kRow + 2 * kWave * c)),
-                16, pad + 1024u * c + vl, so, 0, 0);
-          }
+                16, pad[s] + 1024u * c + vl, so, 0, 0);
         }
       }
     };
@@ -975,7 +1000,8 @@ __device__ __forceinline__ void tscan_bundles(const NtBatch& B, const NtOut& O, 
 #pragma unroll
       for (int t = 0; t < 8; ++t) oacc[p][t] = 0u;
     for (int hs = 0; hs < nhs; ++hs) {
-      // ---- this half stripe's rows have landed (the loads write LDS and count as vmcnt)
+      // ---- this half stripe's rows have landed (the loads write LDS and
+      // count as vmcnt)
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       // ---- walk the half windows (the next half stripe's loads start once
       // the buffer has been read), add the halves
@@ -984,11 +1010,13 @@ __device__ __forceinline__ void tscan_bundles(const NtBatch& B, const NtOut& O, 
         asm volatile("" : "+v"(w));  // (the row addresses are cut per half stripe, not held in registers)
         uint32_t acc[3][8];
         Wk wk;
-        wk.walk(stage, w, sh, hs == 0 && lane == 0, cmask, acc, [&]() {
-          // (every read of the buffer has returned before a load may write it)
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          if (hs + 1 < nhs) fetch(hs + 1);
-        });
+        wk.walk(
+            stage, w, sh, hs == 0 && lane == 0, cmask, acc,
+            [&]() {
+              // (every read of the buffer has returned before a load may write it)
+              asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+              if (hs + 1 < nhs) fetch(hs + 1);
+            });
 #pragma unroll
         for (int p = 0; p < kNP; ++p) {
           uint32_t x[8];
