@@ -859,6 +859,13 @@ __device__ __forceinline__ uint64_t u64of(uint32_t lo, uint32_t hi) { return ((u
 constexpr uint32_t kTsSpanError = 0xFFFFFFFFu;
 constexpr uint64_t kTsMaxSpan = 0x7FFFFFF0ull;  // bytes
 
+// x of lane ^ 32: one v_permlane32_swap (a VALU op: the two halves of x
+// trade places) where __shfl_xor is a ds_bpermute through the LDS
+__device__ __forceinline__ uint32_t xor32(uint32_t x, bool lower) {
+  const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+  return lower ? r[1] : r[0];
+}
+
 __device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
   const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m, kWave);
   const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m, kWave);
@@ -1021,7 +1028,7 @@ __device__ __forceinline__ void tscan_bundles(const NtBatch& B, const NtOut& O, 
         for (int p = 0; p < kNP; ++p) {
           uint32_t x[8];
 #pragma unroll
-          for (int t = 0; t < 8; ++t) x[t] = (uint32_t)__shfl_xor((int)acc[p][t], 32, kWave);
+          for (int t = 0; t < 8; ++t) x[t] = xor32(acc[p][t], mh == 0);
           bitsliced_add(acc[p], x);
 #pragma unroll
           for (int t = 0; t < 8; ++t)  // (an even half stripe clears the second half: none follows the last)
@@ -1097,7 +1104,7 @@ __device__ __forceinline__ void tscan_bundles(const NtBatch& B, const NtOut& O, 
         gb = __builtin_amdgcn_udot4(vb.z, 0x01010101u, gb, false);
         gb = __builtin_amdgcn_udot4(vb.w, 0x01010101u, gb, false);
         const uint32_t mine = ga + gb;
-        const uint32_t other = (uint32_t)__shfl_xor((int)mine, 32, kWave);
+        const uint32_t other = xor32(mine, mh == 0);
         const uint32_t run = mt.run[p];
         const uint32_t c0 = run + (mh ? other : 0u);  // before window k0
         uint32_t* ckr = ckb + (p * NT_BUNDLE + ms) * 4 * Aux::kF + 4 * fs + 2 * mh;
