@@ -697,6 +697,21 @@ struct TWalkerL {
     }
   }
 
+  // both ranges' pieces of every slot (kNR = 2): plane words w, w + 1, w + 2
+  __device__ __forceinline__ static void cut2(const uint2* row, uint32_t sh, uint32_t (&lo)[kNR][32],
+                                              uint32_t (&hi)[kNR][32]) {
+    typedef const volatile __attribute__((address_space(3))) uint64_t lds_u64;
+    lds_u64* vr = (lds_u64*)(row);
+#pragma unroll
+    for (int s = 0; s < NT_BUNDLE; ++s) {
+      const uint64_t a = vr[s * St::kRow], b = vr[s * St::kRow + 1], c = vr[s * St::kRow + 2];
+      lo[0][s] = __builtin_amdgcn_alignbit((uint32_t)b, (uint32_t)a, sh);
+      hi[0][s] = __builtin_amdgcn_alignbit((uint32_t)(b >> 32), (uint32_t)(a >> 32), sh);
+      lo[1][s] = __builtin_amdgcn_alignbit((uint32_t)c, (uint32_t)b, sh);
+      hi[1][s] = __builtin_amdgcn_alignbit((uint32_t)(c >> 32), (uint32_t)(b >> 32), sh);
+    }
+  }
+
   // the first run (of the at most 4 a range's steps split into: prologue /
   // counted, 16 steps at most) of range r that has steps
   template <int r>
@@ -723,10 +738,14 @@ struct TWalkerL {
     pp.init();
     const uint2* row = buf + w;
     uint32_t plo[kNR][32], phi[kNR][32];
-    cut<0>(row, sh, plo[0], phi[0]);
+    if constexpr (kNR == 2) {
+      cut2(row, sh, plo, phi);  // (both ranges from the 3 words they span: a quarter fewer reads)
+    } else {
+      cut<0>(row, sh, plo[0], phi[0]);
+    }
     static_for<0, kNR>([&](auto ri) {
       constexpr int r = decltype(ri)::value;
-      if constexpr (r + 1 < kNR) cut<r + 1>(row, sh, plo[r + 1], phi[r + 1]);
+      if constexpr (kNR != 2 && r + 1 < kNR) cut<r + 1>(row, sh, plo[r + 1], phi[r + 1]);
       uint32_t (&lo)[32] = plo[r];
       uint32_t (&hi)[32] = phi[r];
       transpose32(lo);
@@ -1001,6 +1020,11 @@ __device__ __forceinline__ void tscan_bundles(const NtBatch& B, const NtOut& O, 
       }
     };
     fetch(0);
+    // this lane's slot (ms) of the output stage: windows, aux base, and the
+    // covered bases of the windows before the stripe, per pass (both halves)
+    const int m_nw = (int)sl[ms].nw;
+    const uint64_t m_ab = u64of(sl[ms].ab_lo, sl[ms].ab_hi);
+    uint32_t run[3] = {0u, 0u, 0u};
     uint32_t oacc[3][8];  // the output stripe's counts: lane l + 32 h = window 32 (2 st + h) + l
 #pragma unroll
     for (int p = 0; p < 3; ++p)
@@ -1044,15 +1068,15 @@ __device__ __forceinline__ void tscan_bundles(const NtBatch& B, const NtOut& O, 
       // per slot), and at lane 32 h + s (windows 32 h ..) for the checkpoint
       // sums; the telomeric bits come from a bit-sliced compare and a bit
       // transpose.  Bitmask words and checkpoints wait in LDS for the flush.
-      const TSlot& mt = sl[ms];
-      const int m_nw = (int)mt.nw;
+      // Every pass's rows are written before one wave_sync and read back
+      // after it (one LDS round trip a stripe, not one a pass).
       const int k0 = st * kWave + 32 * mh;  // this lane's first window
       const int nv = m_nw - k0 < 0 ? 0 : (m_nw - k0 > 32 ? 32 : m_nw - k0);  // its windows in the read
       const int fs = st % Aux::kF;          // the stripe's place in the flush buffers
+      const int half = (st & 1) * 16;       // this stripe's 16 words of a row
 #pragma unroll
       for (int p = 0; p < kNP; ++p) {
         uint32_t* ctp = ct + p * NT_BUNDLE * 32;  // this pass's rows
-        const int half = (st & 1) * 16;            // this stripe's 16 words of a row
         uint32_t W[8];
 #pragma unroll
         for (int t = 0; t < 8; ++t) W[t] = acc[p][t];
@@ -1072,11 +1096,15 @@ __device__ __forceinline__ void tscan_bundles(const NtBatch& B, const NtOut& O, 
         for (int j = 0; j < 8; ++j) ctp[(8 * (lane & 3) + j) * 32 + half + (lane >> 2)] = W[j];
         const uint32_t tb = half_bit_transpose(ge, lane) & (nv >= 32 ? ~0u : ((1u << nv) - 1u));
         tmb[((p * NT_BUNDLE + ms) * Aux::kF + fs) * 2 + mh] = tb;
-        wave_sync();
-        // window counts (uint8: L <= 170), every second stripe: the rows' 128
-        // windows as whole lines, store c covers slots 8 c .. 8 c + 7, lane 8 i +
-        // q = the 16 bytes (windows 16 q ..) of slot 8 c + i
-        if ((st & 1) || st == nst - 1) {
+      }
+      wave_sync();
+      // window counts (uint8: L <= 170), every second stripe: the rows' 128
+      // windows as whole lines, store c covers slots 8 c .. 8 c + 7, lane 8 i +
+      // q = the 16 bytes (windows 16 q ..) of slot 8 c + i
+      if ((st & 1) || st == nst - 1) {
+#pragma unroll
+        for (int p = 0; p < kNP; ++p) {
+          const uint32_t* ctp = ct + p * NT_BUNDLE * 32;
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
             const int s = 8 * c + (lane >> 3), q = lane & 7, kq = (st >> 1) * 2 * kWave + 16 * q;
@@ -1091,6 +1119,10 @@ __device__ __forceinline__ void tscan_bundles(const NtBatch& B, const NtOut& O, 
             }
           }
         }
+      }
+#pragma unroll
+      for (int p = 0; p < kNP; ++p) {
+        const uint32_t* ctp = ct + p * NT_BUNDLE * 32;
         // checkpoints: covered bases before windows 16 jj, jj = 4 st + g
         const uint4 va = *reinterpret_cast<const uint4*>(ctp + ms * 32 + half + 8 * mh);
         const uint4 vb = *reinterpret_cast<const uint4*>(ctp + ms * 32 + half + 8 * mh + 4);
@@ -1105,18 +1137,16 @@ __device__ __forceinline__ void tscan_bundles(const NtBatch& B, const NtOut& O, 
         gb = __builtin_amdgcn_udot4(vb.w, 0x01010101u, gb, false);
         const uint32_t mine = ga + gb;
         const uint32_t other = xor32(mine, mh == 0);
-        const uint32_t run = mt.run[p];
-        const uint32_t c0 = run + (mh ? other : 0u);  // before window k0
+        const uint32_t c0 = run[p] + (mh ? other : 0u);  // before window k0
         uint32_t* ckr = ckb + (p * NT_BUNDLE + ms) * 4 * Aux::kF + 4 * fs + 2 * mh;
         ckr[0] = c0;
         ckr[1] = c0 + ga;
         // the read's total when its windows end with the bundle's last stripe
         // (no later stripe holds that checkpoint)
         if (mh && st == nst - 1 && 16 * ((k0 >> 4) + 2) == m_nw)
-          reinterpret_cast<uint32_t*>(tmask + u64of(mt.ab_lo, mt.ab_hi) + (uint64_t)kNP * aux_nmw(m_nw))[
-              p * aux_nck(m_nw) + (m_nw >> 4)] = c0 + mine;
-        wave_sync();  // every lane has read ct and run[p]
-        if (mh == 0) sl[ms].run[p] = run + mine + other;
+          reinterpret_cast<uint32_t*>(tmask + m_ab + (uint64_t)kNP * aux_nmw(m_nw))[p * aux_nck(m_nw) + (m_nw >> 4)] =
+              c0 + mine;
+        run[p] += mine + other;
       }
       // ---- flush the bitmask words and checkpoints of stripes st0 .. st
       // lane -> (slot, stripe) / (slot, checkpoint): coalesced runs of each
