@@ -1101,20 +1101,26 @@ __device__ __forceinline__ void tscan_bundles(const NtBatch& B, const NtOut& O, 
       // window counts (uint8: L <= 170), every second stripe: the rows' 128
       // windows as whole lines, store c covers slots 8 c .. 8 c + 7, lane 8 i +
       // q = the 16 bytes (windows 16 q ..) of slot 8 c + i
+      // (every LDS read first, then the stores: one round trip, not one a store)
       if ((st & 1) || st == nst - 1) {
+        uint4 m[4], x[kNP][4];
 #pragma unroll
-        for (int p = 0; p < kNP; ++p) {
-          const uint32_t* ctp = ct + p * NT_BUNDLE * 32;
+        for (int c = 0; c < 4; ++c) {
+          const int s = 8 * c + (lane >> 3), q = lane & 7;
+          m[c] = *reinterpret_cast<const uint4*>(sl + s);  // nw, wb_lo, wb_hi
 #pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            const int s = 8 * c + (lane >> 3), q = lane & 7, kq = (st >> 1) * 2 * kWave + 16 * q;
-            const uint4 m = *reinterpret_cast<const uint4*>(sl + s);  // nw, wb_lo, wb_hi
-            const uint4 x = *reinterpret_cast<const uint4*>(ctp + s * 32 + 4 * q);
-            if (kq < (int)m.x) {
-              uint8_t* w = reinterpret_cast<uint8_t*>(O.win_counts) + u64of(m.y, m.z) +
-                           (uint64_t)p * NT_WIN_ROWS((uint64_t)m.x) + kq;
+          for (int p = 0; p < kNP; ++p) x[p][c] = *reinterpret_cast<const uint4*>(ct + p * NT_BUNDLE * 32 + s * 32 + 4 * q);
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int kq = (st >> 1) * 2 * kWave + 16 * (lane & 7);
+          if (kq < (int)m[c].x) {
+#pragma unroll
+            for (int p = 0; p < kNP; ++p) {
+              uint8_t* w = reinterpret_cast<uint8_t*>(O.win_counts) + u64of(m[c].y, m[c].z) +
+                           (uint64_t)p * NT_WIN_ROWS((uint64_t)m[c].x) + kq;
               typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-              const u32x4 vv = {x.x, x.y, x.z, x.w};
+              const u32x4 vv = {x[p][c].x, x[p][c].y, x[p][c].z, x[p][c].w};
               __builtin_nontemporal_store(vv, reinterpret_cast<u32x4*>(w));  // (-6 % scan time)
             }
           }
@@ -1157,40 +1163,47 @@ __device__ __forceinline__ void tscan_bundles(const NtBatch& B, const NtOut& O, 
         wave_sync();
         const int st0 = st - fs;
         constexpr int kI1 = NT_BUNDLE * Aux::kF / kWave, kI2 = NT_BUNDLE * 4 * Aux::kF / kWave;
+        // every LDS read of every pass first (slot metadata once), then the stores
+        uint32_t n1[kI1], n2[kI2], c2[kNP][kI2];
+        uint2 a1[kI1], a2[kI2];
+        uint64_t v1[kNP][kI1];
 #pragma unroll
-        for (int p = 0; p < kNP; ++p) {
-          uint32_t n1[kI1], n2[kI2], c2[kI2];
-          uint2 a1[kI1], a2[kI2];
-          uint64_t v1[kI1];
+        for (int i = 0; i < kI1; ++i) {
+          const int e = i * kWave + lane, s = e / Aux::kF, w = e % Aux::kF;
+          const uint32_t* ts = reinterpret_cast<const uint32_t*>(sl + s);
+          n1[i] = ts[0];
+          a1[i] = *reinterpret_cast<const uint2*>(ts + 4);
 #pragma unroll
-          for (int i = 0; i < kI1; ++i) {
-            const int e = i * kWave + lane, s = e / Aux::kF, w = e % Aux::kF;
-            const uint32_t* ts = reinterpret_cast<const uint32_t*>(sl + s);
-            n1[i] = ts[0];
-            a1[i] = *reinterpret_cast<const uint2*>(ts + 4);
-            v1[i] = *reinterpret_cast<const uint64_t*>(tmb + ((p * NT_BUNDLE + s) * Aux::kF + w) * 2);
+          for (int p = 0; p < kNP; ++p)
+            v1[p][i] = *reinterpret_cast<const uint64_t*>(tmb + ((p * NT_BUNDLE + s) * Aux::kF + w) * 2);
+        }
+#pragma unroll
+        for (int i = 0; i < kI2; ++i) {
+          const int e = i * kWave + lane, s = e / (4 * Aux::kF), g = e % (4 * Aux::kF);
+          const uint32_t* ts = reinterpret_cast<const uint32_t*>(sl + s);
+          n2[i] = ts[0];
+          a2[i] = *reinterpret_cast<const uint2*>(ts + 4);
+#pragma unroll
+          for (int p = 0; p < kNP; ++p) c2[p][i] = ckb[(p * NT_BUNDLE + s) * 4 * Aux::kF + g];
+        }
+#pragma unroll
+        for (int i = 0; i < kI1; ++i) {
+          const int e = i * kWave + lane, w = e % Aux::kF, sw = st0 + w;
+          const int nw = (int)n1[i];
+          if (w <= fs && sw * kWave < nw) {
+#pragma unroll
+            for (int p = 0; p < kNP; ++p) tmask[u64of(a1[i].x, a1[i].y) + (uint64_t)p * aux_nmw(nw) + sw] = v1[p][i];
           }
+        }
 #pragma unroll
-          for (int i = 0; i < kI2; ++i) {
-            const int e = i * kWave + lane, s = e / (4 * Aux::kF), g = e % (4 * Aux::kF);
-            const uint32_t* ts = reinterpret_cast<const uint32_t*>(sl + s);
-            n2[i] = ts[0];
-            a2[i] = *reinterpret_cast<const uint2*>(ts + 4);
-            c2[i] = ckb[(p * NT_BUNDLE + s) * 4 * Aux::kF + g];
-          }
+        for (int i = 0; i < kI2; ++i) {
+          const int e = i * kWave + lane, g = e % (4 * Aux::kF), jj = 4 * st0 + g;
+          const int nw = (int)n2[i];
+          if (g < 4 * (fs + 1) && nw > 0 && 16 * jj <= nw) {
 #pragma unroll
-          for (int i = 0; i < kI1; ++i) {
-            const int e = i * kWave + lane, w = e % Aux::kF, sw = st0 + w;
-            const int nw = (int)n1[i];
-            if (w <= fs && sw * kWave < nw) tmask[u64of(a1[i].x, a1[i].y) + (uint64_t)p * aux_nmw(nw) + sw] = v1[i];
-          }
-#pragma unroll
-          for (int i = 0; i < kI2; ++i) {
-            const int e = i * kWave + lane, g = e % (4 * Aux::kF), jj = 4 * st0 + g;
-            const int nw = (int)n2[i];
-            if (g < 4 * (fs + 1) && nw > 0 && 16 * jj <= nw)
+            for (int p = 0; p < kNP; ++p)
               reinterpret_cast<uint32_t*>(tmask + u64of(a2[i].x, a2[i].y) + (uint64_t)kNP * aux_nmw(nw))[
-                  p * aux_nck(nw) + jj] = c2[i];
+                  p * aux_nck(nw) + jj] = c2[p][i];
           }
         }
         wave_sync();
