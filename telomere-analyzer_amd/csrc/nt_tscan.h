@@ -834,21 +834,22 @@ struct TSlot {
 constexpr int kTsSlotWords = 12;
 
 // per-wave LDS of the bundle scan (uint32 words): the slots; the count rows
-// of two stripes per pass (row s = slot s, 32 words = 128 windows, 4 to a
-// word: byte b = window 4 q + b of word q -- the uint8 counts, stored as
-// whole 128-byte lines every second stripe); and the telomeric bitmask words
-// / checkpoints of kF stripes, written out together (whole runs of a read's
-// row instead of 4-byte pieces: a partly written line costs a
-// read-modify-write in the memory system).  22.5 KB at most: one workgroup
-// per CU (the scan runs at one wave per SIMD) leaves room for two of the
-// calling kernel's beside it.
+// of kRS stripes per pass (row s = slot s, 16 kRS words = 64 kRS windows, 4 to a
+// word: byte b = window 4 q + b of word q -- the uint8 counts, stored as whole
+// 128-byte lines every second stripe for 2 passes; a 3-pass program stores
+// 64-byte halves every stripe, which keeps its LDS under the 40 KB of four
+// waves per CU); and the telomeric bitmask words / checkpoints of kF stripes,
+// written out together (whole runs of a read's row instead of 4-byte pieces: a
+// partly written line costs a read-modify-write in the memory system).
 constexpr int kTsFlush2 = 2;  // stripes per flush of a 2-pass program (even; LDS: the half-stripe buffer)
 constexpr int kTsFlush3 = 2;  // ... of a 3-pass program
 template <int kNP>
 struct TsAux {
   static constexpr int kF = kNP == 3 ? kTsFlush3 : kTsFlush2;  // stripes per flush (even)
   static_assert(kF >= 2 && kF % 2 == 0, "flush depth");
-  static constexpr int kCtWords = kNP * NT_BUNDLE * 32;       // [p][s][2 stripes x 16 words]
+  static constexpr int kRS = kNP == 3 ? 1 : 2;                 // stripes of count rows
+  static constexpr int kRow = 16 * kRS;                         // words of a count row
+  static constexpr int kCtWords = kNP * NT_BUNDLE * kRow;      // [p][s][kRS stripes x 16 words]
   static constexpr int kTmWords = kNP * NT_BUNDLE * kF * 2;   // [p][s][stripe] u64
   static constexpr int kCkWords = kNP * NT_BUNDLE * 4 * kF;   // [p][s][4 stripe + g] u32
   static constexpr int kWords = kCtWords + kTmWords + kCkWords;
@@ -1073,10 +1074,10 @@ __device__ __forceinline__ void tscan_bundles(const NtBatch& B, const NtOut& O, 
       const int k0 = st * kWave + 32 * mh;  // this lane's first window
       const int nv = m_nw - k0 < 0 ? 0 : (m_nw - k0 > 32 ? 32 : m_nw - k0);  // its windows in the read
       const int fs = st % Aux::kF;          // the stripe's place in the flush buffers
-      const int half = (st & 1) * 16;       // this stripe's 16 words of a row
+      const int half = (st % Aux::kRS) * 16;  // this stripe's 16 words of a row
 #pragma unroll
       for (int p = 0; p < kNP; ++p) {
-        uint32_t* ctp = ct + p * NT_BUNDLE * 32;  // this pass's rows
+        uint32_t* ctp = ct + p * NT_BUNDLE * Aux::kRow;  // this pass's rows
         uint32_t W[8];
 #pragma unroll
         for (int t = 0; t < 8; ++t) W[t] = acc[p][t];
@@ -1093,7 +1094,7 @@ __device__ __forceinline__ void tscan_bundles(const NtBatch& B, const NtOut& O, 
 #pragma unroll
         for (int j = 0; j < 8; ++j) W[j] = quad_byte_transpose(W[j], sel2, sel1);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) ctp[(8 * (lane & 3) + j) * 32 + half + (lane >> 2)] = W[j];
+        for (int j = 0; j < 8; ++j) ctp[(8 * (lane & 3) + j) * Aux::kRow + half + (lane >> 2)] = W[j];
         const uint32_t tb = half_bit_transpose(ge, lane) & (nv >= 32 ? ~0u : ((1u << nv) - 1u));
         tmb[((p * NT_BUNDLE + ms) * Aux::kF + fs) * 2 + mh] = tb;
       }
@@ -1102,18 +1103,22 @@ __device__ __forceinline__ void tscan_bundles(const NtBatch& B, const NtOut& O, 
       // windows as whole lines, store c covers slots 8 c .. 8 c + 7, lane 8 i +
       // q = the 16 bytes (windows 16 q ..) of slot 8 c + i
       // (every LDS read first, then the stores: one round trip, not one a store)
-      if ((st & 1) || st == nst - 1) {
-        uint4 m[4], x[kNP][4];
+      // (kRS = 1: stores c cover slots 16 c .. 16 c + 15, lane 4 i + q the 16
+      // bytes (windows 16 q ..) of slot 16 c + i, 64 bytes a slot)
+      if ((st % Aux::kRS) == Aux::kRS - 1 || st == nst - 1) {
+        constexpr int kC = 2 * Aux::kRS, kQ = 4 * Aux::kRS;  // stores; lanes a slot
+        uint4 m[kC], x[kNP][kC];
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const int s = 8 * c + (lane >> 3), q = lane & 7;
+        for (int c = 0; c < kC; ++c) {
+          const int s = (kWave / kQ) * c + lane / kQ, q = lane % kQ;
           m[c] = *reinterpret_cast<const uint4*>(sl + s);  // nw, wb_lo, wb_hi
 #pragma unroll
-          for (int p = 0; p < kNP; ++p) x[p][c] = *reinterpret_cast<const uint4*>(ct + p * NT_BUNDLE * 32 + s * 32 + 4 * q);
+          for (int p = 0; p < kNP; ++p)
+            x[p][c] = *reinterpret_cast<const uint4*>(ct + (p * NT_BUNDLE + s) * Aux::kRow + 4 * q);
         }
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const int kq = (st >> 1) * 2 * kWave + 16 * (lane & 7);
+        for (int c = 0; c < kC; ++c) {
+          const int kq = (st / Aux::kRS) * Aux::kRS * kWave + 16 * (lane % kQ);
           if (kq < (int)m[c].x) {
 #pragma unroll
             for (int p = 0; p < kNP; ++p) {
@@ -1128,10 +1133,10 @@ __device__ __forceinline__ void tscan_bundles(const NtBatch& B, const NtOut& O, 
       }
 #pragma unroll
       for (int p = 0; p < kNP; ++p) {
-        const uint32_t* ctp = ct + p * NT_BUNDLE * 32;
+        const uint32_t* ctp = ct + p * NT_BUNDLE * Aux::kRow;
         // checkpoints: covered bases before windows 16 jj, jj = 4 st + g
-        const uint4 va = *reinterpret_cast<const uint4*>(ctp + ms * 32 + half + 8 * mh);
-        const uint4 vb = *reinterpret_cast<const uint4*>(ctp + ms * 32 + half + 8 * mh + 4);
+        const uint4 va = *reinterpret_cast<const uint4*>(ctp + ms * Aux::kRow + half + 8 * mh);
+        const uint4 vb = *reinterpret_cast<const uint4*>(ctp + ms * Aux::kRow + half + 8 * mh + 4);
         uint32_t ga = 0u, gb = 0u;
         ga = __builtin_amdgcn_udot4(va.x, 0x01010101u, ga, false);
         ga = __builtin_amdgcn_udot4(va.y, 0x01010101u, ga, false);
