@@ -17,18 +17,20 @@
 // neighbour moves and popcounts (tools/valu_issue_bench.hip).
 //
 // Work split.  A wave claims a bundle from the per-XCD queues and walks its
-// stripes: lane k of stripe st owns block 64 st + k = positions [kL, kL + L),
-// i.e. split_telo window k of every read.  It walks positions [kL - kLam,
-// (k+1) L + kLam) (kLam = longest pattern - 1, rounded up to even; the left
-// halo feeds the coverage of the block's first bases, the right halo the
-// letter tests of its last starts) in RANGES of 32 positions: per range one
-// new 8-byte plane word {lo, hi} of each of the 32 reads (buffer loads, one
-// range ahead), the 32-position piece at the block's bit offset (v_alignbit)
-// and two 32 x 32 bit transposes in the lane's own registers (v_perm for the
-// byte stages, shift + v_bitop3 for the bit stages) give the 32 position
-// words of the range, walked fully unrolled (L and the patterns are baked
-// into the hiprtc build) into 8 bit planes of counts per pass (acc[b] bit s =
-// bit b of read s's count; counts <= L <= 170).
+// HALF STRIPES (32 windows of every read) in turn.  The half stripe's plane
+// words of the 32 reads are loaded straight into a per-wave LDS buffer (one
+// 16-byte buffer load per read and lane); lane (l, h) walks half h of window
+// 32 hs + l -- L0 = ceil(L / 2) positions plus kLam of halo on each side
+// (kLam = longest pattern - 1: the left halo feeds the coverage of the half's
+// first bases, the right halo the letter tests of its last starts) -- in
+// RANGES of 32 positions: the 32-position piece of every read at the lane's
+// bit offset (ds_read_b64 of two plane words, v_alignbit) and two 32 x 32 bit
+// transposes in the lane's own registers (v_perm for the byte stages, shift +
+// v_bfi for the bit stages) give the 32 position words of the range, walked
+// fully unrolled (L and the patterns are baked into the hiprtc build) into 8
+// bit planes of counts per pass (acc[b] bit s = bit b of read s's count;
+// counts <= L <= 170).  The halves' counts are added across the wave's halves
+// (v_permlane32_swap); two half stripes make one output stripe of 64 windows.
 //
 // Output, lane = window, per stripe and pass: the telomeric bits (count >=
 // thr[L]) by a bit-sliced compare and a 32 x 32 bit transpose inside each
@@ -144,8 +146,7 @@ struct TProg {
   static constexpr int kNP = kNTvr ? 3 : 2;
   static constexpr int kM = kMP > kMT ? kMP : kMT;
   static constexpr int kH = kM - 1;               // halo on each side
-  static constexpr int kLam = kH + (kH & 1);      // counting lag (even: loop runs start on slot boundaries)
-  static constexpr int kNPos = kL + 2 * kLam;     // positions walked per block
+  static constexpr int kLam = kH;                 // counting lag = the halo (a walk: 2 kLam prologue steps)
 };
 
 // Widths of the sliding-OR stages of the coverage spread for pattern length
