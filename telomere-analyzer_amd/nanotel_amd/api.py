@@ -133,7 +133,7 @@ class NanoTel:
         """nt_host_times: cumulative seconds of the host path's phases."""
         t = np.zeros(6, np.float64)
         _check(lib().nt_host_times(self._h, t.ctypes.data), self._h)
-        return dict(zip(("layout", "pack", "tlayout", "upload", "device", "checks"), t.tolist()))
+        return dict(zip(("layout", "pack", "plan", "upload", "device", "checks"), t.tolist()))
 
     def call_jit_wait(self):
         """Wait for the background build of the calling kernel specialised for
