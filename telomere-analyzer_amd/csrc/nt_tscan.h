@@ -909,6 +909,11 @@ __device__ __forceinline__ void tscan_bundles(const NtBatch& B, const NtOut& O, 
   static_assert(kL <= 170, "8-bit counts (nt_tscan_eligible)");
   using St = TsStage<kL>;
   using Wk = TWalkerL<TP, Pats, Tvrs>;
+  // The calling kernel of the previous bundle range runs beside this one
+  // (nt_host.cpp: a second stream) on the same SIMDs: the scan, VALU-bound at
+  // one wave per SIMD, takes the issue arbitration first (priority, then age),
+  // the latency-bound calling fills the cycles it leaves
+  __builtin_amdgcn_s_setprio(2);
   const int lane = threadIdx.x & (kWave - 1);
   TSlot* sl = reinterpret_cast<TSlot*>(wlds);
   uint32_t* ct = wlds + NT_BUNDLE * kTsSlotWords;  // the count rows

@@ -216,7 +216,7 @@ def test_mixed_length_lists_bundle_scan(cfg):
 
 
 # Reads with a few non-ACGT letters through the bundle scan (VERDICT r3 item
-# 6): the T-layout holds A at the letters; the calling kernel recounts every
+# 6): the planes hold A at the letters; the calling kernel recounts every
 # window within (longest pattern - 1) of one (call_fix_windows, nt_call.h).
 EXC_WINDOWS = 16  # NT_EXC_WINDOWS (nt_common.h)
 
@@ -680,7 +680,7 @@ def test_device_bundle_scan_matches_per_read_scan(read_len):
 @pytest.mark.parametrize("tvr", [None, "TGAGGG TTGGGG"], ids=["p2", "p3"])
 def test_device_bundles_with_sparse_exceptions(tvr):
     # bench.py --n-frac: device-generated reads, one N in every 4th read as an
-    # exception list entry only (the planes and the T-layout keep the
+    # exception list entry only (the planes keep the
     # generator's base there), all of them in the bundles; against the oracle
     # on the reads with that letter written in, window counts included
     import torch
