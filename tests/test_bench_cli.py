@@ -42,3 +42,19 @@ def test_bench_refuses_debug_environment():
     clean = {k: v for k, v in os.environ.items() if not k.startswith("NT_")}
     assert bench.refused_env(clean) == []
     assert bench.env_knobs(dict(clean, NT_TSUB="2", NT_JIT_CACHE="/x")) == {"NT_JIT_CACHE": "/x", "NT_TSUB": "2"}
+
+
+def test_bench_default_is_the_metric_configuration():
+    """The driver runs bench.py without --config: its default is BASELINE.json
+    configs[4]'s per-GPU shard (12.5 M x 50 kb, TTAGGG), the configuration the
+    headline metric is quoted on."""
+    import json
+    sys.path.insert(0, ROOT)
+    import bench
+    src = open(os.path.join(ROOT, "bench.py")).read()
+    assert 'ap.add_argument("--config", default="c5"' in src
+    cfg = bench.CONFIGS["c5"]
+    assert (cfg["reads"], cfg["read_len"], cfg["patterns"], cfg["tvr"]) == (12_500_000, 50_000, "TTAGGG", None)
+    base = json.load(open(os.path.join(ROOT, "BASELINE.json")))
+    assert "TTAGGG, 50 kb reads" in base["metric"] and bench.METRICS["c5"].startswith("Gbases/s scanned (TTAGGG, 50 kb")
+    assert "100M" in base["configs"][4] and 100_000_000 // 8 == cfg["reads"]

@@ -1,7 +1,7 @@
 """Summary of tools/gpu_quick.sh's outputs for a tag."""
 import json, sys
 tag = sys.argv[1] if len(sys.argv) > 1 else "q"
-for f, pick in (("diag", lambda l: "reads with" in l), ("t", lambda l: "passed" in l or "failed" in l)):
+for f, pick in (("t", lambda l: "passed" in l or "failed" in l),):
     try:
         for l in open(f"gpurun_out/{f}_{tag}.log"):
             if pick(l):
