@@ -375,7 +375,8 @@ def main():
     # a stream of resident batches runs; consecutive steps write alternate
     # output sets, and the timed region ends after nt_join (every step's rows
     # complete).  --no-pipeline: each step waits for its own calling.
-    pipelined = bundles is not None and want_pipe
+    # (the per-read scan pipelines when it runs in sub-batches, NT_SUBBATCH > 1)
+    pipelined = want_pipe and (bundles is not None or int(os.environ.get("NT_SUBBATCH", "1")) > 1)
     outs = [(start, end, dens, flags, wc)]
     if pipelined:
         outs.append(tuple(torch.empty_like(x) for x in outs[0][:4]) + (big_buffer(wc_bytes, torch.uint8),))
