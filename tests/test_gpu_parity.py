@@ -892,11 +892,12 @@ def test_full_size_bundle_scan_equals_per_read_scan(cfg):
     torch.cuda.empty_cache()
 
 
-@pytest.mark.parametrize("L", [37, 100, 50])
+@pytest.mark.parametrize("L", [37, 100, 50, 127, 170])
 def test_bundle_scan_ragged_packed_batch(L):
     # ragged bundles from the host packer (lengths sorted within a bundle, read
     # ends inside plane words, bundles whose reads lie anywhere in the batch),
-    # odd L (the second half window one position short): the bundle scan
+    # odd L (the second half window one position short), L = 127 and 170
+    # (rows of more than 64 units: two loads a slot; 3 ranges a walk): the bundle scan
     # against the per-read scan of the same device batch on every output
     import ctypes
     import torch
