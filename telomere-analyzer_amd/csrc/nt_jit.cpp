@@ -118,15 +118,62 @@ bool nt_tscan_eligible(const NtProgram& P) {
 
 namespace {
 
+// The bundle scan's pattern list with the patterns of one length that differ
+// in a single letter merged into one (that letter's truth table the union):
+// TTAGGG + TCAGGG -> TYAGGG.  The walk counts coverage only, and for two
+// patterns P, Q equal but at letter k the <= 1-mismatch matches of P or Q are
+// exactly those of the merged R (x_k in P's or Q's set: R's mismatches are P's
+// or Q's; x_k in neither: R's one mismatch is at k and P's is too), as are the
+// exact ones -- one combine a step instead of two (c4's TTAGGG TCAGGG).  The
+// per-read scan keeps the list as given (its hit counters are per pattern).
+std::string merged_types(const NtPat* v, int n) {
+  struct T {
+    int m;
+    std::vector<int> tt;
+  };
+  std::vector<T> ps;
+  for (int i = 0; i < n; ++i) {
+    T t{v[i].m, std::vector<int>(v[i].tt_scan, v[i].tt_scan + v[i].m)};
+    bool dup = false;
+    for (const T& q : ps) dup = dup || (q.m == t.m && q.tt == t.tt);
+    if (!dup) ps.push_back(t);
+  }
+  for (bool again = true; again;) {
+    again = false;
+    for (size_t i = 0; i < ps.size() && !again; ++i)
+      for (size_t j = i + 1; j < ps.size() && !again; ++j) {
+        if (ps[i].m != ps[j].m) continue;
+        int k = -1, nd = 0;
+        for (int x = 0; x < ps[i].m; ++x)
+          if (ps[i].tt[x] != ps[j].tt[x]) {
+            k = x;
+            ++nd;
+          }
+        if (nd != 1) continue;
+        ps[i].tt[k] |= ps[j].tt[k];
+        ps.erase(ps.begin() + (long)j);
+        again = true;
+      }
+  }
+  std::string out;
+  for (size_t i = 0; i < ps.size(); ++i) {
+    out += (i ? ", " : "") + std::string("nt::CtPat<") + std::to_string(ps[i].m);
+    for (int t : ps[i].tt) out += ", " + std::to_string(t);
+    out += ">";
+  }
+  return out;
+}
+
 std::string jit_source(const NtProgram& P) {
   std::string pats, tvrs;
   for (int i = 0; i < P.n_pat; ++i) pats += (i ? ", " : "") + pat_type(P.pat[i]);
   for (int i = 0; i < P.n_tvr; ++i) tvrs += (i ? ", " : "") + pat_type(P.tvr[i]);
+  const std::string tpats = merged_types(P.pat, P.n_pat), ttvrs = merged_types(P.tvr, P.n_tvr);
   std::string s = kTypedefs;
   s += "#include \"nt_tscan.h\"\n";
   s += "using JitSet = nt::CtSet<nt::CtList<" + pats + ">, nt::CtList<" + tvrs + ">>;\n";
   if (nt_tscan_eligible(P)) {
-    s += "using TPats = nt::CtList<" + pats + ">;\nusing TTvrs = nt::CtList<" + tvrs + ">;\n";
+    s += "using TPats = nt::CtList<" + tpats + ">;\nusing TTvrs = nt::CtList<" + ttvrs + ">;\n";
     s += "using TJit = nt::TProg<TPats, TTvrs, " + std::to_string(P.L) + ">;\n";
     // one wave per bundle; as many waves a workgroup (at most 4, one per
     // SIMD) as their LDS (slots, output rows, the half-stripe buffer) fits in

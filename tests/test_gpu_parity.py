@@ -215,6 +215,23 @@ def test_mixed_length_lists_bundle_scan(cfg):
     assert nt.tscan, "mixed-length list not on the bundle scan"
 
 
+# Pattern lists whose patterns differ in one letter: the bundle scan walks them
+# merged (TTAGGG + TCAGGG -> TYAGGG, nt_jit.cpp merged_types; the union of the
+# <= 1-mismatch matches is the merged pattern's); the per-read scan keeps them
+# apart (its hit counters); both against the oracle on the unmerged list.
+MERGED = [
+    dict(patterns="TTAGGG TCAGGG TAAGGG"),                      # three merge into one
+    dict(patterns="TTAGGG TTAGGC TCAGGG", tvr_patterns="TGAGGG TTAGGA"),  # chains and a TVR pair
+    dict(patterns="TTAGGG TTRGGG"),                             # an IUPAC letter in the union
+]
+
+
+@pytest.mark.parametrize("cfg", MERGED, ids=["three", "chain_tvr", "iupac"])
+def test_merged_pattern_lists_bundle_scan(cfg):
+    nt = _random_reads(cfg, True, check_tscan=False)
+    assert nt.tscan
+
+
 # Reads with a few non-ACGT letters through the bundle scan (VERDICT r3 item
 # 6): the planes hold A at the letters; the calling kernel recounts every
 # window within (longest pattern - 1) of one (call_fix_windows, nt_call.h).
