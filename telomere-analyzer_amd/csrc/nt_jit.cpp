@@ -487,8 +487,8 @@ bool nt_jit_get(int device, const NtProgram& P, void* fn[4], void** tfn, std::st
   return true;
 }
 
-// a JIT kernel's block size (its __launch_bounds__: the bundle scan has 320
-// threads with walker / writer waves, 256 without)
+// a JIT kernel's block size (its __launch_bounds__: the bundle scan's is 64
+// kTsNW, a wave per bundle and as many as the CU's LDS holds; 256 otherwise)
 static int jit_threads(void* fn) {
   int v = 0;
   if (hipFuncGetAttribute(&v, HIP_FUNC_ATTRIBUTE_MAX_THREADS_PER_BLOCK, (hipFunction_t)fn) != hipSuccess || v <= 0)
