@@ -1,7 +1,10 @@
 #!/bin/bash
 # A/B of two builds on one box: _ab/old (a copy of the package built from an
 # earlier tree) against the working tree, c50k and c10k, twice, alternating.
-# tools/ab_run.sh [extra bench args] [tag]
+# tools/ab_run.sh [extra bench args] [tag]; AB_ORDER="new old" reverses the order.
+# Make _ab/old from a clean tree: git stash; python -c 'import __graft_entry__ as g;
+# g.build()'; mkdir -p _ab/old; cp -r telomere-analyzer_amd bench.py tests _ab/old/;
+# git stash pop; rebuild.  (_ab/ is git-ignored; delete it when done.)
 set -o pipefail
 extra=${1:-}; tag=${2:-ab}
 mkdir -p gpurun_out
