@@ -1156,6 +1156,7 @@ static __device__ __forceinline__ bool bundle_span_error(const NtProgram* __rest
                                                          const uint64_t* __restrict__ tmask, uint64_t r) {
   const int np = prog->n_pass;
   const int nw = (int)split_window_count((int)B.len[r], prog->L);
+  if (nw == 0) return false;  // nothing to call from the scan's outputs (its ck[0] is written anyway)
   const uint32_t* ck = reinterpret_cast<const uint32_t*>(tmask + aux_base(B.win_off[r], r, np) + (uint64_t)np * aux_nmw(nw));
   return ck[0] == 0xFFFFFFFFu;
 }

@@ -1182,7 +1182,8 @@ int nt_analyze_host(nt_ctx* ctx, const char* const* seqs, const uint64_t* lens, 
     const uint8_t f = h_flags[r];
     if (!(f & NT_FLAG_DONE)) return fail(ctx, NT_E_HIP, "read " + std::to_string(r) + " not processed");
     if (f & NT_FLAG_ERR_ALIGN)
-      return fail(ctx, NT_E_ARG, "read " + std::to_string(r) + ": blk_off must be even");
+      return fail(ctx, NT_E_ARG, "read " + std::to_string(r) +
+                                     ": layout error (an odd blk_off, or its bundle's planes more than 2 GiB apart)");
     if (f & NT_FLAG_ERR_RIGHT)
       return fail(ctx, NT_E_RIGHT_EMPTY,
                   "read " + std::to_string(r) + ": find_right_telo on a read without windows");

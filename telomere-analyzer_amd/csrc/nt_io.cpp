@@ -748,11 +748,17 @@ int fq_parse_one(const char* d, size_t n, size_t p, nt_reader::FqRec& rec, size_
   size_t c = ep >= n ? n : ep + 1;
   if (sl > 0 && c < n) {
     const size_t qe = c + sl;
-    if (qe == n) {
+    // one quality line of exactly sl letters: a line end at qe, no line end
+    // inside [c, qe) (a wrapped quality whose lines and newlines add up to
+    // sl), no '\r' at qe - 1 (a CRLF line of sl - 1 letters) -- otherwise the
+    // line walk below, which is the line parser's (parse_record): both then
+    // see the same lines and reject the same malformed records
+    const bool one_line = qe <= n && d[qe - 1] != '\r' && !std::memchr(d + c, '\n', sl);
+    if (one_line && qe == n) {
       c = n;
-    } else if (qe < n && d[qe] == '\n') {
+    } else if (one_line && qe < n && d[qe] == '\n') {
       c = qe + 1;
-    } else if (qe + 1 < n && d[qe] == '\r' && d[qe + 1] == '\n') {
+    } else if (one_line && qe + 1 < n && d[qe] == '\r' && d[qe + 1] == '\n') {
       c = qe + 2;
     } else {  // wrapped (or longer) quality: its lines, up to the sequence's length
       uint64_t ql = 0;

@@ -983,8 +983,12 @@ __device__ __forceinline__ void tscan_bundles(const NtBatch& B, const NtOut& O, 
         t.run[0] = t.run[1] = t.run[2] = 0u;
         t.pad = o && span_ok ? (uint32_t)((bo - base) * 8ull) : 0u;  // the slot's planes, bytes from base
         sl[lane] = t;
-        if (o && !span_ok)  // see kTsSpanError
-          reinterpret_cast<uint32_t*>(tmask + ab + (uint64_t)kNP * aux_nmw((int)t.nw))[0] = kTsSpanError;
+        // the first checkpoint (the calling kernel's span check reads it for
+        // every bundled read): the flush writes it for a read with windows; a
+        // read of none (<= L/2 bases) or an unscanned bundle gets it here
+        if (o && (!span_ok || t.nw == 0u))  // see kTsSpanError
+          reinterpret_cast<uint32_t*>(tmask + ab + (uint64_t)kNP * aux_nmw((int)t.nw))[0] =
+              span_ok ? 0u : kTsSpanError;
       }
       n_max = (uint32_t)__builtin_amdgcn_readfirstlane((int)len);  // slot 0 = the longest
     }
@@ -997,19 +1001,20 @@ __device__ __forceinline__ void tscan_bundles(const NtBatch& B, const NtOut& O, 
         const_cast<uint32_t*>(B.planes) + base * 2ull, (short)0, (int)(uint32_t)((top - base) * 8ull), 0x00020000);
     // the buffer's loads: row s piece c <- 16-byte units 64 c + lane of slot s
     // (lanes past the row's end idle), voffset = the slot's planes (bytes from
-    // the descriptor base, lane s of pad_v) + the unit, soffset = the half
-    // stripe's first word (half stripe 0 starts 2 words before the reads: the
-    // range check does not wrap voffset + soffset, so that offset goes into
-    // voffset, where a slot at the descriptor base wraps past the range and
-    // loads zeros)
+    // the descriptor base, lane s of pad_v) + the half stripe's first word +
+    // the unit, soffset = 0: the whole offset is in voffset, which the raw
+    // buffer's range check covers, so a short slot's rows past the bundle's
+    // last plane word (its half stripes beyond its read; at the planes
+    // allocation's end for the batch's last read) load zeros and never reach
+    // past the allocation (half stripe 0 starts 2 words before the reads: a
+    // slot at the descriptor base wraps past the range there and loads zeros)
     const uint32_t pad_v = sl[lane & (NT_BUNDLE - 1)].pad;
     // the buffer's LDS address, provably wave-uniform (the loads' M0)
     const uint32_t stage_lds = (uint32_t)__builtin_amdgcn_readfirstlane(
         (int)(uint32_t)(unsigned long)(__attribute__((address_space(3))) void*)stage);
     auto fetch = [&](int hs) {
       const int fw = St::first_word(hs);
-      const uint32_t so = fw < 0 ? 0u : (uint32_t)(fw * 8);
-      const uint32_t vl = 16u * (uint32_t)lane - (fw < 0 ? (uint32_t)(-fw * 8) : 0u);
+      const uint32_t vl = 16u * (uint32_t)lane + (uint32_t)(fw * 8);  // (mod 2^32: fw = -2 wraps)
       // (the slots' offsets are read with every lane active: a lane the load's
       // mask leaves out has no defined value to read)
       uint32_t pad[NT_BUNDLE];
@@ -1022,7 +1027,7 @@ __device__ __forceinline__ void tscan_bundles(const NtBatch& B, const NtOut& O, 
           for (int s = 0; s < NT_BUNDLE; ++s)
             __builtin_amdgcn_raw_ptr_buffer_load_lds(
                 rs, (__attribute__((address_space(3))) void*)(unsigned long)(stage_lds + 8u * (s * St::kRow + 2 * kWave * c)),
-                16, pad[s] + 1024u * c + vl, so, 0, 0);
+                16, pad[s] + 1024u * c + vl, 0, 0, 0);
         }
       }
     };

@@ -1,4 +1,4 @@
-/* Declarations of the public R C API subset that INTEGRATION.md's .Call shim
+/* Declarations of the public R C API subset that r/nanotel_r.c (the .Call shim)
  * uses (R is not installed in this image).  Test scaffolding only: it lets
  * tests/test_integration_shim.py type-check the documented shim against
  * include/nanotel.h with gcc -fsyntax-only; nothing is linked or run. */

@@ -976,6 +976,85 @@ def test_bundle_scan_ragged_packed_batch(L):
     assert int(((ref["flags"] & 1) != 0).sum()) > 5
 
 
+@pytest.mark.parametrize("L", [100, 170])
+def test_bundle_scan_short_last_read_at_allocation_end(L):
+    # The batch's last read is short and shares a bundle with 31 long reads,
+    # and the planes end exactly at the end of their device allocation: every
+    # half stripe of the long slots loads a row for the short slot too, up to
+    # ~13 KB past its last plane word.  Those loads must stay inside the
+    # bundle's buffer range (they load zeros past it; the whole offset is in
+    # voffset, which the range check covers).  Bundle scan against the per-read
+    # scan of the same device batch on every output.
+    import ctypes
+    import torch
+    from nanotel_amd import _lib
+    from nanotel_amd.api import DeviceBundles
+    rng = np.random.default_rng(400 + L)
+    seqs = []
+    for i in range(63):
+        n_i = int(rng.integers(30000, 40000))
+        s_i = bytearray(rng.choice(list(b"ACGT"), n_i).tolist())
+        if i % 2 == 0:
+            s_i[:4000] = (b"TTAGGG" * 700)[:4000]
+        seqs.append(bytes(s_i))
+    seqs.append(b"TTAGGGTTAGGGTTAGGGTTAGGGTTAGGGTTAGGGTTAGGGTT")  # 44 bases: no window
+    lib = _lib.lib()
+    n = len(seqs)
+    ptrs = (ctypes.c_char_p * n)(*seqs)
+    lens = np.array([len(x) for x in seqs], np.uint64)
+    tb, tw, te, ml, bad = (ctypes.c_uint64() for _ in range(5))
+    assert lib.nt_pack_count(ctypes.cast(ptrs, ctypes.c_void_p), lens.ctypes.data, n, L, ctypes.byref(tb),
+                             ctypes.byref(tw), ctypes.byref(te), ctypes.byref(ml), ctypes.byref(bad)) == 0
+    planes = np.zeros(2 * tb.value, np.uint32)
+    blk, ln, wo = np.zeros(n, np.uint64), np.zeros(n, np.uint32), np.zeros(n, np.uint64)
+    assert lib.nt_pack_reads(ctypes.cast(ptrs, ctypes.c_void_p), lens.ctypes.data, n, 0, L, planes.ctypes.data,
+                             blk.ctypes.data, ln.ctypes.data, wo.ctypes.data, None, None, None) == 0
+    assert int(blk[-1]) + 2 == tb.value  # the short read's one block pair ends the planes
+    nt = _nt(patterns="TTAGGG", subseq_length=L)
+    assert nt.tscan
+    plan = nt.bundle_plan(ln, blk_off=blk)
+    assert plan.n_bundles == 2 and len(plan.list) == 0
+    assert n - 1 in set(plan.bnd_read[32:64].tolist())  # with 31 long reads
+    # the planes at the very end of an allocation of whole 2 MiB pages
+    pb = planes.nbytes
+    alloc = (pb + (2 << 20) - 1) // (2 << 20) * (2 << 20)
+    buf = torch.zeros(alloc // 4, dtype=torch.int32, device="cuda")
+    off = (alloc - pb) // 4
+    assert off % 4 == 0  # 16-byte aligned base
+    buf[off:].copy_(torch.from_numpy(planes.view(np.int32)))
+    pl_ptr = buf.data_ptr() + 4 * off
+    dev = {k: torch.from_numpy(v).cuda() for k, v in (("blk", blk.view(np.int64)), ("ln", ln.view(np.int32)),
+                                                    ("wo", wo.view(np.int64)))}
+    br = torch.from_numpy(plan.bnd_read.view(np.int32)).cuda()
+    bb = DeviceBundles(br.data_ptr(), plan.n_bundles, 0, 0)
+    nwc = int(tw.value) * nt.n_pass
+    outs = []
+    for bundles in (None, bb):
+        o = dict(start=torch.full((n * 3,), 7, dtype=torch.int32, device="cuda"),
+                 end=torch.full((n * 3,), 7, dtype=torch.int32, device="cuda"),
+                 dens=torch.full((n * 3,), 7.0, dtype=torch.float64, device="cuda"),
+                 flags=torch.zeros(n, dtype=torch.uint8, device="cuda"),
+                 wc=torch.full((nwc,), 0x55, dtype=torch.uint8, device="cuda"))
+        nt.scan_call_device(pl_ptr, dev["blk"].data_ptr(), dev["ln"].data_ptr(),
+                            dev["wo"].data_ptr(), n, int(tw.value), int(ml.value), o["start"].data_ptr(),
+                            o["end"].data_ptr(), o["dens"].data_ptr(), o["flags"].data_ptr(), o["wc"].data_ptr(),
+                            bundles=bundles)
+        nt.synchronize()
+        outs.append({k: v.cpu().numpy() for k, v in o.items()})
+    ref, got = outs
+    for k in ("start", "end", "flags"):
+        assert np.array_equal(got[k], ref[k]), (k, np.flatnonzero(got[k] != ref[k])[:8])
+    assert np.array_equal(got["dens"].view(np.uint64), ref["dens"].view(np.uint64))
+    for r in range(n):
+        nw = int(lib.nt_window_count(int(ln[r]), L))
+        rows = int(lib.nt_window_rows(nw))
+        for p in range(nt.n_pass):
+            o = int(wo[r]) * nt.n_pass + p * rows
+            assert np.array_equal(got["wc"][o:o + nw], ref["wc"][o:o + nw]), (r, p)
+    assert int(((ref["flags"] & 1) != 0).sum()) >= 20
+    nt.close()
+
+
 def test_rc_device_matches_host_packer():
     # nt_rc_device (the --rc transform of a device-resident batch) against the
     # host packer's fused reverse complement (nt_pack_reads rc = 1) on every
@@ -1034,6 +1113,100 @@ def test_bundle_plan_keeps_bundles_compact():
     assert set(plan.bnd_read.tolist()) == set(range(32)) | set(range(64, 96))
     plan = nt.bundle_plan(ln)  # no blk_off: the caller vouches
     assert plan.n_bundles == 3 and len(plan.list) == 0
+
+
+@pytest.mark.parametrize("cfg", [("TTAGGG", None, {}), ("TTAGGG", None, {"NT_CALL_JIT": "1"}),
+                                 ("TTAGGG TCAGGG", "TGAGGG TTGGGG", {}),
+                                 ("TTAGGG TCAGGG", "TGAGGG TTGGGG", {"NT_CALL_JIT": "1", "NT_CALL_SPLIT": "1"})],
+                         ids=["fused_aot", "fused_jit", "p3_aot", "p3_split"])
+def test_bundle_spanning_more_than_2gib_is_reported(cfg, monkeypatch):
+    # A device batch planned without its blk_off (the caller vouches) whose
+    # bundle's planes lie more than 2 GiB apart: the bundle scan cannot address
+    # them with one buffer descriptor, so it skips the bundle and marks its
+    # reads' first checkpoint (kTsSpanError); every calling form (the fused
+    # kernel ahead of time / specialised, the per-pass split and its combine
+    # kernel) reports exactly those reads as ROW_DONE | ROW_ERR_ALIGN, and every
+    # other read equals the per-read scan of the same batch.
+    import torch
+    from nanotel_amd import read_blocks, synth_params
+    from nanotel_amd._lib import ROW_DONE, ROW_ERR_ALIGN
+    from nanotel_amd.api import DeviceBundles
+    pats, tvr, env = cfg
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    n, read_len, far = 96, 5000, 40
+    nt = _nt(patterns=pats, tvr_patterns=tvr)
+    assert nt.tscan
+    t = _device_batch(nt, synth_params(read_len=read_len, first_read=300), n, read_len, hits=False)
+    wpr = 2 * read_blocks(read_len)  # int32 plane words a read
+    far_blk = (1 << 28) + 2          # plane words of 8 bytes: 2 GiB + 16 B into the buffer
+    big = torch.zeros(2 * far_blk + wpr + 64, dtype=torch.int32, device="cuda")
+    big[:n * wpr].copy_(t["planes"])
+    big[2 * far_blk:2 * far_blk + wpr].copy_(t["planes"][far * wpr:(far + 1) * wpr])
+    t["planes"] = big
+    t["blk_off"][far] = far_blk
+    torch.cuda.synchronize()
+
+    def run(bundles):
+        for k in ("start", "end"):
+            t[k].fill_(7)
+        t["dens"].fill_(7.0)
+        t["flags"].zero_()
+        t["wc"].fill_(0x55)
+        torch.cuda.synchronize()
+        nt.scan_call_device(t["planes"].data_ptr(), t["blk_off"].data_ptr(), t["lens"].data_ptr(),
+                            t["win_off"].data_ptr(), n, n * t["rows"], read_len, t["start"].data_ptr(),
+                            t["end"].data_ptr(), t["dens"].data_ptr(), t["flags"].data_ptr(), t["wc"].data_ptr(),
+                            bundles=bundles)
+        nt.synchronize()
+        return {k: t[k].cpu().numpy().copy() for k in ("start", "end", "dens", "flags", "wc")}
+
+    ref = run(None)  # the per-read scan: one 64-bit address a read
+    assert not (ref["flags"] & ROW_ERR_ALIGN).any()
+    plan = nt.bundle_plan(np.full(n, read_len, np.uint32))  # no blk_off: the bundle stays
+    assert plan.n_bundles == 3 and len(plan.list) == 0
+    br = torch.from_numpy(plan.bnd_read.view(np.int32)).cuda()
+    got = run(DeviceBundles(br.data_ptr(), plan.n_bundles, 0, 0))
+    bad_b = int(np.flatnonzero(plan.bnd_read == far)[0]) // 32
+    bad = set(int(r) for r in plan.bnd_read[32 * bad_b:32 * bad_b + 32] if r != 0xFFFFFFFF)
+    assert far in bad and len(bad) == 32
+    ok = np.array([r not in bad for r in range(n)])
+    assert all(int(got["flags"][r]) == (ROW_DONE | ROW_ERR_ALIGN) for r in bad), got["flags"][sorted(bad)]
+    assert np.array_equal(got["flags"][ok], ref["flags"][ok])
+    assert int(((ref["flags"][ok] & 1) != 0).sum()) > 8  # telomeric reads among the others
+    for k in ("start", "end"):
+        assert np.array_equal(got[k].reshape(n, 3)[ok], ref[k].reshape(n, 3)[ok]), k
+    assert np.array_equal(got["dens"].reshape(n, 3)[ok].view(np.uint64), ref["dens"].reshape(n, 3)[ok].view(np.uint64))
+    wc_g = got["wc"].reshape(n, nt.n_pass, t["rows"])[:, :, :t["nw"]]
+    wc_r = ref["wc"].reshape(n, nt.n_pass, t["rows"])[:, :, :t["nw"]]
+    assert np.array_equal(wc_g[ok], wc_r[ok])
+    nt.close()
+    del big, t
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("tvr", [None, "TGAGGG TTGGGG"], ids=["p2", "p3"])
+def test_reads_without_windows_in_bundles_on_a_poisoned_aux_buffer(tvr, monkeypatch):
+    # Reads of <= L/2 bases have no window (split_telo, NanoTel.R:216-223) but
+    # sit in bundles; the calling kernel's span check reads their first
+    # checkpoint, which the bundle scan must write although no flush covers
+    # it.  The context first runs a telomeric batch (bitmask words of all
+    # ones in the reused aux buffer), then, with the aux buffer filled with
+    # 0xFF bytes before every call (NT_DBG_POISON_AUX: every word read must
+    # be written), bundles that mix windowless and windowed reads.
+    monkeypatch.setenv("NT_DBG_POISON_AUX", "255")
+    rng = np.random.default_rng(93)
+    nt = _nt(patterns="TTAGGG", tvr_patterns=tvr)
+    assert nt.tscan
+    telo = [_telo_read(rng, 12000, tract=(6000, 11000), sub=0.0) for _ in range(64)]
+    nt.analyze(telo, want_windows=True)
+    seqs = [_telo_read(rng, int(k), tract=(0, int(k))) for k in rng.integers(1, 51, 80)]
+    seqs += [_telo_read(rng, int(k), tract=(0, int(k))) for k in rng.integers(51, 400, 30)]
+    seqs += ["TTAGGG" * 8, "T" * 50, "TTAGGGTTAGGGTTAGGGTTAGGGTTAGGGTTAGGGTTAGGGTTAGGGTT"]
+    rng.shuffle(seqs)
+    res = nt.analyze(seqs, want_windows=True)
+    compare(nt, res, oracle_rows(seqs, "TTAGGG", tvr=tvr), check_hits=False)
+    nt.close()
 
 
 # BASELINE.json configs[2], [3] (10M x 50 kb) and one GPU's shard of

@@ -371,8 +371,16 @@ def test_fastq_fast_path_matches_line_parser(tmp_path, monkeypatch):
     cases["no_final_newline"] = cases["mixed"].rstrip("\r\n")
     cases["truncated_quality"] = cases["mixed"] + "@tail\nACGTACGT\n+\nIII"
     cases["malformed"] = cases["mixed"] + "@bad\nACGT\nIIII\n"
+    # a wrapped quality whose lines and newline add up to the sequence's
+    # length (a line end at qe, another inside [c, qe)), and a CRLF quality one
+    # letter short (its '\r' at qe - 1): the fast path must not take either as
+    # one quality line; the line parser walks on into the next record
+    tail = "@next\nACGTACGTAC\n+\nIIIIIIIIII\n"
+    cases["wrapped_to_length"] = cases["mixed"] + "@w\nACGTACGTAC\n+\nIIII\nIIIII\n" + tail
+    cases["crlf_short"] = cases["mixed"] + "@c\nACGTACGTAC\n+\nIIIIIIIII\r\n" + tail
     big = "".join(body(i, f"b{i}", "ACGT" * 2500, False) for i in range(4000))  # 40 MB: several threads
     cases["big"] = big
+    cases["big_wrapped_to_length"] = big + "@w\nACGTACGTAC\n+\nIIII\nIIIII\n" + big[:200000]
 
     def read_all(path, nrec):
         out, err = [], None
@@ -396,4 +404,5 @@ def test_fastq_fast_path_matches_line_parser(tmp_path, monkeypatch):
             monkeypatch.setenv("NT_READER_FQ_FAST", "1")
             fast = read_all(p, nrec)
             assert fast == slow, (key, nrec)
-        assert (slow[1] is not None) == (key == "malformed"), (key, slow[1])
+        rejected = ("malformed", "wrapped_to_length", "crlf_short", "big_wrapped_to_length")
+        assert (slow[1] is not None) == (key in rejected), (key, slow[1])
