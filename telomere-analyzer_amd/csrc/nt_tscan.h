@@ -656,6 +656,74 @@ struct TsStage {
   __device__ __forceinline__ static int first_word(int hs) { return (hs * kL - 2) & ~1; }
 };
 
+// LDS banks of the cuts.  Every lane reads its pieces from all 32 rows, one
+// ds_read_b64 a row; in slot order the 32 lanes of a half wave read ONE row
+// at their own words (lane l: word (l L + h L0 - kLam) / 32 + c), ~3.1 L / 32
+// words apart, whose bank words (mod 32) collide pairwise: 2-way conflicts,
+// twice the LDS cycles of every cut read (SQ_LDS_BANK_CONFLICT at c5: 2.75
+// extra cycles a LDS instruction, profiles/r06).  So lane l reads the rows in
+// its own rotated order, row (s + rot_l) mod 32 at read s: its bank word
+// moves by rot_l kRow (mod 32), and rot_l in 0..kMaxRot is chosen per lane
+// and half (a bipartite matching of lanes to the 32 bank words, at compile
+// time) so that every read of a half wave hits 32 distinct bank words.  The
+// walk is bitwise in the slots, so bit s of every word then belongs to slot
+// (s + rot_l) mod 32: the lane's counters are rotated back before the halves
+// are added (one v_alignbit a counter word).
+constexpr int kTsMaxRot = 3;
+template <int kL, int kLam, int kRow>
+struct TsRot {
+  struct Tab {
+    int rot[64];
+  };
+  // lane l of half h: its first word mod 32, and the bank word of rotation r
+  static constexpr int word(int l, int h) { return (l * kL + h * ((kL + 1) / 2) - kLam) >> 5; }
+  static constexpr int bank(int l, int h, int r) { return (((word(l, h) + r * kRow) % 32) + 32) % 32; }
+  struct Match {
+    int owner[32];  // bank word -> lane (or -1)
+    int rot[32];
+  };
+  // Kuhn's augmenting path from lane l (visited: bank words seen this round)
+  static constexpr bool augment(Match& m, int l, int h, bool (&seen)[32]) {
+    for (int r = 0; r <= kTsMaxRot; ++r) {
+      const int b = bank(l, h, r);
+      if (seen[b]) continue;
+      seen[b] = true;
+      if (m.owner[b] < 0 || augment(m, m.owner[b], h, seen)) {
+        m.owner[b] = l;
+        m.rot[l] = r;
+        return true;
+      }
+    }
+    return false;
+  }
+  static constexpr Tab make() {
+    Tab t{};
+    for (int h = 0; h < 2; ++h) {
+      Match m{};
+      for (int b = 0; b < 32; ++b) m.owner[b] = -1;
+      for (int l = 0; l < 32; ++l) m.rot[l] = 0;
+      for (int l = 0; l < 32; ++l) {
+        bool seen[32] = {};
+        augment(m, l, h, seen);  // (an unmatched lane keeps rotation 0: a conflict, not an error)
+      }
+      for (int l = 0; l < 32; ++l) t.rot[32 * h + l] = m.rot[l];
+    }
+    return t;
+  }
+  static constexpr Tab kTab = make();
+  static constexpr uint64_t mask(int bit) {
+    uint64_t x = 0;
+    for (int l = 0; l < 64; ++l) x |= (uint64_t)((kTab.rot[l] >> bit) & 1) << l;
+    return x;
+  }
+  static constexpr uint64_t kBit0 = mask(0), kBit1 = mask(1);
+  static_assert(kTsMaxRot <= 3, "two mask bits");
+  // this lane's rotation
+  __device__ __forceinline__ static int of_lane(int lane) {
+    return (int)((kBit0 >> lane) & 1u) | ((int)((kBit1 >> lane) & 1u) << 1);
+  }
+};
+
 // The walk of one half stripe per lane, from the LDS buffer.  Lane (l, h) =
 // (lane & 31, lane >> 5) walks window 32 hs + l's positions [h L0, h L0 + L0)
 // -- L0 = ceil(L / 2); the second half is L0 - 1 long when L is odd, its last
@@ -681,36 +749,46 @@ struct TWalkerL {
   using St = TsStage<kL>;
   typename TPipeSel<TP, Pats, Tvrs>::type pp;
 
-  // range r's pieces of every slot: rows from the lane's word w (LDS)
+  typedef const volatile __attribute__((address_space(3))) uint64_t lds_u64;
+  // the row of read s in this lane's rotated order (TsRot): row (s + rot) mod
+  // 32; the reads that wrap (s >= 32 - kTsMaxRot) pick their base per lane
+  template <int s>
+  __device__ __forceinline__ static lds_u64* rrow(lds_u64* a, int rot) {
+    if constexpr (s + kTsMaxRot < NT_BUNDLE) return a + s * St::kRow;
+    else return a + s * St::kRow - (s + rot >= NT_BUNDLE ? NT_BUNDLE * St::kRow : 0);
+  }
+
+  // range r's pieces of every slot: rows from the lane's word w (LDS), read
+  // s = slot (s + rot) mod 32
   template <int r>
-  __device__ __forceinline__ static void cut(const uint2* row, uint32_t sh, uint32_t (&lo)[32],
+  __device__ __forceinline__ static void cut(const uint2* row, uint32_t sh, int rot, uint32_t (&lo)[32],
                                              uint32_t (&hi)[32]) {
     // (volatile: one ds_read_b64 a word -- two accesses of 32 lanes, 256 B a
     // clock -- where the compiler would pair a word with its neighbour into a
     // ds_read2_b64, which the LDS serves at half that rate)
-    typedef const volatile __attribute__((address_space(3))) uint64_t lds_u64;
-    lds_u64* vr = (lds_u64*)(row);
-#pragma unroll
-    for (int s = 0; s < NT_BUNDLE; ++s) {
-      const uint64_t a = vr[s * St::kRow + r], b = vr[s * St::kRow + r + 1];
-      lo[s] = __builtin_amdgcn_alignbit((uint32_t)b, (uint32_t)a, sh);
-      hi[s] = __builtin_amdgcn_alignbit((uint32_t)(b >> 32), (uint32_t)(a >> 32), sh);
-    }
+    lds_u64* a = (lds_u64*)(row) + rot * St::kRow;
+    static_for<0, NT_BUNDLE>([&](auto si) {
+      constexpr int s = decltype(si)::value;
+      lds_u64* vr = rrow<s>(a, rot);
+      const uint64_t x = vr[r], y = vr[r + 1];
+      lo[s] = __builtin_amdgcn_alignbit((uint32_t)y, (uint32_t)x, sh);
+      hi[s] = __builtin_amdgcn_alignbit((uint32_t)(y >> 32), (uint32_t)(x >> 32), sh);
+    });
   }
 
   // both ranges' pieces of every slot (kNR = 2): plane words w, w + 1, w + 2
-  __device__ __forceinline__ static void cut2(const uint2* row, uint32_t sh, uint32_t (&lo)[kNR][32],
+  __device__ __forceinline__ static void cut2(const uint2* row, uint32_t sh, int rot, uint32_t (&lo)[kNR][32],
                                               uint32_t (&hi)[kNR][32]) {
-    typedef const volatile __attribute__((address_space(3))) uint64_t lds_u64;
-    lds_u64* vr = (lds_u64*)(row);
-#pragma unroll
-    for (int s = 0; s < NT_BUNDLE; ++s) {
-      const uint64_t a = vr[s * St::kRow], b = vr[s * St::kRow + 1], c = vr[s * St::kRow + 2];
-      lo[0][s] = __builtin_amdgcn_alignbit((uint32_t)b, (uint32_t)a, sh);
-      hi[0][s] = __builtin_amdgcn_alignbit((uint32_t)(b >> 32), (uint32_t)(a >> 32), sh);
-      lo[1][s] = __builtin_amdgcn_alignbit((uint32_t)c, (uint32_t)b, sh);
-      hi[1][s] = __builtin_amdgcn_alignbit((uint32_t)(c >> 32), (uint32_t)(b >> 32), sh);
-    }
+    lds_u64* a = (lds_u64*)(row) + rot * St::kRow;
+    static_for<0, NT_BUNDLE>([&](auto si) {
+      constexpr int s = decltype(si)::value;
+      lds_u64* vr = rrow<s>(a, rot);
+      const uint64_t x = vr[0], y = vr[1], z = vr[2];
+      lo[0][s] = __builtin_amdgcn_alignbit((uint32_t)y, (uint32_t)x, sh);
+      hi[0][s] = __builtin_amdgcn_alignbit((uint32_t)(y >> 32), (uint32_t)(x >> 32), sh);
+      lo[1][s] = __builtin_amdgcn_alignbit((uint32_t)z, (uint32_t)y, sh);
+      hi[1][s] = __builtin_amdgcn_alignbit((uint32_t)(z >> 32), (uint32_t)(y >> 32), sh);
+    });
   }
 
   // the first run (of the at most 4 a range's steps split into: prologue /
@@ -732,21 +810,22 @@ struct TWalkerL {
   // staged rows; w: the lane's first plane word, relative to the row start;
   // sh: its bit offset; first: the lane walks position -1 of the read;
   // cmask: 0 when the lane's last counted step is past its window (odd L, h = 1);
+  // rot: the lane's row rotation (TsRot; acc comes back in slot order);
   // issue(): called once the buffer has been read
   template <class Issue>
-  __device__ __forceinline__ void walk(const uint2* buf, int w, uint32_t sh, bool first, uint32_t cmask,
+  __device__ __forceinline__ void walk(const uint2* buf, int w, uint32_t sh, bool first, uint32_t cmask, int rot,
                                        uint32_t (&acc)[3][8], Issue&& issue) {
     pp.init();
     const uint2* row = buf + w;
     uint32_t plo[kNR][32], phi[kNR][32];
     if constexpr (kNR == 2) {
-      cut2(row, sh, plo, phi);  // (both ranges from the 3 words they span: a quarter fewer reads)
+      cut2(row, sh, rot, plo, phi);  // (both ranges from the 3 words they span: a quarter fewer reads)
     } else {
-      cut<0>(row, sh, plo[0], phi[0]);
+      cut<0>(row, sh, rot, plo[0], phi[0]);
     }
     static_for<0, kNR>([&](auto ri) {
       constexpr int r = decltype(ri)::value;
-      if constexpr (kNR != 2 && r + 1 < kNR) cut<r + 1>(row, sh, plo[r + 1], phi[r + 1]);
+      if constexpr (kNR != 2 && r + 1 < kNR) cut<r + 1>(row, sh, rot, plo[r + 1], phi[r + 1]);
       uint32_t (&lo)[32] = plo[r];
       uint32_t (&hi)[32] = phi[r];
       transpose32(lo);
@@ -779,10 +858,13 @@ struct TWalkerL {
         }
       });
     });
+    // bit s of the counters is slot (s + rot) mod 32: rotate them back
+    const uint32_t rsh = (uint32_t)(32 - rot) & 31u;
 #pragma unroll
     for (int p = 0; p < 3; ++p)
 #pragma unroll
-      for (int b = 0; b < 8; ++b) acc[p][b] = pp.bc[p].acc[b];
+      for (int b = 0; b < 8; ++b)
+        acc[p][b] = p < TP::kNP ? __builtin_amdgcn_alignbit(pp.bc[p].acc[b], pp.bc[p].acc[b], rsh) : 0u;
   }
 };
 
@@ -932,6 +1014,7 @@ __device__ __forceinline__ void tscan_bundles(const NtBatch& B, const NtOut& O, 
   const int wq = p0 >> 5;                        // (arithmetic: -1 for lane 0)
   const uint32_t sh = (uint32_t)(p0 & 31);
   const uint32_t cmask = (mh && (kL & 1)) ? 0u : 0xFFFFFFFFu;
+  const int rot = TsRot<kL, kLam, St::kRow>::of_lane(lane);  // this lane's row order in the cuts
   const uint64_t nb = B.n_bundles;
   uint32_t qi = blockIdx.x % NT_QUEUES, qtried = 0;
   auto claim = [&]() -> uint64_t {
@@ -1000,34 +1083,42 @@ __device__ __forceinline__ void tscan_bundles(const NtBatch& B, const NtOut& O, 
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint32_t*>(B.planes) + base * 2ull, (short)0, (int)(uint32_t)((top - base) * 8ull), 0x00020000);
     // the buffer's loads: row s piece c <- 16-byte units 64 c + lane of slot s
-    // (lanes past the row's end idle), voffset = the slot's planes (bytes from
-    // the descriptor base, lane s of pad_v) + the half stripe's first word +
-    // the unit, soffset = 0: the whole offset is in voffset, which the raw
-    // buffer's range check covers, so a short slot's rows past the bundle's
-    // last plane word (its half stripes beyond its read; at the planes
-    // allocation's end for the batch's last read) load zeros and never reach
-    // past the allocation (half stripe 0 starts 2 words before the reads: a
-    // slot at the descriptor base wraps past the range there and loads zeros)
+    // (lanes past the row's end idle), voffset = the unit (16 lane + 1024 c,
+    // one register for every slot), soffset = the slot's planes (bytes from
+    // the descriptor base, lane s of pad_v) + the half stripe's first word,
+    // M0 = the row's LDS address: no VALU a load.  The raw buffer's range
+    // check covers voffset + soffset (tools/fused_probe.hip k_soff: lane 32 of
+    // an in-range voffset with a soffset past the range loads 0), so a short
+    // slot's rows past the bundle's last plane word (its half stripes beyond
+    // its read; at the planes allocation's end for the batch's last read) load
+    // zeros and never reach past the allocation.  Half stripe 0 starts 2 words
+    // before the reads: that negative offset goes into voffset (the sum is not
+    // taken mod 2^32: a slot at the descriptor base loads zeros there)
     const uint32_t pad_v = sl[lane & (NT_BUNDLE - 1)].pad;
     // the buffer's LDS address, provably wave-uniform (the loads' M0)
     const uint32_t stage_lds = (uint32_t)__builtin_amdgcn_readfirstlane(
         (int)(uint32_t)(unsigned long)(__attribute__((address_space(3))) void*)stage);
     auto fetch = [&](int hs) {
       const int fw = St::first_word(hs);
-      const uint32_t vl = 16u * (uint32_t)lane + (uint32_t)(fw * 8);  // (mod 2^32: fw = -2 wraps)
+      const uint32_t vl = 16u * (uint32_t)lane + (fw < 0 ? (uint32_t)(fw * 8) : 0u);  // (mod 2^32)
+      const uint32_t so = fw < 0 ? 0u : (uint32_t)(fw * 8);
+      // (the M0 values summed here, on the scalar unit: hoisted out of the
+      // loop they were 32 SGPRs, spilled to VGPR lanes and read back a load)
+      uint32_t m0 = stage_lds;
+      asm volatile("" : "+s"(m0));
       // (the slots' offsets are read with every lane active: a lane the load's
       // mask leaves out has no defined value to read)
       uint32_t pad[NT_BUNDLE];
 #pragma unroll
-      for (int s = 0; s < NT_BUNDLE; ++s) pad[s] = (uint32_t)__builtin_amdgcn_readlane((int)pad_v, s);
+      for (int s = 0; s < NT_BUNDLE; ++s) pad[s] = (uint32_t)__builtin_amdgcn_readlane((int)pad_v, s) + so;
 #pragma unroll
       for (int c = 0; c < St::kLoads; ++c) {
         if (kWave * c + lane < St::kRowUnits) {
 #pragma unroll
           for (int s = 0; s < NT_BUNDLE; ++s)
             __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                rs, (__attribute__((address_space(3))) void*)(unsigned long)(stage_lds + 8u * (s * St::kRow + 2 * kWave * c)),
-                16, pad[s] + 1024u * c + vl, 0, 0, 0);
+                rs, (__attribute__((address_space(3))) void*)(unsigned long)(m0 + 8u * (s * St::kRow + 2 * kWave * c)),
+                16, 1024u * c + vl, pad[s], 0, 0);
         }
       }
     };
@@ -1054,7 +1145,7 @@ __device__ __forceinline__ void tscan_bundles(const NtBatch& B, const NtOut& O, 
         uint32_t acc[3][8];
         Wk wk;
         wk.walk(
-            stage, w, sh, hs == 0 && lane == 0, cmask, acc,
+            stage, w, sh, hs == 0 && lane == 0, cmask, rot, acc,
             [&]() {
               // (every read of the buffer has returned before a load may write it)
               asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");

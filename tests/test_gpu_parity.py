@@ -1139,7 +1139,7 @@ def test_bundle_spanning_more_than_2gib_is_reported(cfg, monkeypatch):
     assert nt.tscan
     t = _device_batch(nt, synth_params(read_len=read_len, first_read=300), n, read_len, hits=False)
     wpr = 2 * read_blocks(read_len)  # int32 plane words a read
-    far_blk = (1 << 28) + 2          # plane words of 8 bytes: 2 GiB + 16 B into the buffer
+    far_blk = (1 << 28) + 8192       # blocks of 8 bytes: 2 GiB + 64 KB into the buffer (> 2 GiB from the bundle base)
     big = torch.zeros(2 * far_blk + wpr + 64, dtype=torch.int32, device="cuda")
     big[:n * wpr].copy_(t["planes"])
     big[2 * far_blk:2 * far_blk + wpr].copy_(t["planes"][far * wpr:(far + 1) * wpr])
