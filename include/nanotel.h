@@ -48,6 +48,7 @@ extern "C" {
 #define NT_E_NOMEM (-8)
 #define NT_E_LIMIT (-9)       /* > 64 patterns, TVR > 64 letters, subseq_length > 43690 */
 #define NT_E_STATE (-10)      /* nt_compile() not called */
+#define NT_E_IO (-11)         /* an output file could not be written */
 
 /* summary flags per read */
 #define NT_ROW_TELOMERIC 0x01 /* row emitted: max telomere width >= 30 (NanoTel.R:1847) */
@@ -376,6 +377,20 @@ int nt_reader_count_files(nt_reader* r, const uint64_t* files, uint64_t n, uint6
 int nt_reader_plan(nt_reader* r, const uint64_t* files, uint64_t n);
 int nt_reader_seek(nt_reader* r, int mode, uint64_t a, uint64_t b);
 int nt_reader_stats(const nt_reader* r, uint64_t* out2);
+
+/* --- reads/<serial>.fasta.gz ---------------------------------------------
+ * writeXStringSet(current_seq, "<output_dir>/reads/<serial>.fasta.gz",
+ * compress = TRUE) for n telomeric reads (NanoTel.R:1869-1873): file i =
+ * '>' names[i], then seqs[i] in 80-column lines (rc[i] != 0: its reverse
+ * complement, Biostrings' letter pairs -- rc may be NULL), gzip as R's
+ * gzfile() writes it (deflate level `level`, R's default 6; mtime 0, OS 3).
+ * The files are written by `threads` host threads (<= 0: the library's
+ * default, at most 16, divided by LOCAL_WORLD_SIZE).  Returns NT_OK, or
+ * NT_E_IO with *err_index = the first read whose file failed (NT_E_LIMIT: a
+ * read of 4 Gbases or more). */
+int nt_write_fasta_gz(const char* const* paths, const char* const* names, const uint64_t* name_lens,
+                      const char* const* seqs, const uint64_t* seq_lens, const uint8_t* rc, uint64_t n,
+                      int32_t level, int32_t threads, uint64_t* err_index);
 
 /* --- synthetic long reads (bench / tests) --------------------------------- */
 int nt_synth_device(nt_ctx* ctx, const nt_synth_params* sp, uint64_t n_reads, uint32_t* planes_dev);

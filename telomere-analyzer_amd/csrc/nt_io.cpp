@@ -1300,3 +1300,130 @@ int nt_reader_stats(const nt_reader* r, uint64_t* out2) {
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------
+// reads/<serial>.fasta.gz: writeXStringSet(current_seq,
+// output_telo_fasta, compress = TRUE) per telomeric read (NanoTel.R:1869-1873)
+// -- '>' name, the sequence in 80-column lines, gzip through R's gzfile():
+// zlib deflate at level 6, raw stream (windowBits -15, memLevel 8, default
+// strategy), header with mtime 0, no flags, xfl 0, OS 3 (R's gzio.h), CRC-32
+// and size trailer.  The files are independent: a pool of host threads, one
+// text buffer, output buffer and deflate stream each (deflateReset between
+// files).  Level 6 on 2-bit-entropy text runs ~8-15 MB/s a core (zlib's lazy
+// matcher walks long hash chains on a 4-letter alphabet), so the writes are
+// bound by compression, not by formatting or the file system.
+namespace {
+
+struct RcTable {
+  uint8_t t[256];
+  RcTable() {
+    for (int i = 0; i < 256; ++i) t[i] = (uint8_t)i;
+    const char* a = "ACGTMRWSYKVHDBNacgtmrwsykvhdbn";
+    const char* b = "TGCAKYWSRMBDHVNtgcakywsrmbdhvn";
+    for (int i = 0; a[i]; ++i) t[(uint8_t)a[i]] = (uint8_t)b[i];
+  }
+};
+const RcTable kRcTable;  // Biostrings' complement of the DNA_ALPHABET letters; others kept
+
+struct GzWriter {
+  z_stream zs{};
+  int level = -1;
+  std::vector<uint8_t> text, out;
+  ~GzWriter() {
+    if (level >= 0) deflateEnd(&zs);
+  }
+  // the FASTA record of one read, compressed, written to path
+  bool write(const char* path, const char* name, uint64_t nl, const char* seq, uint64_t sl, bool rc, int lvl) {
+    const uint64_t lines = (sl + 79) / 80;
+    text.resize(1 + nl + 1 + sl + lines);
+    uint8_t* p = text.data();
+    *p++ = '>';
+    std::memcpy(p, name, nl);
+    p += nl;
+    *p++ = '\n';
+    for (uint64_t i = 0; i < sl; i += 80) {
+      const uint64_t k = std::min<uint64_t>(80, sl - i);
+      if (!rc) {
+        std::memcpy(p, seq + i, k);
+      } else {  // reverseComplement: position i of the written read is sl - 1 - i of the input
+        for (uint64_t j = 0; j < k; ++j) p[j] = kRcTable.t[(uint8_t)seq[sl - 1 - (i + j)]];
+      }
+      p += k;
+      *p++ = '\n';
+    }
+    const uint64_t tn = (uint64_t)(p - text.data());
+    if (level != lvl) {
+      if (level >= 0) deflateEnd(&zs);
+      zs = z_stream{};
+      if (deflateInit2(&zs, lvl, Z_DEFLATED, -MAX_WBITS, 8, Z_DEFAULT_STRATEGY) != Z_OK) {
+        level = -1;
+        return false;
+      }
+      level = lvl;
+    } else if (deflateReset(&zs) != Z_OK) {
+      return false;
+    }
+    out.resize(10 + deflateBound(&zs, (uLong)tn) + 8);
+    static const uint8_t kHead[10] = {0x1f, 0x8b, Z_DEFLATED, 0, 0, 0, 0, 0, 0, 3};
+    std::memcpy(out.data(), kHead, 10);
+    zs.next_in = text.data();
+    zs.avail_in = (uInt)tn;
+    zs.next_out = out.data() + 10;
+    zs.avail_out = (uInt)(out.size() - 18);
+    if (deflate(&zs, Z_FINISH) != Z_STREAM_END) return false;
+    uint64_t n = 10 + zs.total_out;
+    const uint32_t crc = (uint32_t)crc32(crc32(0L, Z_NULL, 0), text.data(), (uInt)tn);
+    const uint32_t isz = (uint32_t)tn;
+    for (int b = 0; b < 4; ++b) out[n + b] = (uint8_t)(crc >> (8 * b));
+    for (int b = 0; b < 4; ++b) out[n + 4 + b] = (uint8_t)(isz >> (8 * b));
+    n += 8;
+    const int fd = ::open(path, O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0666);
+    if (fd < 0) return false;
+    uint64_t w = 0;
+    while (w < n) {
+      const ssize_t k = ::write(fd, out.data() + w, n - w);
+      if (k <= 0) {
+        ::close(fd);
+        return false;
+      }
+      w += (uint64_t)k;
+    }
+    return ::close(fd) == 0;
+  }
+};
+
+}  // namespace
+
+extern "C" {
+
+int nt_write_fasta_gz(const char* const* paths, const char* const* names, const uint64_t* name_lens,
+                      const char* const* seqs, const uint64_t* seq_lens, const uint8_t* rc, uint64_t n,
+                      int32_t level, int32_t threads, uint64_t* err_index) {
+  if (n == 0) return NT_OK;
+  if (!paths || !names || !name_lens || !seqs || !seq_lens || level < 0 || level > 9) return NT_E_ARG;
+  for (uint64_t i = 0; i < n; ++i)  // (one deflate call a file: its text fits a uInt)
+    if (seq_lens[i] + seq_lens[i] / 80 + name_lens[i] + 3 >= (1ull << 32)) {
+      if (err_index) *err_index = i;
+      return NT_E_LIMIT;
+    }
+  unsigned nt = threads > 0 ? (unsigned)threads : host_threads();
+  nt = (unsigned)std::min<uint64_t>(nt, n);
+  std::atomic<uint64_t> next{0}, bad{~0ull};
+  par(nt, [&](unsigned) {
+    GzWriter g;
+    for (uint64_t i = next++; i < n; i = next++) {
+      if (!g.write(paths[i], names[i], name_lens[i], seqs[i], seq_lens[i], rc && rc[i], level)) {
+        uint64_t b = bad.load();
+        while (i < b && !bad.compare_exchange_weak(b, i)) {
+        }
+      }
+    }
+  });
+  if (bad.load() != ~0ull) {
+    if (err_index) *err_index = bad.load();
+    return NT_E_IO;
+  }
+  return NT_OK;
+}
+
+}  // extern "C"

@@ -1083,36 +1083,35 @@ __device__ __forceinline__ void tscan_bundles(const NtBatch& B, const NtOut& O, 
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint32_t*>(B.planes) + base * 2ull, (short)0, (int)(uint32_t)((top - base) * 8ull), 0x00020000);
     // the buffer's loads: row s piece c <- 16-byte units 64 c + lane of slot s
-    // (lanes past the row's end idle), voffset = the unit (16 lane + 1024 c,
-    // one register for every slot), soffset = the slot's planes (bytes from
-    // the descriptor base, lane s of pad_v) + the half stripe's first word,
-    // M0 = the row's LDS address: no VALU a load.  The raw buffer's range
-    // check covers voffset + soffset (tools/fused_probe.hip k_soff: lane 32 of
-    // an in-range voffset with a soffset past the range loads 0), so a short
-    // slot's rows past the bundle's last plane word (its half stripes beyond
-    // its read; at the planes allocation's end for the batch's last read) load
-    // zeros and never reach past the allocation.  Half stripe 0 starts 2 words
-    // before the reads: that negative offset goes into voffset (the sum is not
-    // taken mod 2^32: a slot at the descriptor base loads zeros there)
+    // (lanes past the row's end idle), voffset = the half stripe's first word
+    // + the unit (16 lane + 1024 c: one register for every slot), soffset =
+    // the slot's planes (bytes from the descriptor base, lane s of pad_v), M0
+    // = the row's LDS address: a load costs its soffset (v_readlane) and its
+    // M0 (s_add) besides itself.  The raw buffer's range check covers voffset
+    // + soffset (tools/fused_probe.hip k_soff: lane 32 of an in-range voffset
+    // with a soffset past the range loads 0), so a short slot's rows past the
+    // bundle's last plane word (its half stripes beyond its read; at the planes
+    // allocation's end for the batch's last read) load zeros and never reach
+    // past the allocation.  Half stripe 0 starts 2 words before the reads:
+    // voffset wraps for lane 0 there, which then loads zeros or the 16 bytes
+    // before the read (positions -64 .. -1, masked in the walk's prologue)
     const uint32_t pad_v = sl[lane & (NT_BUNDLE - 1)].pad;
     // the buffer's LDS address, provably wave-uniform (the loads' M0)
     const uint32_t stage_lds = (uint32_t)__builtin_amdgcn_readfirstlane(
         (int)(uint32_t)(unsigned long)(__attribute__((address_space(3))) void*)stage);
     auto fetch = [&](int hs) {
-      const int fw = St::first_word(hs);
-      const uint32_t vl = 16u * (uint32_t)lane + (fw < 0 ? (uint32_t)(fw * 8) : 0u);  // (mod 2^32)
-      const uint32_t so = fw < 0 ? 0u : (uint32_t)(fw * 8);
+      const uint32_t vl = 16u * (uint32_t)lane + (uint32_t)(St::first_word(hs) * 8);  // (mod 2^32)
       // (the M0 values summed here, on the scalar unit: hoisted out of the
       // loop they were 32 SGPRs, spilled to VGPR lanes and read back a load)
       uint32_t m0 = stage_lds;
       asm volatile("" : "+s"(m0));
-      // (the slots' offsets are read with every lane active: a lane the load's
-      // mask leaves out has no defined value to read)
-      uint32_t pad[NT_BUNDLE];
-#pragma unroll
-      for (int s = 0; s < NT_BUNDLE; ++s) pad[s] = (uint32_t)__builtin_amdgcn_readlane((int)pad_v, s) + so;
 #pragma unroll
       for (int c = 0; c < St::kLoads; ++c) {
+        // (the slots' offsets are read with every lane active: a lane the
+        // load's mask leaves out has no defined value to read)
+        uint32_t pad[NT_BUNDLE];
+#pragma unroll
+        for (int s = 0; s < NT_BUNDLE; ++s) pad[s] = (uint32_t)__builtin_amdgcn_readlane((int)pad_v, s);
         if (kWave * c + lane < St::kRowUnits) {
 #pragma unroll
           for (int s = 0; s < NT_BUNDLE; ++s)

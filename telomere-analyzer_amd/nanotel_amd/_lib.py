@@ -13,7 +13,7 @@ NT_OK = 0
 ERRORS = {
     -1: "NT_E_ARG", -2: "NT_E_PATTERN", -3: "NT_E_LETTER", -4: "NT_E_EMPTY_READ",
     -5: "NT_E_RIGHT_EMPTY", -6: "NT_E_NEG_WIDTH", -7: "NT_E_HIP", -8: "NT_E_NOMEM",
-    -9: "NT_E_LIMIT", -10: "NT_E_STATE",
+    -9: "NT_E_LIMIT", -10: "NT_E_STATE", -11: "NT_E_IO",
 }
 
 ROW_TELOMERIC = 0x01
@@ -136,6 +136,8 @@ SIGNATURES = {
     "nt_reader_plan": (ctypes.c_int, [_P, _P, ctypes.c_uint64]),
     "nt_reader_seek": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64]),
     "nt_reader_stats": (ctypes.c_int, [_P, _U64P]),
+    "nt_write_fasta_gz": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, ctypes.c_uint64, ctypes.c_int32, ctypes.c_int32,
+                                         _U64P]),
     "nt_synth_device": (ctypes.c_int, [_P, ctypes.POINTER(NtSynthParams), ctypes.c_uint64, _P]),
     "nt_rc_device": (ctypes.c_int, [_P, _P, _P, _P, _P, ctypes.c_uint64]),
     "nt_uniform_layout_device": (ctypes.c_int, [_P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int32,

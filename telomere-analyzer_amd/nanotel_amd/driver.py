@@ -15,6 +15,7 @@ only.  --analysis writes the filtered/sorted summary and the results text
 (analysis.py).  Every telomeric read gets the reference's three density plots
 (plots.py: single_read_plots*/read<serial>.jpeg|eps) unless plot=False.
 """
+import ctypes
 import math
 import os
 import time
@@ -23,9 +24,9 @@ from concurrent.futures import ThreadPoolExecutor
 import numpy as np
 
 from . import plots, shard
-from .analysis import write_analysis
+from .analysis import _keep_first, write_analysis
 from .api import NanoTel, rows_columns, rows_csv
-from .io import Reader, csv_field, format_double, format_int, r_as_character, write_fasta_gz
+from .io import Reader, csv_field, format_double, format_int, r_as_character, write_fasta_gz, write_fasta_gz_batch
 from .runlog import RunLog, r_time
 from . import __version__
 
@@ -81,40 +82,109 @@ class ChunkRows:
         return int(self.cols["serial"].size)
 
 
-class SummaryRows:
-    """The run's rows (ChunkRows in chunk order): len(), the columns of the
-    data frame (NA as NaN) and, for --analysis, the rows as Python lists."""
+def _chunk_payload(rows, lengths):
+    """What a rank sends rank 0 for one of its chunks, once its group round is
+    done: the rows' summary.csv and reads_ids.txt bytes, and for run.log the
+    value counts of the chunk's read lengths and of its rows' length / width
+    columns (not the columns: rank 0 never holds a run's rows).  rows: a
+    ChunkRows, or None when --use_filter kept no read of the chunk."""
+    from .runlog import ValueCounts
+    p = {"lengths": ValueCounts().add(lengths), "csv": b"", "ids": b"", "n": 0}
+    if rows is not None and len(rows):
+        c = rows.cols
+        p.update(csv=rows.csv, ids=rows.ids, n=len(rows), row_len=ValueCounts().add(c["length"]))
+        w = []
+        for q in range(c["width"].shape[0]):
+            v = c["width"][q].astype(np.float64)
+            v[c["na"][q]] = np.nan
+            w.append(ValueCounts().add(v))
+        p["width"] = w
+    return p
 
-    def __init__(self, chunks, n_pass):
-        self.chunks, self.n_pass = [c for c in chunks if c is not None], n_pass
+
+class SummarySink:
+    """Rank 0's end of the row stream: every group round's chunks arrive in
+    chunk order and are appended to <basename>_summary.csv and reads_ids.txt
+    (written as *.partial, renamed when the run succeeds: the reference writes
+    them at the end, NanoTel.R:2430-2433, so a failed run leaves none); run.log
+    gets its summaries from value counts (len(), column()).  Memory: one group
+    round's rows at a time, plus the rows --analysis keeps (those passing its
+    first filter, NanoTel.R:2442-2443)."""
+
+    def __init__(self, save_path, barcode, tvr, n_pass, analysis=False):
+        from .runlog import ValueCounts
+        self.n_pass = n_pass
+        self.paths = (os.path.join(save_path, f"{barcode}_summary.csv"), os.path.join(save_path, "reads_ids.txt"))
+        self._csv = open(self.paths[0] + ".partial", "wb")
+        self._ids = open(self.paths[1] + ".partial", "wb")
+        self._csv.write((",".join(columns(tvr)) + "\n").encode())  # write_csv's header
+        self.lengths, self.row_len = ValueCounts(), ValueCounts()
+        self.width = [ValueCounts() for _ in range(n_pass)]
+        self.n_rows = 0
+        self.kept = [] if analysis else None
+        self.rounds, self.max_round_bytes, self._round = 0, 0, 0
+
+    def end_round(self):
+        """A group round's rows are in: the most row bytes one round brought."""
+        self.rounds += 1
+        self.max_round_bytes = max(self.max_round_bytes, self._round)
+        self._round = 0
+
+    def add(self, p):
+        self._round += len(p["csv"]) + len(p["ids"])
+        self._csv.write(p["csv"])
+        self._ids.write(p["ids"])
+        self.lengths.add(p["lengths"])
+        if p["n"]:
+            self.n_rows += p["n"]
+            self.row_len.add(p["row_len"])
+            for q in range(self.n_pass):
+                self.width[q].add(p["width"][q])
+            if self.kept is not None:
+                self.kept += [r for r in _csv_rows(p["csv"], p["ids"], self.n_pass) if _keep_first(r)]
 
     def __len__(self):
-        return sum(len(c) for c in self.chunks)
+        return self.n_rows
 
     def column(self, key, p=None):
-        """A column over all rows as float64 (pass p's for the per-pass ones; NA -> NaN)."""
-        if not self.chunks:
-            return np.zeros(0)
-        if p is None:
-            return np.concatenate([c.cols[key] for c in self.chunks]).astype(np.float64)
-        v = np.concatenate([c.cols[key][p] for c in self.chunks]).astype(np.float64)
-        v[np.concatenate([c.cols["na"][p] for c in self.chunks])] = np.nan
-        return v
+        """run.log's columns as value counts: length (the rows' read lengths),
+        width (pass p's telomere lengths, NA for a pass without one)."""
+        return self.row_len if key == "length" else self.width[p]
 
     def rows(self):
-        """The rows as [Serial, sequence_ID, sequence_length, (density, start,
-        end, length) per pass], None for NA (--analysis)."""
-        out = []
-        for c in self.chunks:
-            names = c.ids.decode("utf-8", "replace").split("\n")
-            k = c.cols
-            for i in range(len(c)):
-                row = [float(k["serial"][i]), names[i], int(k["length"][i])]
-                for p in range(self.n_pass):
-                    row += [None] * 4 if k["na"][p, i] else [float(k["density"][p, i]), int(k["start"][p, i]),
-                                                            int(k["end"][p, i]), int(k["width"][p, i])]
-                out.append(row)
-        return out
+        """The rows --analysis keeps (its first filter applied)."""
+        return self.kept
+
+    def finish(self, ok):
+        self._csv.close()
+        self._ids.close()
+        for f in self.paths:
+            if ok:
+                os.replace(f + ".partial", f)
+            else:
+                os.remove(f + ".partial")
+
+
+def _csv_rows(csv, ids, n_pass):
+    """summary.csv lines back into rows [Serial, sequence_ID, sequence_length,
+    (density, start, end, length) per pass], None for NA: --analysis reads
+    what was written (the numbers round-trip: shortest round-trip doubles)."""
+    names = ids.decode("utf-8", "replace").split("\n")
+    out = []
+    for i, line in enumerate(csv.decode("utf-8", "replace").split("\n")[:-1]):
+        f = _split_csv_line(line)
+        row = [float(f[0]), names[i], int(f[2])]
+        for k in range(n_pass):
+            d, a, e, w = f[3 + 4 * k:7 + 4 * k]
+            row += [None] * 4 if d == "NA" else [float(d), int(a), int(e), int(w)]
+        out.append(row)
+    return out
+
+
+def _split_csv_line(line):
+    """Fields of one write_csv line (a sequence_ID may be quoted, with "" for ")."""
+    import csv as _csv
+    return next(_csv.reader([line]))
 
 
 def format_row(row, sci_threshold=None):
@@ -154,10 +224,10 @@ def _write_run_log(save_path, t0, input_path, files, patterns, tvr_patterns, rc,
     log.print("The input files:")
     for p in (files if os.path.isdir(input_path) else [input_path]):
         log.print(p)
-    n = int(lengths.size)
+    n = lengths.n
     log.print(f"Total reads in sample: {n}")
     log.print("Summary statistics of the sample reads length:")
-    log.summary(np.asarray(lengths))
+    log.summary(lengths)
     log.print(f"Number of reads which identified as Telomeric: {len(rows)}")
     pct = r_as_character(round(100 * len(rows) / n, 2)) if n else "NaN"
     log.print(f"% of total reads: {pct}%")
@@ -173,6 +243,20 @@ def _write_run_log(save_path, t0, input_path, files, patterns, tvr_patterns, rc,
         log.summary(rows.column("width", 2))
     log.print(f"Work ended at: {r_time()}")
     log.close()  # log_close(footer = FALSE)
+
+
+def _peak_rss_kb():
+    """This process's peak resident set (VmHWM: per address space, so a
+    spawned rank reports its own, not its parent's as ru_maxrss would)."""
+    try:
+        with open("/proc/self/status") as f:
+            for line in f:
+                if line.startswith("VmHWM:"):
+                    return int(line.split()[1])
+    except OSError:
+        pass
+    import resource
+    return resource.getrusage(resource.RUSAGE_SELF).ru_maxrss
 
 
 def _write_read(path, name, seq, rc):
@@ -246,12 +330,13 @@ class _LazyNames(dict):
         return v
 
 
-def _scan_group(nt, chunks, use_filter, write_reads, log, want_windows=False):
+def _scan_group(nt, chunks, use_filter, log, want_windows=False):
     """Scan + call the reads of several chunks in as few device calls as
     possible -- one per kGroupBases bases (after --use_filter, per chunk, when
     on).  Returns per chunk (rel_serials, row_order, rel_max, result view,
-    name_of(j), lengths, {read: seq}) over the reads that were scanned;
-    rel_max is shard.SKIPPED for a chunk that --use_filter emptied."""
+    name_of(j), lengths) over the reads that were scanned (the view holds the
+    reads' name and sequence addresses in the reader's chunk buffers); rel_max
+    is shard.SKIPPED for a chunk that --use_filter emptied."""
     parts = []
     for ch in chunks:
         idx = np.arange(ch.n)
@@ -279,7 +364,7 @@ def _scan_group(nt, chunks, use_filter, write_reads, log, want_windows=False):
         for ch, idx in call:
             b = a + idx.size
             if idx.size == 0:
-                out.append((None, np.zeros(0, np.int64), shard.SKIPPED, None, None, lens[:0], {}))
+                out.append((None, np.zeros(0, np.int64), shard.SKIPPED, None, None, lens[:0]))
                 continue
             v = _View({k: res[k][a:b] for k in ("start", "end", "density", "flags", "width", "telomeric")
                        if k in res})
@@ -288,10 +373,10 @@ def _scan_group(nt, chunks, use_filter, write_reads, log, want_windows=False):
                     res["win_counts"]
             np_, nl_ = ch.name_pointers()
             v["name_ptrs"], v["name_lens"] = np_[idx], nl_[idx]
+            v["seq_ptrs"] = ch.pointers()[idx]
             rel, order, rmax = shard.chunk_relative(v["telomeric"])
             name_of = (lambda c, ix: (lambda j: c.name(int(ix[j]))))(ch, idx)
-            seqs = {int(j): ch.seq(int(idx[int(j)])) for j in order} if write_reads else {}
-            out.append((rel, order, rmax, v, name_of, lens[a:b], seqs))
+            out.append((rel, order, rmax, v, name_of, lens[a:b]))
             a = b
     return out
 
@@ -384,8 +469,10 @@ def run(input_path, save_path, patterns, fmt="fastq", nrec=10000, rc=False, min_
         subseq_length=100, check_right_edge=False, tvr_patterns=None, legacy_no_ext=False,
         device=0, write_reads=True, sci_threshold=None, use_filter=False, analysis=False,
         plot=True, plot_jpeg=True, log=print, stats=None):
-    """Run the pipeline; returns (summary rows, all read lengths) on rank 0.
-    stats: a dict filled with the run's phase times (seconds)."""
+    """Run the pipeline; returns (the run's SummarySink: len() = rows, the
+    run.log columns as value counts; the read lengths' value counts) on rank
+    0, (None, None) elsewhere.  stats: a dict filled with the run's phase
+    times (seconds)."""
     import torch.distributed as dist
     dist_on = dist.is_available() and dist.is_initialized()
     rank = dist.get_rank() if dist_on else 0
@@ -429,8 +516,8 @@ def run(input_path, save_path, patterns, fmt="fastq", nrec=10000, rc=False, min_
     writers = ThreadPoolExecutor(min(16, os.cpu_count() or 1)) if (write_reads or plot) else None
     plotters = None  # worker processes for the plots of large chunks (Python drawing holds the GIL)
     pending = []
-    lengths_own = {}  # chunk -> read lengths (uint32), gathered to rank 0 for run.log
-    local_rows = {}
+    barcode = os.path.basename(os.path.normpath(os.path.abspath(input_path)))
+    sink = SummarySink(save_path, barcode, tvr, nt.n_pass, analysis) if rank == 0 else None
     held = None  # (chunk, read args, plot job) of this rank's last -Inf row (see _targets)
     k = 0  # global chunk index of the group's first chunk
     s_next, m_run = 1.0, shard.NEG_INF  # serial_start of the next chunk, running max(Serial)
@@ -467,9 +554,8 @@ def run(input_path, save_path, patterns, fmt="fastq", nrec=10000, rc=False, min_
                     n_grp += 1
             for pos, ch in own:
                 log(f"processing chunk {k + pos + 1} ...")
-                lengths_own[k + pos] = ch.lengths.astype(np.uint32)
             ts = time.perf_counter()
-            scanned = _scan_group(nt, [ch for _, ch in own], use_filter, write_reads, log, want_windows=plot)
+            scanned = _scan_group(nt, [ch for _, ch in own], use_filter, log, want_windows=plot)
             tm["scan"] += time.perf_counter() - ts
         except Exception as ex:  # noqa: BLE001 -- re-raised after the collective
             failure, scanned = ex, []
@@ -483,16 +569,17 @@ def run(input_path, save_path, patterns, fmt="fastq", nrec=10000, rc=False, min_
         for r in range(n_grp):  # the reference's recurrence, chunk by chunk
             starts[r], s_next, m_run = shard.advance(s_next, m_run, float(maxima[r]))
         tw = time.perf_counter()
+        payload = {}  # this group's chunks, for rank 0
         try:
-            for (pos, _), (rel, order, _, res, name_of, lens, seqs) in zip(own, scanned):
-                if res is None:
-                    local_rows[k + pos] = None  # --use_filter kept no read of this chunk
+            for (pos, ch), (rel, order, _, res, name_of, lens) in zip(own, scanned):
+                if res is None:  # --use_filter kept no read of this chunk
+                    payload[k + pos] = _chunk_payload(None, ch.lengths)
                     continue
                 ser = shard.assign_chunk_serials(rel, starts[pos])
                 cols = rows_columns(res, lens, ser, order, nt.n_pass)
                 csv, ids = rows_csv(cols, res["name_ptrs"][order], res["name_lens"][order], nt.n_pass,
                                     sci_threshold)
-                local_rows[k + pos] = ChunkRows(csv, ids, cols)
+                payload[k + pos] = _chunk_payload(ChunkRows(csv, ids, cols), ch.lengths)
                 names = _LazyNames(name_of)
                 for f in pending:  # the previous chunk's files (errors surface here)
                     f.result()
@@ -501,11 +588,13 @@ def run(input_path, save_path, patterns, fmt="fastq", nrec=10000, rc=False, min_
                 jobs = _plot_jobs(nt, res, order, lens, ser, save_path) if plot else []
                 job_of = {int(j): jb for j, jb in zip(_plot_rows(res, order), jobs)} if plot else {}
                 if last_inf is not None:
-                    held = (k + pos, (names[last_inf], seqs.get(last_inf), rc), job_of.get(last_inf))
-                if write_reads:
-                    pending += [writers.submit(_write_read, os.path.join(
-                        reads_dir, f"{r_as_character(float(ser[j]))}.fasta.gz"), names[j], seqs[j], rc)
-                        for j in now]
+                    seq = ctypes.string_at(int(res["seq_ptrs"][last_inf]), int(lens[last_inf])) if write_reads else None
+                    held = (k + pos, (names[last_inf], seq, rc), job_of.get(last_inf))
+                if write_reads and now:  # one library call a chunk: formatting + gzip on the host threads
+                    sel = np.asarray(now, np.int64)
+                    paths = [os.path.join(reads_dir, f"{r_as_character(float(ser[j]))}.fasta.gz") for j in now]
+                    pending.append(writers.submit(write_fasta_gz_batch, paths, res["name_ptrs"][sel],
+                                                  res["name_lens"][sel], res["seq_ptrs"][sel], lens[sel], rc))
                 if plot:
                     jobs = [job_of[j] for j in now if j in job_of]
                     if len(jobs) >= 64 and plotters is None:
@@ -515,6 +604,16 @@ def run(input_path, save_path, patterns, fmt="fastq", nrec=10000, rc=False, min_
         except Exception as ex:  # noqa: BLE001
             failure = ex
         tm["rows_files"] += time.perf_counter() - tw
+        # the group's rows to rank 0 now, in chunk order (every rank joins, a
+        # failed one with what it has: the next round's exchange stops them all)
+        tc = time.perf_counter()
+        parts = shard.gather_chunks(payload)
+        del payload
+        if sink is not None:
+            for p in parts:
+                sink.add(p)
+            sink.end_round()
+        tm["collectives"] += time.perf_counter() - tc
         k += n_grp
         if ended:
             break
@@ -540,12 +639,12 @@ def run(input_path, save_path, patterns, fmt="fastq", nrec=10000, rc=False, min_
     if shard.any_rank(failure is not None, device=coll_dev):
         rdr.close()
         nt.close()
+        if sink is not None:
+            sink.finish(False)
         if failure is not None:
             raise failure
         raise RuntimeError("NanoTel: another rank failed (see its error)")
     t_end = time.time()
-    rows = SummaryRows(shard.gather_chunks(local_rows) or [], nt.n_pass)
-    lengths_all = shard.gather_chunks(lengths_own)
     if stats is not None:
         stats.update(tm)
         stats["ingest"] = plan.mode or "unsharded"
@@ -553,6 +652,9 @@ def run(input_path, save_path, patterns, fmt="fastq", nrec=10000, rc=False, min_
         stats["bytes_parsed"], stats["bytes_inflated"] = rdr.stats()
         stats.update({"host_" + k: v for k, v in nt.host_times().items()} if hasattr(nt, "host_times") else {})
         stats["groups_rounds"] = g
+        stats["peak_rss_kb"] = _peak_rss_kb()
+        if sink is not None:
+            stats["rows_rounds"], stats["rows_max_round_bytes"] = sink.rounds, sink.max_round_bytes
     tc = time.time()
     rdr.close()
     tc2 = time.time()
@@ -562,20 +664,13 @@ def run(input_path, save_path, patterns, fmt="fastq", nrec=10000, rc=False, min_
         stats["final_close_ctx"] = time.time() - tc2
     if rank != 0:
         return None, None
-    lengths = np.concatenate(lengths_all) if lengths_all else np.zeros(0, np.uint64)
-    barcode = os.path.basename(os.path.normpath(os.path.abspath(input_path)))
-    with open(os.path.join(save_path, f"{barcode}_summary.csv"), "wb") as f:  # write_csv (NanoTel.R:2430-2432)
-        f.write((",".join(columns(tvr)) + "\n").encode())
-        for c in rows.chunks:
-            f.write(c.csv)
-    with open(os.path.join(save_path, "reads_ids.txt"), "wb") as f:  # write_lines (NanoTel.R:2433)
-        for c in rows.chunks:
-            f.write(c.ids)
+    # write_csv / write_lines (NanoTel.R:2430-2433): streamed, complete now
+    sink.finish(True)
     if analysis:  # --analysis post-processing (NanoTel.R:2437-2508)
-        write_analysis(save_path, barcode, rows.rows(), columns(tvr), format_row, sci_threshold)
+        write_analysis(save_path, barcode, sink.rows(), columns(tvr), format_row, sci_threshold)
     _write_run_log(save_path, t0, input_path, files, patterns, tvr_patterns, rc, subseq_length, min_density,
-                   lengths, rows, tvr)
+                   sink.lengths, sink, tvr)
     if stats is not None:
         stats["final"] = time.time() - t_end
         stats["total"] = time.time() - t0
-    return rows, lengths
+    return sink, sink.lengths

@@ -243,6 +243,36 @@ def r_as_character(x):
     return fixed_s if len(fixed_s) <= len(sci_s) else sci_s
 
 
+GZIP_LEVEL = 6  # R's gzfile() default (writeXStringSet compress = TRUE)
+
+
+def write_fasta_gz_batch(paths, name_ptrs, name_lens, seq_ptrs, seq_lens, rc=False, level=None, threads=0):
+    """reads/<serial>.fasta.gz of many reads in one library call
+    (nt_write_fasta_gz: formatting, reverse complement and gzip in C++ on the
+    host threads; the GIL is dropped).  name/seq: host addresses and lengths
+    (the reader's chunk buffers, valid while the chunk is kept); rc: write the
+    reverse complements (--rc).  level: NT_GZIP_LEVEL, else 6."""
+    import numpy as np
+    from ._lib import NanoTelError, lib
+    n = len(paths)
+    if n == 0:
+        return
+    if level is None:
+        level = int(os.environ.get("NT_GZIP_LEVEL", GZIP_LEVEL))
+    pb = [os.fsencode(p) for p in paths]
+    parr = (ctypes.c_char_p * n)(*pb)
+    arrs = [np.ascontiguousarray(a, np.uint64) for a in (name_ptrs, name_lens, seq_ptrs, seq_lens)]
+    rcv = np.full(n, 1 if rc else 0, np.uint8)
+    bad = ctypes.c_uint64(0)
+    e = lib().nt_write_fasta_gz(ctypes.cast(parr, ctypes.c_void_p), arrs[0].ctypes.data, arrs[1].ctypes.data,
+                                arrs[2].ctypes.data, arrs[3].ctypes.data, rcv.ctypes.data, n, int(level),
+                                int(threads), ctypes.byref(bad))
+    if e == -11:
+        raise OSError(f"NanoTel: cannot write {paths[bad.value]}")
+    if e != 0:
+        raise NanoTelError(e, f"nt_write_fasta_gz ({paths[bad.value] if bad.value < n else ''})")
+
+
 def write_fasta_gz(path, name, seq, width=80):
     """writeXStringSet(x, path, compress = TRUE): '>' name, 80-column lines,
     gzip at R's gzfile() default level 6.  One buffer, one zlib call (which

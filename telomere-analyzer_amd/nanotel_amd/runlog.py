@@ -81,9 +81,68 @@ def _zapsmall(v, digits):
     return [round(x, d) if math.isfinite(x) else x for x in v]
 
 
+class ValueCounts:
+    """A numeric column kept as its distinct values and their counts (plus an
+    NA count), merged chunk by chunk: summary() of a column of 10^8 reads
+    without holding it.  Integral values (read and telomere lengths) make the
+    mean exact: their sum is an exact integer below 2^53."""
+
+    def __init__(self):
+        self.vals = np.zeros(0, np.float64)
+        self.cnts = np.zeros(0, np.int64)
+        self.na = 0
+
+    def add(self, x):
+        """x: array (NaN = NA) or another ValueCounts."""
+        if isinstance(x, ValueCounts):
+            v, c, na = x.vals, x.cnts, x.na
+        else:
+            v = np.asarray(x, np.float64)
+            nan = np.isnan(v)
+            na = int(nan.sum())
+            v, c = np.unique(v[~nan], return_counts=True)
+        self.na += na
+        if v.size:
+            u, inv = np.unique(np.concatenate([self.vals, v]), return_inverse=True)
+            self.cnts = np.bincount(inv, weights=np.concatenate([self.cnts, c]), minlength=u.size).astype(np.int64)
+            self.vals = u
+        return self
+
+    @property
+    def n(self):
+        return int(self.cnts.sum())
+
+    def order_stat(self, i):
+        """The i-th smallest value (0-based) of the column without its NAs."""
+        return float(self.vals[int(np.searchsorted(np.cumsum(self.cnts), i, side="right"))])
+
+    def quantile(self, q):
+        """np.quantile(column, q) (method 'linear' = R's type 7), same arithmetic."""
+        n = self.n
+        h = (n - 1) * q
+        lo = math.floor(h)
+        a, b = self.order_stat(lo), self.order_stat(min(lo + 1, n - 1))
+        t = h - lo
+        d = b - a
+        return b - d * (1.0 - t) if t >= 0.5 else a + d * t
+
+    def mean(self):
+        """np.mean of the column: for integral values its pairwise float64 sum
+        is the exact integer sum (below 2^53), as here"""
+        if np.all(self.vals == np.round(self.vals)) and np.abs(self.vals).max(initial=0) < 2 ** 31:
+            return float(int(np.dot(self.vals.astype(np.int64), self.cnts))) / self.n
+        return float(np.dot(self.vals, self.cnts)) / self.n
+
+
 def r_summary(x):
     """summary(x) of a numeric vector: (names, values, NA count) -- Min, the
     type-7 quartiles, median, mean, max; NA's when x holds NAs."""
+    if isinstance(x, ValueCounts):
+        names = ["Min.", "1st Qu.", "Median", "Mean", "3rd Qu.", "Max."]
+        if x.n == 0:
+            return names, [None, None, None, float("nan"), None, None], x.na
+        q = [x.quantile(p) for p in (0, 0.25, 0.5, 0.75, 1.0)]
+        return names, [q[0], q[1], q[2], x.mean(), q[3], q[4]], x.na
     if isinstance(x, np.ndarray):  # (NA as NaN): no per-element Python work for millions of reads
         v = x.astype(np.float64, copy=False)
     else:

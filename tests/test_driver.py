@@ -506,3 +506,92 @@ def test_dist_backend_choice():
     assert dist_backend(1, 1, None, 8, env={}) == "gloo"
     assert dist_backend(8, 8, None, 8, env={"NT_DIST_BACKEND": "gloo"}) == "gloo"
     assert dist_backend(1, 1, None, 1, env={"NT_DIST_BACKEND": "nccl"}) == "nccl"
+
+
+class FastNanoTel:
+    """Test double of nanotel_amd.NanoTel for the row stream at scale: rows
+    computed from the read lengths alone (vectorised), so that a gloo run of
+    10^6 rows takes seconds.  Two thirds of the reads are telomeric; pass 1
+    is NA for one read in eleven."""
+
+    def __init__(self, patterns, tvr_patterns=None, subseq_length=100, min_density=0.6,
+                 check_right_edge=False, rc=False, legacy_no_ext=False, device=0):
+        self.n_pass = 3 if tvr_patterns else 2
+        self.subseq_length = subseq_length
+
+    def analyze_pointers(self, ptrs, lens, want_windows=False):
+        n = lens.size
+        ln = lens.astype(np.int64)
+        st = np.full((n, 3), -1, np.int32)
+        en = np.full((n, 3), -1, np.int32)
+        st[:, :2] = (1 + ln % 7)[:, None]
+        en[:, :2] = (ln - ln % 5)[:, None]
+        na = ln % 11 == 0
+        st[na, 0] = en[na, 0] = -1
+        dens = np.zeros((n, 3))
+        dens[:, :2] = ((ln % 97) / 97.0)[:, None]
+        return {"start": st, "end": en, "density": dens, "telomeric": ln % 3 != 0}
+
+    def close(self):
+        pass
+
+
+def _big_rank(rank, world, port, inp, out, stats_dir):
+    import json
+    import torch.distributed as dist
+    from nanotel_amd import driver
+    driver.NanoTel = FastNanoTel
+    if world > 1:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    st = {}
+    driver.run(inp, out, "TTAGGG", fmt="fasta", nrec=2000, write_reads=False, plot=False,
+               log=lambda *a: None, stats=st)
+    with open(os.path.join(stats_dir, f"big_{world}_{rank}.json"), "w") as f:
+        json.dump({k: v for k, v in st.items() if isinstance(v, (int, float, str))}, f)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(900)
+def test_row_stream_million_rows_identical_across_world_sizes(tmp_path):
+    """the rows go to rank 0 group round by group round (no
+    end-of-run gather of every row).  1.2 M reads, >= 10^6 rows: world 2 and 8
+    (gloo) write summary.csv / reads_ids.txt byte-identical to world 1, rank 0
+    never receives more than one round's rows at a time, and every rank's peak
+    RSS is recorded (stats JSON beside the outputs)."""
+    import json
+    import torch.multiprocessing as mp
+    rng = np.random.default_rng(123)
+    n = 1_560_000
+    lens = rng.integers(40, 130, n)
+    inp = tmp_path / "big.fasta"
+    with open(inp, "wb") as f:
+        seq = b"ACGT" * 40
+        f.write(b"".join(b">r%d x\n%s\n" % (i, seq[:int(k)]) for i, k in enumerate(lens)))
+    n_rows = int((lens % 3 != 0).sum())
+    assert n_rows >= 1_000_000
+    outs, st = {}, {}
+    for world in (1, 2, 8):
+        out = tmp_path / f"out{world}"
+        if world == 1:
+            _big_rank(0, 1, 0, str(inp), str(out), str(tmp_path))
+        else:
+            mp.start_processes(_big_rank, args=(world, _free_port(), str(inp), str(out), str(tmp_path)),
+                               nprocs=world, join=True, start_method="spawn")
+        outs[world] = {f: (out / f).read_bytes() for f in ("big.fasta_summary.csv", "reads_ids.txt")}
+        st[world] = [json.load(open(tmp_path / f"big_{world}_{r}.json")) for r in range(world)]
+    assert outs[1]["big.fasta_summary.csv"].count(b"\n") == n_rows + 1
+    for world in (2, 8):
+        assert outs[world] == outs[1], world
+    total = sum(len(v) for v in outs[1].values())
+    for world in (1, 2, 8):
+        s0 = st[world][0]
+        assert s0["rows_rounds"] >= 3, s0  # several rounds ...
+        assert s0["rows_max_round_bytes"] <= total // 2, s0  # ... none holding the run's rows
+        print(f"world {world}: rank-0 peak RSS {s0['peak_rss_kb'] / 1024:.0f} MiB, "
+              f"{s0['rows_rounds']} rounds, at most {s0['rows_max_round_bytes'] / 2**20:.1f} MiB of rows a round "
+              f"(of {total / 2**20:.1f} MiB); other ranks' peak RSS "
+              f"{[round(x['peak_rss_kb'] / 1024) for x in st[world][1:]]} MiB")

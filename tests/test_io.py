@@ -406,3 +406,39 @@ def test_fastq_fast_path_matches_line_parser(tmp_path, monkeypatch):
             assert fast == slow, (key, nrec)
         rejected = ("malformed", "wrapped_to_length", "crlf_short", "big_wrapped_to_length")
         assert (slow[1] is not None) == (key in rejected), (key, slow[1])
+
+
+def test_write_fasta_gz_batch_matches_python_writer(tmp_path):
+    """nt_write_fasta_gz (reads/<serial>.fasta.gz in C++, NanoTel.R:1869-1873)
+    against the Python writer: the same FASTA text (80-column lines, the
+    reverse complement under --rc with Biostrings' IUPAC pairs), gzip with R's
+    gzfile header (mtime 0, OS 3) at level 6; an unwritable path raises."""
+    import ctypes
+    import gzip as _gz
+    import zlib
+    from nanotel_amd.io import write_fasta_gz, write_fasta_gz_batch
+    from nanotel_amd.driver import reverse_complement
+    rng = np.random.default_rng(8)
+    alpha = list(b"ACGTACGTACGTNRYKMSWBDHVacgtn-")
+    seqs = [bytes(rng.choice(alpha, int(n)).tolist()) for n in
+            [0, 1, 79, 80, 81, 159, 160, 161, 1000, 50000] + list(rng.integers(1, 5000, 20))]
+    names = [f"read_{i} runid=abc ch={i}".encode() for i in range(len(seqs))]
+    keep = [ctypes.create_string_buffer(x, len(x) or 1) for x in seqs + names]
+    sp = np.array([ctypes.addressof(b) for b in keep[:len(seqs)]], np.uint64)
+    npp = np.array([ctypes.addressof(b) for b in keep[len(seqs):]], np.uint64)
+    sl = np.array([len(x) for x in seqs], np.uint64)
+    nl = np.array([len(x) for x in names], np.uint64)
+    for rc in (False, True):
+        paths = [str(tmp_path / f"c{int(rc)}_{i}.fasta.gz") for i in range(len(seqs))]
+        write_fasta_gz_batch(paths, npp, nl, sp, sl, rc=rc, threads=3)
+        for i, p in enumerate(paths):
+            ref = tmp_path / "ref.fasta.gz"
+            write_fasta_gz(str(ref), names[i].decode(), reverse_complement(seqs[i]) if rc else seqs[i])
+            got = open(p, "rb").read()
+            assert _gz.decompress(got) == _gz.decompress(ref.read_bytes()), (rc, i)
+            assert got[:10] == bytes([0x1F, 0x8B, 8, 0, 0, 0, 0, 0, 0, 3])
+            text = _gz.decompress(got)
+            co = zlib.compressobj(6, zlib.DEFLATED, -15)  # the raw stream: zlib's level 6, memLevel 8
+            assert got[10:-8] == co.compress(text) + co.flush(), (rc, i)
+    with pytest.raises(OSError):
+        write_fasta_gz_batch([str(tmp_path / "no" / "dir" / "x.fasta.gz")], npp[:1], nl[:1], sp[:1], sl[:1])

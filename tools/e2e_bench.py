@@ -89,6 +89,8 @@ def main():
     ap.add_argument("--profile", default="", help="cProfile the summary-only run into this file (text)")
     ap.add_argument("--no-reads-run", action="store_true", help="skip the run that writes reads/*.fasta.gz")
     ap.add_argument("--cleanup", action="store_true", help="delete the input and outputs at the end")
+    ap.add_argument("--gzip-levels", default="6",
+                    help="gzip levels of the reads/*.fasta.gz runs (comma separated; 6 = R's gzfile default)")
     a = ap.parse_args()
     os.makedirs(a.dir, exist_ok=True)
     inp = os.path.join(a.dir, "run" if a.parts > 1 else "reads.fastq" + (".gz" if a.gz else ""))
@@ -110,11 +112,15 @@ def main():
     print("# warm-up run done", file=sys.stderr, flush=True)
     # the first full-size run also grows the pinned staging and device buffers
     # (a long run pays that once): reported, then the steady-state run
-    runs = [("summary_only_first", False, False), ("summary_only", False, False)] + \
-        ([] if a.no_reads_run else [("with_reads_fasta_gz", True, False)])
+    levels = [int(x) for x in a.gzip_levels.split(",")]
+    runs = [("summary_only_first", False, False, None), ("summary_only", False, False, None)]
+    if not a.no_reads_run:
+        runs += [("with_reads_fasta_gz" + ("" if lv == 6 else f"_level{lv}"), True, False, lv) for lv in levels]
     if a.plots:
-        runs.append(("with_reads_and_plots", True, True))
-    for key, write_reads, plot in runs:
+        runs.append(("with_reads_and_plots", True, True, levels[0]))
+    for key, write_reads, plot, level in runs:
+        if level is not None:
+            os.environ["NT_GZIP_LEVEL"] = str(level)
         save = os.path.join(a.dir, "out_" + key)
         t = time.perf_counter()
         st = {}
