@@ -248,6 +248,8 @@ def main():
     ap.add_argument("--n-frac", type=float, default=0.0,
                     help="fraction of reads carrying one N (an exception list entry at a random position): the "
                          "bundle scan takes them, the calling kernel recounts their windows near it")
+    ap.add_argument("--p-tract", type=float, default=0.5,
+                    help="fraction of reads with a telomeric tract (SURVEY §8(d): 0.5; a workload probe)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     args = ap.parse_args()
     if args.gpus < 1:
@@ -331,7 +333,8 @@ def main():
     end = torch.empty(n * 3, dtype=torch.int32, device=dev)
     dens = torch.empty(n * 3, dtype=torch.float64, device=dev)
     flags = torch.empty(n, dtype=torch.uint8, device=dev)
-    sp = synth_params(first_read=rank * n, read_len=L, variant_rate=cfg["variant"], rc_layout=cfg["rc"])
+    sp = synth_params(first_read=rank * n, read_len=L, variant_rate=cfg["variant"], rc_layout=cfg["rc"],
+                      p_tract=args.p_tract)
     nt.synth_device(sp, n, planes.data_ptr())
     nt.uniform_layout_device(n, L, blk_off.data_ptr(), lens.data_ptr(), win_off.data_ptr())
     # --n-frac: reads with one non-ACGT letter (N, Biostrings code 15) each
@@ -472,6 +475,7 @@ def main():
                        "env_knobs": env_knobs(),
                        "device_buffers": ", ".join(sorted(set(alloc_kinds))),
                        **({"reads_with_an_n": round(args.n_frac, 6)} if args.n_frac > 0 else {}),
+                       **({"p_tract": args.p_tract} if args.p_tract != 0.5 else {}),
                        "parallelism": f"dp{world} (read shards)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
