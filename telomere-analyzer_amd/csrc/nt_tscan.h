@@ -235,6 +235,38 @@ struct LTests<CtList<P...>> {
   static constexpr uint32_t kMask = (0u | ... | one<P>());
 };
 
+// Exact matches of a list of TVRs of one length (NanoTel.R:360-393: P3 adds
+// the TVRs' exact matches) with the letters every TVR shares factored out:
+// hit = AND(shared letters) & OR_t AND(t's other letters).  TGAGGG + TTGGGG
+// share T....GGG: 4 bitwise ops a position instead of 7 (two and-chains of
+// six letters and an OR).  Pure bitwise: the same hits as OR_t AND_j.
+template <class List>
+struct TvrShared;
+template <class... P>
+struct TvrShared<CtList<P...>> {
+  template <class D>
+  static constexpr int tt(int j) { return D::kTT[j] & 15; }
+  // bit j: every TVR has the same truth table at letter j
+  static constexpr uint64_t mask() {
+    using D0 = typename CtAt<0, P...>::type;
+    uint64_t m = 0;
+    for (int j = 0; j < D0::kM; ++j)  // (a fold, not a braced list: hiprtc has no <initializer_list>)
+      if (((tt<P>(j) == tt<D0>(j)) && ...)) m |= 1ull << j;
+    return m;
+  }
+  static constexpr uint64_t kMask = mask();
+};
+
+// AND of n words, three at a time (v_bitop3 and3), times an extra word x
+template <int N>
+__device__ __forceinline__ uint32_t and_all(const uint32_t (&q)[N], int n, uint32_t x) {
+  uint32_t r = x;
+  int j = 0;
+  for (; j + 2 <= n; j += 2) r = and3(r, q[j], q[j + 1]);
+  if (j < n) r &= q[j];
+  return r;
+}
+
 // The per-lane pipeline of the walk: position by position, the letter tests
 // (one word per distinct truth table), the hits of the starts whose last
 // letter is the position (exact, <= 1 mismatch; TVRs exact), the sliding-OR
@@ -333,16 +365,34 @@ struct TPipe {
       }
       if constexpr (kNTvr > 0) {  // TVRs (exact): the start x - (kMT - 1)
         constexpr int j0 = x - (kMT - 1);
+        constexpr uint64_t sh = TvrShared<Tvrs>::kMask;  // letters every TVR shares
         uint32_t e = 0u;
         static_for<0, kNTvr>([&](auto ti) {
           using D = typename LAt<Tvrs, decltype(ti)::value>::type;
           uint32_t q[kMT];
+          int nq = 0;
 #pragma unroll
-          for (int j = 0; j < kMT; ++j) q[j] = Ts[D::kTT[j] & 15][j0 + j];
-          uint32_t b0, b1;
-          tcombine<kMT, true>(q, b0, b1);
-          e |= b0;
+          for (int j = 0; j < kMT; ++j)
+            if (!((sh >> j) & 1u)) q[nq++] = Ts[D::kTT[j] & 15][j0 + j];
+          if (nq == 0) {
+            e = 0xFFFFFFFFu;  // (a TVR made of shared letters only: the shared AND is its hit)
+          } else {
+            uint32_t r = q[0];
+            int j = 1;
+            for (; j + 2 <= nq; j += 2) r = and3(r, q[j], q[j + 1]);
+            if (j < nq) e = __builtin_amdgcn_bitop3_b32(r, q[j], e, 0xEA);  // (r & q) | e
+            else e |= r;
+          }
         });
+        {
+          using D0 = typename LAt<Tvrs, 0>::type;
+          uint32_t q[kMT];
+          int nq = 0;
+#pragma unroll
+          for (int j = 0; j < kMT; ++j)
+            if ((sh >> j) & 1u) q[nq++] = Ts[D0::kTT[j] & 15][j0 + j];
+          e = and_all(q, nq, e);
+        }
         at[0][x] = e;
         static_for<1, kST + 1>([&](auto si) {
           constexpr int s = decltype(si)::value;
