@@ -916,10 +916,6 @@ def test_bundle_scan_ragged_packed_batch(L):
     # odd L (the second half window one position short), L = 127 and 170
     # (rows of more than 64 units: two loads a slot; 3 ranges a walk): the bundle scan
     # against the per-read scan of the same device batch on every output
-    import ctypes
-    import torch
-    from nanotel_amd import _lib
-    from nanotel_amd.api import DeviceBundles
     rng = np.random.default_rng(5 + L)
     seqs = []
     for i in range(150):
@@ -929,6 +925,16 @@ def test_bundle_scan_ragged_packed_batch(L):
             a0 = int(rng.integers(0, n_i - 2000))
             s_i[a0:a0 + 1800] = (b"TTAGGG" * 300)[:1800]
         seqs.append(bytes(s_i))
+    _bundle_scan_vs_per_read(seqs, L, 5, min_telomeric=6)
+
+
+def _bundle_scan_vs_per_read(seqs, L, n_bundles, min_telomeric=0):
+    # host-packed reads: the bundle scan against the per-read scan of the same
+    # device batch on every output (every window count of every read and pass)
+    import ctypes
+    import torch
+    from nanotel_amd import _lib
+    from nanotel_amd.api import DeviceBundles
     lib = _lib.lib()
     n = len(seqs)
     ptrs = (ctypes.c_char_p * n)(*seqs)
@@ -943,7 +949,7 @@ def test_bundle_scan_ragged_packed_batch(L):
     nt = _nt(patterns="TTAGGG", subseq_length=L)
     assert nt.tscan
     plan = nt.bundle_plan(ln, blk_off=blk)
-    assert plan.n_bundles == 5 and len(plan.list) == 0
+    assert plan.n_bundles == n_bundles and len(plan.list) == 0
     dev = {k: torch.from_numpy(v).cuda() for k, v in (("planes", planes.view(np.int32)), ("blk", blk.view(np.int64)),
                                                     ("ln", ln.view(np.int32)), ("wo", wo.view(np.int64)))}
     br = torch.from_numpy(plan.bnd_read.view(np.int32)).cuda()
@@ -973,7 +979,29 @@ def test_bundle_scan_ragged_packed_batch(L):
         for p in range(nt.n_pass):
             o = int(wo[r]) * nt.n_pass + p * rows
             assert np.array_equal(got["wc"][o:o + nw], ref["wc"][o:o + nw]), (r, p)
-    assert int(((ref["flags"] & 1) != 0).sum()) > 5
+    assert int(((ref["flags"] & 1) != 0).sum()) >= min_telomeric
+
+
+@pytest.mark.parametrize("L", [100, 37, 127, 170])
+def test_bundle_scan_short_last_half_stripe(L):
+    # bundles whose longest read ends 1..9 windows into its last half stripe
+    # (most of the walk's lanes past every read: DESIGN 4.4 tried a tail walk
+    # for them) and around them, ragged inside each bundle, a telomeric tract
+    # reaching the longest read's end in every other bundle
+    rng = np.random.default_rng(40 + L)
+    tops = [100, 73, 72, 41, 40, 37, 36, 34, 33, 9, 8, 5, 4, 2, 1]  # windows of each bundle's longest read
+    seqs = []
+    for i, t in enumerate(tops):
+        lo = tops[i + 1] * L + 1 if i + 1 < len(tops) else 1
+        hi = t * L
+        lens = [hi] + [int(x) for x in rng.integers(lo, hi + 1, 31)]
+        for j, n_i in enumerate(lens):
+            s_i = bytearray(rng.choice(list(b"ACGT"), n_i).tolist())
+            if j == 0 and i % 2 == 0:
+                k = min(n_i, 40 * L) // 6 * 6
+                s_i[n_i - k:] = (b"TTAGGG" * (k // 6 + 1))[:k]
+            seqs.append(bytes(s_i))
+    _bundle_scan_vs_per_read(seqs, L, len(tops), min_telomeric=4)
 
 
 @pytest.mark.parametrize("L", [100, 170])

@@ -1,7 +1,8 @@
 """The hiprtc sources of the pattern-specialised kernels build on the CPU (no
 GPU needed: hiprtc only drives the compiler): the bundle scan (nt_tscan.h) and
 the calling kernel (nt_call.h) for the Example's TTAGGG and for BASELINE's c4
-set (2 patterns + 2 TVRs, the largest specialised calling kernel).  Catches
+set (2 patterns + 2 TVRs, the largest specialised calling kernel), and the
+bundle scan for an 18-letter pattern (a halo of 17 positions each side).  Catches
 JIT-only failures (hiprtc has no libc headers, only what nt_*.h include) before
 a GPU run; the GPU tests run the same kernels for parity."""
 import importlib.util
@@ -23,6 +24,8 @@ def _tool():
 TTAGGG = "nt::CtPat<6, 8, 8, 1, 4, 4, 4>"
 C4_PATS = "nt::CtPat<6, 8, 8, 1, 4, 4, 4>, nt::CtPat<6, 8, 2, 1, 4, 4, 4>"
 C4_TVRS = "nt::CtPat<6, 8, 4, 1, 4, 4, 4>, nt::CtPat<6, 8, 8, 4, 4, 4, 4>"
+# an 18-letter pattern (TAGGGTTAGGGTTAGGGT): the longest halo the walk has
+LONG = "nt::CtPat<18, 8, 1, 4, 4, 4, 8, 8, 1, 4, 4, 4, 8, 8, 1, 4, 4, 4, 8>"
 
 
 @pytest.mark.skipif(not os.path.exists(HIPRTC), reason="no hiprtc in this image")
@@ -31,6 +34,7 @@ C4_TVRS = "nt::CtPat<6, 8, 4, 1, 4, 4, 4>, nt::CtPat<6, 8, 8, 4, 4, 4, 4>"
     ("call", C4_PATS, C4_TVRS),
     ("tscan", TTAGGG, ""),
     ("tscan", C4_PATS, C4_TVRS),
+    ("tscan", LONG, ""),
 ])
 def test_specialised_kernel_sources_build(kernel, pats, tvrs):
     t = _tool()
