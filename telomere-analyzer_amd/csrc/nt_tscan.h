@@ -788,6 +788,15 @@ struct TsRot {
 // Position -1 of the first window (Biostrings' out-of-bound start) is masked
 // in the prologue; the read ends are not (the calling kernel recounts every
 // read's last window, see the header).
+// Lane conditions as mask words (v_and / v_bitop3) instead of selects
+// (v_cndmask, a fifth of the issue rate at one wave a SIMD:
+// profiles/r06/valu_issue_1w/) in the walk's prologue, the halves' add and the
+// checkpoints: same box, c5 / c50k +2 %, c10k +1.7 % -- but c4 (3 passes)
+// -1.5 % with every variant tried (profiles/r06/ab_masks/), so 2-pass
+// programs only
+template <class TP>
+constexpr bool ts_mask_selects() { return TP::kNP == 2; }
+
 template <class TP, class Pats, class Tvrs>
 struct TWalkerL {
   static constexpr int kL = TP::kL, kLam = TP::kLam;
@@ -796,6 +805,7 @@ struct TWalkerL {
   static constexpr int kNR = (kN + 31) / 32;       // ranges of 32 positions
   static constexpr int kPro = 2 * kLam;            // prologue steps (no counts)
   static constexpr int kIssueAt = kNR >= 2 ? kNR - 2 : 0;  // the range walked after the buffer's last read
+  static constexpr bool kMaskSel = ts_mask_selects<TP>();
   using St = TsStage<kL>;
   typename TPipeSel<TP, Pats, Tvrs>::type pp;
 
@@ -866,6 +876,9 @@ struct TWalkerL {
   __device__ __forceinline__ void walk(const uint2* buf, int w, uint32_t sh, bool first, uint32_t cmask, int rot,
                                        uint32_t (&acc)[3][8], Issue&& issue) {
     pp.init();
+    // position -1 of the read masked by a mask word (an AND), not a select
+    uint32_t fmask = first ? 0u : 0xFFFFFFFFu;
+    if constexpr (kMaskSel) asm volatile("" : "+v"(fmask));
     const uint2* row = buf + w;
     uint32_t plo[kNR][32], phi[kNR][32];
     if constexpr (kNR == 2) {
@@ -894,7 +907,10 @@ struct TWalkerL {
           pp.template run<u1 - u0, !pro, pro, ms>(
               [&](auto ui) {
                 constexpr int i = u0 + decltype(ui)::value, j = i - 32 * r;
-                if constexpr (pro) return make_uint3(lo[j], hi[j], (i < kLam && first) ? 0u : 0xFFFFFFFFu);
+                if constexpr (pro) {
+                  if constexpr (kMaskSel) return make_uint3(lo[j], hi[j], i < kLam ? fmask : 0xFFFFFFFFu);
+                  else return make_uint3(lo[j], hi[j], (i < kLam && first) ? 0u : 0xFFFFFFFFu);
+                }
                 else return make_uint3(lo[j], hi[j], cmask);
               },
               [](auto) {});
@@ -1200,15 +1216,40 @@ __device__ __forceinline__ void tscan_bundles(const NtBatch& B, const NtOut& O, 
               asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
               if (hs + 1 < nhs) fetch(hs + 1);
             });
+        // the halves added: v_permlane32_swap of x with itself gives the lower
+        // half's x in both halves of one result and the upper half's in both
+        // halves of the other, so their sum needs no per-lane select; the sums
+        // go to this half stripe's lanes of the output stripe by a mask
+        // (v_bitop3: a select on a lane condition is a v_cndmask, which
+        // issues at a fifth of the rate at one wave a SIMD, tools/
+        // valu_issue_bench.hip).  An even half stripe leaves the upper lanes
+        // as they were: when no odd one follows, their windows lie past every
+        // read of the bundle (masked bitmask bits, padding counts, no
+        // checkpoint)
+        uint32_t sel = mh == (hs & 1) ? ~0u : 0u;
+        if constexpr (ts_mask_selects<TP>()) asm volatile("" : "+v"(sel));
 #pragma unroll
         for (int p = 0; p < kNP; ++p) {
-          uint32_t x[8];
+          if constexpr (!ts_mask_selects<TP>()) {
+            uint32_t x[8];
 #pragma unroll
-          for (int t = 0; t < 8; ++t) x[t] = xor32(acc[p][t], mh == 0);
-          bitsliced_add(acc[p], x);
+            for (int t = 0; t < 8; ++t) x[t] = xor32(acc[p][t], mh == 0);
+            bitsliced_add(acc[p], x);
 #pragma unroll
-          for (int t = 0; t < 8; ++t)  // (an even half stripe clears the second half: none follows the last)
-            oacc[p][t] = mh == (hs & 1) ? acc[p][t] : ((hs & 1) ? oacc[p][t] : 0u);
+            for (int t = 0; t < 8; ++t)  // (an even half stripe clears the second half: none follows the last)
+              oacc[p][t] = mh == (hs & 1) ? acc[p][t] : ((hs & 1) ? oacc[p][t] : 0u);
+            continue;
+          }
+          uint32_t a[8], x[8];
+#pragma unroll
+          for (int t = 0; t < 8; ++t) {
+            const auto r = __builtin_amdgcn_permlane32_swap(acc[p][t], acc[p][t], false, false);
+            a[t] = r[0];
+            x[t] = r[1];
+          }
+          bitsliced_add(a, x);
+#pragma unroll
+          for (int t = 0; t < 8; ++t) oacc[p][t] = __builtin_amdgcn_bitop3_b32(sel, a[t], oacc[p][t], 0xCA);
         }
       }
       if (!(hs & 1) && hs + 1 < nhs) continue;
@@ -1223,6 +1264,8 @@ __device__ __forceinline__ void tscan_bundles(const NtBatch& B, const NtOut& O, 
       // Every pass's rows are written before one wave_sync and read back
       // after it (one LDS round trip a stripe, not one a pass).
       const int k0 = st * kWave + 32 * mh;  // this lane's first window
+      uint32_t hmask = 0u - (uint32_t)mh;   // (a mask, not a select: see the halves' add)
+      if constexpr (ts_mask_selects<TP>()) asm volatile("" : "+v"(hmask));
       const int nv = m_nw - k0 < 0 ? 0 : (m_nw - k0 > 32 ? 32 : m_nw - k0);  // its windows in the read
       const int fs = st % Aux::kF;          // the stripe's place in the flush buffers
       const int half = (st % Aux::kRS) * 16;  // this stripe's 16 words of a row
@@ -1298,8 +1341,18 @@ __device__ __forceinline__ void tscan_bundles(const NtBatch& B, const NtOut& O, 
         gb = __builtin_amdgcn_udot4(vb.z, 0x01010101u, gb, false);
         gb = __builtin_amdgcn_udot4(vb.w, 0x01010101u, gb, false);
         const uint32_t mine = ga + gb;
-        const uint32_t other = xor32(mine, mh == 0);
-        const uint32_t c0 = run[p] + (mh ? other : 0u);  // before window k0
+        uint32_t c0, both;  // before window k0; both halves' sum
+        if constexpr (ts_mask_selects<TP>()) {
+          // (lower half's sum in both halves of lo2, the upper half's in hi2)
+          const auto r2 = __builtin_amdgcn_permlane32_swap(mine, mine, false, false);
+          const uint32_t lo2 = r2[0], hi2 = r2[1];
+          c0 = run[p] + (lo2 & hmask);
+          both = lo2 + hi2;
+        } else {
+          const uint32_t other = xor32(mine, mh == 0);
+          c0 = run[p] + (mh ? other : 0u);
+          both = mine + other;
+        }
         uint32_t* ckr = ckb + (p * NT_BUNDLE + ms) * 4 * Aux::kF + 4 * fs + 2 * mh;
         ckr[0] = c0;
         ckr[1] = c0 + ga;
@@ -1308,7 +1361,7 @@ __device__ __forceinline__ void tscan_bundles(const NtBatch& B, const NtOut& O, 
         if (mh && st == nst - 1 && 16 * ((k0 >> 4) + 2) == m_nw)
           reinterpret_cast<uint32_t*>(tmask + m_ab + (uint64_t)kNP * aux_nmw(m_nw))[p * aux_nck(m_nw) + (m_nw >> 4)] =
               c0 + mine;
-        run[p] += mine + other;
+        run[p] += both;
       }
       // ---- flush the bitmask words and checkpoints of stripes st0 .. st
       // lane -> (slot, stripe) / (slot, checkpoint): coalesced runs of each

@@ -55,6 +55,9 @@ __global__ void __launch_bounds__(256) kern(uint32_t* out, uint32_t seed) {
   if constexpr (KIND == 23) asm volatile("v_and_b32 %0, %1, %0\n\tv_xor_b32 %0, %2, %0\n\tv_or_b32 %0, %1, %0\n\tv_alignbit_b32 %0, %1, %0, 3" : "+v"(r[i]) : "v"(b), "v"(c)); \
   if constexpr (KIND == 24) asm volatile("v_and_b32 %0, %1, %0\n\tv_xor_b32 %0, %2, %0\n\tv_or_b32 %0, %1, %0\n\tv_and_b32 %0, %2, %0\n\tv_xor_b32 %0, %1, %0\n\tv_or_b32 %0, %2, %0\n\tv_add_u32 %0, %1, %0\n\tv_alignbit_b32 %0, %1, %0, 3" : "+v"(r[i]) : "v"(b), "v"(c)); \
   if constexpr (KIND == 25) { if ((threadIdx.x >> 6) & 1) asm volatile("v_alignbit_b32 %0, %1, %0, 3" : "+v"(r[i]) : "v"(b)); else asm volatile("v_and_b32 %0, %1, %0" : "+v"(r[i]) : "v"(b)); } \
+  if constexpr (KIND == 28) asm volatile("v_perm_b32 %0, %0, %1, %2" : "+v"(r[i]) : "v"(b), "v"(c));            \
+  if constexpr (KIND == 29) asm volatile("v_lshrrev_b64 %0, 3, %0" : "+v"(*(uint64_t*)&r[i & 14]));           \
+  if constexpr (KIND == 30) asm volatile("v_mov_b32 %0, %1" : "=v"(r[i]) : "v"(r[(i + 3) & 15]));              \
   if constexpr (KIND == 26) asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x80\n\tv_lshrrev_b32 %0, 3, %0" : "+v"(r[i]) : "v"(b), "v"(c));
     X16(OP)
 #undef OP
@@ -80,7 +83,8 @@ static const char* kNames[] = {"v_and_b32 (VOP2)",     "v_bitop3_b32 (VOP3)",  "
                                "v_or_b32 (VOP2)", "v_cndmask_b32 (VOP2)", "v_lshlrev_b64", "v_or3_b32",
                                "v_and_or_b32", "v_lshrrev_b32 (VOP2)", "v_alignbyte_b32", "2 v_and + v_alignbit",
                                "v_xor_b32", "v_not_b32 (VOP1)", "3 fast (and xor or)", "3 fast + alignbit",
-                               "7 fast + alignbit", "waves: alignbit | and", "bitop3 + lshrrev", "7 fast x16, then alignbit x16"};
+                               "7 fast + alignbit", "waves: alignbit | and", "bitop3 + lshrrev", "7 fast x16, then alignbit x16",
+                               "v_perm_b32", "v_lshrrev_b64", "v_mov_b32"};
 
 template <int KIND>
 static void run(int cus, uint32_t* out, int wps) {
@@ -113,6 +117,7 @@ int main(int argc, char** argv) {
   if (only < 0 || only == k) run<k>(cus, out, wps);
   RUN(0) RUN(1) RUN(2) RUN(3) RUN(4) RUN(5) RUN(6) RUN(7) RUN(8) RUN(9) RUN(10) RUN(11) RUN(12) RUN(13)
   RUN(14) RUN(15) RUN(16) RUN(17) RUN(18) RUN(19) RUN(20) RUN(21) RUN(22) RUN(23) RUN(24) RUN(25) RUN(26) RUN(27)
+  RUN(28) RUN(29) RUN(30)
   (void)hipFree(out);
   return 0;
 }
