@@ -792,8 +792,9 @@ struct TsRot {
 // (v_cndmask, a fifth of the issue rate at one wave a SIMD:
 // profiles/r06/valu_issue_1w/) in the walk's prologue, the halves' add and the
 // checkpoints: same box, c5 / c50k +2 %, c10k +1.7 % -- but c4 (3 passes)
-// -1.5 % with every variant tried (profiles/r06/ab_masks/), so 2-pass
-// programs only
+// -1.5 % with the halves' add and checkpoints masked, so those are 2-pass
+// programs only; the prologue's mask is every program's (c4 +0.6 %;
+// profiles/r06/ab_masks/)
 template <class TP>
 constexpr bool ts_mask_selects() { return TP::kNP == 2; }
 
@@ -805,7 +806,7 @@ struct TWalkerL {
   static constexpr int kNR = (kN + 31) / 32;       // ranges of 32 positions
   static constexpr int kPro = 2 * kLam;            // prologue steps (no counts)
   static constexpr int kIssueAt = kNR >= 2 ? kNR - 2 : 0;  // the range walked after the buffer's last read
-  static constexpr bool kMaskSel = ts_mask_selects<TP>();
+  static constexpr bool kMaskSel = true;  // (the prologue's mask: every program)
   using St = TsStage<kL>;
   typename TPipeSel<TP, Pats, Tvrs>::type pp;
 

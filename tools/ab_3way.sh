@@ -8,7 +8,7 @@ for i in 1 2; do
  for v in old exp new; do
   for c in ${AB_CONFIGS:-c4 c5}; do
    case $v in old) b=_ab/old/bench.py;; exp) b=_ab/exp/bench.py;; *) b=bench.py;; esac
-   extra=""; [ $c = c4 ] && extra="--reads 2000000"
+   extra=""; case $c in c4|c3) extra="--reads 2000000";; esac
    timeout -k 10 200 python -u $b --config $c $extra --steps 10 --warmup 5 --no-cpu-baseline > gpurun_out/$tag/${v}_${c}_$i.log 2>&1 || exit 1
   done
  done
