@@ -1453,3 +1453,57 @@ def test_use_filter_matches_oracle(cfg):
     bad = [i for i in range(len(seqs)) if bool(keep[i]) != want[i]]
     assert not bad, (len(bad), bad[:5])
     assert 20 < sum(want) < 380
+
+
+# ---- random programs (seeded fuzz): pattern sets of 1-3 patterns of one
+# length (3-12 letters, some IUPAC), optional exact TVRs, subseq_length,
+# min_density, --rc and --check_right_edge drawn at random; reads with tracts
+# of the first pattern (its IUPAC letters resolved to a base of their set).
+# The ahead-of-time kernels for most seeds, the hiprtc bundle scan for a few
+# (each of those builds its own kernel).
+_IUPAC = {"R": "AG", "Y": "CT", "K": "GT", "M": "AC", "S": "CG", "W": "AT", "B": "CGT", "D": "AGT",
+          "H": "ACT", "V": "ACG", "N": "ACGT"}
+
+
+def _rand_pattern(rng, m, iupac):
+    return "".join(rng.choice(list(_IUPAC)) if rng.random() < iupac else "ACGT"[rng.integers(0, 4)]
+                   for _ in range(m))
+
+
+def _fuzz_cfg(seed):
+    rng = np.random.default_rng(1000 + seed)
+    m = int(rng.integers(3, 13))
+    pats = [_rand_pattern(rng, m, 0.15) for _ in range(int(rng.integers(1, 4)))]
+    cfg = dict(patterns=" ".join(pats), subseq_length=int(rng.choice([37, 50, 64, 100, 127, 150])),
+               min_density=float(rng.choice([0.3, 0.5, 0.6, 0.8])))
+    if rng.random() < 0.4:
+        m2 = int(rng.integers(3, 13))
+        cfg["tvr_patterns"] = " ".join(_rand_pattern(rng, m2, 0.0) for _ in range(int(rng.integers(1, 3))))
+    if rng.random() < 0.25:
+        cfg["rc"] = True
+    if rng.random() < 0.2:
+        cfg["check_right_edge"] = True
+    motif = "".join(c if c in "ACGT" else _IUPAC[c][rng.integers(0, len(_IUPAC[c]))] for c in pats[0])
+    if cfg.get("rc"):  # (the reads are scanned reverse-complemented)
+        motif = motif[::-1].translate(str.maketrans("ACGT", "TGCA"))
+    return cfg, motif, rng
+
+
+@pytest.mark.parametrize("seed", range(64))
+def test_fuzz_random_programs(seed):
+    cfg, motif, rng = _fuzz_cfg(seed)
+    jit = seed % 7 == 3  # 9 of the 64 through the hiprtc bundle scan
+    right = cfg.get("check_right_edge", False)
+    seqs = []
+    for i in range(60):
+        # (--check_right_edge: reads of at least one window, the reference's
+        # find_right_telo stops on an empty window table, NanoTel.R:861)
+        n = int(rng.choice([rng.integers(cfg["subseq_length"] // 2 + 1 if right else 1, 600),
+                            rng.integers(600, 8000), rng.integers(8000, 20000)]))
+        seqs.append(_telo_read(rng, n, motif=motif, where=["left", "right", "mid"][i % 3],
+                               tract=(min(n, 3 * len(motif)), max(min(n, 3 * len(motif)), min(n, 4000))),
+                               exc=0.002 if i % 6 == 0 else 0.0))
+    nt = _nt(jit=jit, **cfg)
+    orow = oracle_rows(seqs, cfg["patterns"], tvr=cfg.get("tvr_patterns"), L=cfg["subseq_length"],
+                       min_density=cfg["min_density"], right_edge=right, rc=cfg.get("rc", False))
+    _check_both(nt, seqs, orow)
