@@ -32,6 +32,8 @@ they are not pixel-identical to R's rasteriser.
 import math
 import os
 
+import numpy as np
+
 from . import _psdata as F
 
 # colours (R's colour table, 0-255)
@@ -431,12 +433,18 @@ def render_jpeg(ops, W, H, path, S=3):
             clip = op[1]
         elif kind == "polygon":
             xs, ys, fill, col, st = op[1:]
-            pts = [P(*cl(x, y)) for x, y in zip(xs, ys) if not (math.isnan(x) or math.isnan(y))]
-            if len(pts) >= 3:
+            # (the points clipped and scaled as arrays: the same float64
+            # arithmetic as P(*cl(x, y)) point by point, a fifth of the time)
+            xa, ya = np.asarray(xs, np.float64), np.asarray(ys, np.float64)
+            ok = ~(np.isnan(xa) | np.isnan(ya))
+            xa = np.minimum(np.maximum(xa[ok], clip[0]), clip[2]) * S
+            ya = (H - np.minimum(np.maximum(ya[ok], clip[1]), clip[3])) * S
+            if xa.size >= 3:
+                pts = np.stack((xa, ya), axis=1).ravel().tolist()
                 if fill is not None:
                     dr.polygon(pts, fill=fill)
                 if col is not None:
-                    dr.line(pts + [pts[0]], fill=col, width=width(st), joint="curve")
+                    dr.line(pts + pts[:2], fill=col, width=width(st), joint="curve")
         elif kind == "line":
             x0, y0, x1, y1, col, st = op[1:]
             if inside(x0, y0, x1, y1):
