@@ -1,6 +1,7 @@
 // nt_pack.h -- host-only helpers shared by nt_host.cpp and nt_pack.cpp.
 #pragma once
 #include <stdint.h>
+#include <stdlib.h>
 
 #include <string>
 #include <thread>
@@ -24,11 +25,21 @@ int make_program(const nt_params* prm, NtProgram& P, std::vector<uint32_t>& thr,
 int64_t pack_one(const unsigned char* s, uint64_t n, int rc, uint32_t* out, uint32_t* exc_pos, uint8_t* exc_code);
 NtSynth to_synth(const nt_synth_params* sp);
 
+// Host worker threads: the machine's, at most 16 (a GPU's share of the host
+// on an 8-GPU node), divided among the ranks of a node (one process per GPU)
+inline unsigned pool_threads() {
+  unsigned nt = std::thread::hardware_concurrency();
+  nt = nt == 0 ? 1u : (nt > 16u ? 16u : nt);
+  if (const char* w = std::getenv("LOCAL_WORLD_SIZE")) {
+    const int k = std::atoi(w);
+    if (k > 1) nt = nt / (unsigned)k > 0 ? nt / (unsigned)k : 1u;
+  }
+  return nt;
+}
+
 template <class F>
 void parallel_for(uint64_t n, F&& f) {
-  unsigned nt = std::thread::hardware_concurrency();
-  if (nt == 0) nt = 1;
-  if (nt > 32) nt = 32;
+  const unsigned nt = pool_threads();
   if (n < 64 || nt == 1) {
     for (uint64_t i = 0; i < n; ++i) f(i);
     return;

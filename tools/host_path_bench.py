@@ -56,7 +56,7 @@ def main():
         L.nt_pack_reads(ctypes.cast(ptrs, ctypes.c_void_p), lens.ctypes.data, n, 0, 100, planes.ctypes.data,
                         blk.ctypes.data, ln.ctypes.data, wo.ctypes.data, None, None, None)
         pk.append(time.perf_counter() - t)
-    out = {"reads": n, "read_len": a.read_len, "bases": bases, "host_threads": os.cpu_count()}
+    out = {"reads": n, "read_len": a.read_len, "bases": bases, "host_cpus": os.cpu_count(), "host_threads": min(16, os.cpu_count() or 1)}
     out["pack_only"] = {"seconds": round(min(pk), 4), "Gbases_per_s": round(bases / min(pk) / 1e9, 2)}
     with NanoTel("TTAGGG") as nt:
         for want in (False, True):
