@@ -354,12 +354,14 @@ constexpr size_t kWindow = 64u << 20;  // gzip stream window / index slice (grow
 
 unsigned host_threads() {
   unsigned nt = std::thread::hardware_concurrency();
-  nt = std::max(1u, std::min(nt == 0 ? 1u : nt, 16u));
-  // one process per GPU: the ranks of a node share its cores
+  nt = nt == 0 ? 1u : nt;
+  // one process per GPU: the ranks of a node share its cores; at most 16 a
+  // rank (a GPU's share of the host on the MI355X nodes)
   if (const char* w = std::getenv("LOCAL_WORLD_SIZE")) {
     const int k = atoi(w);
     if (k > 1) nt = std::max(1u, nt / (unsigned)k);
   }
+  nt = std::min(nt, 16u);
   if (const char* v = std::getenv("NT_READER_PARSE_THREADS")) nt = (unsigned)std::max(1, atoi(v));
   return nt;
 }

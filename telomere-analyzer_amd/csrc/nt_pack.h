@@ -25,16 +25,17 @@ int make_program(const nt_params* prm, NtProgram& P, std::vector<uint32_t>& thr,
 int64_t pack_one(const unsigned char* s, uint64_t n, int rc, uint32_t* out, uint32_t* exc_pos, uint8_t* exc_code);
 NtSynth to_synth(const nt_synth_params* sp);
 
-// Host worker threads: the machine's, at most 16 (a GPU's share of the host
-// on an 8-GPU node), divided among the ranks of a node (one process per GPU)
+// Host worker threads: this rank's share of the machine's (one process per
+// GPU: the cores divided among the node's ranks), at most 16 (a GPU's share
+// of the host on the MI355X nodes)
 inline unsigned pool_threads() {
   unsigned nt = std::thread::hardware_concurrency();
-  nt = nt == 0 ? 1u : (nt > 16u ? 16u : nt);
+  if (nt == 0) nt = 1;
   if (const char* w = std::getenv("LOCAL_WORLD_SIZE")) {
     const int k = std::atoi(w);
     if (k > 1) nt = nt / (unsigned)k > 0 ? nt / (unsigned)k : 1u;
   }
-  return nt;
+  return nt > 16u ? 16u : nt;
 }
 
 template <class F>
