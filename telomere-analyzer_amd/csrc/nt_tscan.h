@@ -789,7 +789,8 @@ struct TsRot {
 // in the prologue; the read ends are not (the calling kernel recounts every
 // read's last window, see the header).
 // Lane conditions as mask words (v_and / v_bitop3) instead of selects
-// (v_cndmask, a fifth of the issue rate at one wave a SIMD:
+// (v_cndmask: on a non-VCC SGPR pair ~1.5 issue slots more than other VALU at
+// one wave a SIMD, on VCC a quarter of the rate back to back:
 // profiles/r06/valu_issue_1w/) in the walk's prologue, the halves' add and the
 // checkpoints: same box, c5 / c50k +2 %, c10k +1.7 % -- but c4 (3 passes)
 // -1.5 % with the halves' add and checkpoints masked, so those are 2-pass
@@ -806,7 +807,6 @@ struct TWalkerL {
   static constexpr int kNR = (kN + 31) / 32;       // ranges of 32 positions
   static constexpr int kPro = 2 * kLam;            // prologue steps (no counts)
   static constexpr int kIssueAt = kNR >= 2 ? kNR - 2 : 0;  // the range walked after the buffer's last read
-  static constexpr bool kMaskSel = true;  // (the prologue's mask: every program)
   using St = TsStage<kL>;
   typename TPipeSel<TP, Pats, Tvrs>::type pp;
 
@@ -879,7 +879,7 @@ struct TWalkerL {
     pp.init();
     // position -1 of the read masked by a mask word (an AND), not a select
     uint32_t fmask = first ? 0u : 0xFFFFFFFFu;
-    if constexpr (kMaskSel) asm volatile("" : "+v"(fmask));
+    asm volatile("" : "+v"(fmask));
     const uint2* row = buf + w;
     uint32_t plo[kNR][32], phi[kNR][32];
     if constexpr (kNR == 2) {
@@ -908,10 +908,7 @@ struct TWalkerL {
           pp.template run<u1 - u0, !pro, pro, ms>(
               [&](auto ui) {
                 constexpr int i = u0 + decltype(ui)::value, j = i - 32 * r;
-                if constexpr (pro) {
-                  if constexpr (kMaskSel) return make_uint3(lo[j], hi[j], i < kLam ? fmask : 0xFFFFFFFFu);
-                  else return make_uint3(lo[j], hi[j], (i < kLam && first) ? 0u : 0xFFFFFFFFu);
-                }
+                if constexpr (pro) return make_uint3(lo[j], hi[j], i < kLam ? fmask : 0xFFFFFFFFu);
                 else return make_uint3(lo[j], hi[j], cmask);
               },
               [](auto) {});
