@@ -68,6 +68,8 @@ __global__ void __launch_bounds__(256) kern(uint32_t* out, uint32_t seed) {
   if constexpr (KIND == 34) asm volatile("v_cndmask_b32 %0, %0, %1, vcc\n\tv_and_b32 %0, %1, %0\n\tv_xor_b32 %0, %2, %0\n\tv_or_b32 %0, %1, %0" : "+v"(r[i]) : "v"(b), "v"(c)); \
   if constexpr (KIND == 35) asm volatile("v_cndmask_b32_e64 %0, %0, %1, vcc\n\tv_and_b32 %0, %1, %0\n\tv_xor_b32 %0, %2, %0\n\tv_or_b32 %0, %1, %0" : "+v"(r[i]) : "v"(b), "v"(c)); \
   if constexpr (KIND == 36) asm volatile("v_cndmask_b32_e64 %0, %0, %1, %3\n\tv_and_b32 %0, %1, %0\n\tv_xor_b32 %0, %2, %0\n\tv_or_b32 %0, %1, %0" : "+v"(r[i]) : "v"(b), "v"(c), "s"(lm2)); \
+  if constexpr (KIND == 37) asm volatile("v_cndmask_b32 %0, %0, %1, vcc\n\tv_cndmask_b32 %0, %0, %2, vcc\n\tv_and_b32 %0, %1, %0\n\tv_xor_b32 %0, %2, %0\n\tv_or_b32 %0, %1, %0" : "+v"(r[i]) : "v"(b), "v"(c)); \
+  if constexpr (KIND == 38) asm volatile("v_cndmask_b32_e64 %0, %0, %1, %3\n\tv_cndmask_b32_e64 %0, %0, %2, %3\n\tv_and_b32 %0, %1, %0\n\tv_xor_b32 %0, %2, %0\n\tv_or_b32 %0, %1, %0" : "+v"(r[i]) : "v"(b), "v"(c), "s"(lm2)); \
   if constexpr (KIND == 26) asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x80\n\tv_lshrrev_b32 %0, 3, %0" : "+v"(r[i]) : "v"(b), "v"(c));
     X16(OP)
 #undef OP
@@ -96,7 +98,8 @@ static const char* kNames[] = {"v_and_b32 (VOP2)",     "v_bitop3_b32 (VOP3)",  "
                                "7 fast + alignbit", "waves: alignbit | and", "bitop3 + lshrrev", "7 fast x16, then alignbit x16",
                                "v_perm_b32", "v_lshrrev_b64", "v_mov_b32", "v_cndmask e64 SGPR-pair mask",
                                "cndmask(s) + 3 fast", "bitop3 select + 3 fast",
-                               "cndmask(vcc, e32) + 3 fast", "cndmask(vcc, e64) + 3 fast", "cndmask(s, v_cmp'd) + 3 fast"};
+                               "cndmask(vcc, e32) + 3 fast", "cndmask(vcc, e64) + 3 fast", "cndmask(s, v_cmp'd) + 3 fast",
+                               "2 cndmask(vcc) + 3 fast", "2 cndmask(s) + 3 fast"};
 
 template <int KIND>
 static void run(int cus, uint32_t* out, int wps) {
@@ -111,7 +114,7 @@ static void run(int cus, uint32_t* out, int wps) {
   (void)hipEventSynchronize(b);
   float ms = 0.f;
   (void)hipEventElapsedTime(&ms, a, b);
-  const double per = KIND == 32 || KIND == 33 || KIND >= 34 ? 4.0 : KIND == 9 || KIND == 26 ? 2.0 : (KIND == 19 || KIND == 22 ? 3.0 : (KIND == 23 ? 4.0 : (KIND == 24 || KIND == 27 ? 8.0 : 1.0)));
+  const double per = KIND >= 37 ? 5.0 : KIND == 32 || KIND == 33 || KIND >= 34 ? 4.0 : KIND == 9 || KIND == 26 ? 2.0 : (KIND == 19 || KIND == 22 ? 3.0 : (KIND == 23 ? 4.0 : (KIND == 24 || KIND == 27 ? 8.0 : 1.0)));
   const double instr_per_simd = (double)wps * 16.0 * ITER * per;
   const double cyc = ms * 1e-3 * 2.4e9;
   printf("%-24s waves/SIMD %d  %8.3f ms  %.3f wave-instr/cycle/SIMD\n", kNames[KIND], wps, ms, instr_per_simd / cyc);
@@ -129,7 +132,7 @@ int main(int argc, char** argv) {
   if (only < 0 || only == k) run<k>(cus, out, wps);
   RUN(0) RUN(1) RUN(2) RUN(3) RUN(4) RUN(5) RUN(6) RUN(7) RUN(8) RUN(9) RUN(10) RUN(11) RUN(12) RUN(13)
   RUN(14) RUN(15) RUN(16) RUN(17) RUN(18) RUN(19) RUN(20) RUN(21) RUN(22) RUN(23) RUN(24) RUN(25) RUN(26) RUN(27)
-  RUN(28) RUN(29) RUN(30) RUN(31) RUN(32) RUN(33) RUN(34) RUN(35) RUN(36)
+  RUN(28) RUN(29) RUN(30) RUN(31) RUN(32) RUN(33) RUN(34) RUN(35) RUN(36) RUN(37) RUN(38)
   (void)hipFree(out);
   return 0;
 }
