@@ -789,8 +789,8 @@ struct TsRot {
 // in the prologue; the read ends are not (the calling kernel recounts every
 // read's last window, see the header).
 // Lane conditions as mask words (v_and / v_bitop3) instead of selects
-// (v_cndmask: on a non-VCC SGPR pair ~1.5 issue slots more than other VALU at
-// one wave a SIMD, on VCC a quarter of the rate back to back:
+// (v_cndmask: on a non-VCC SGPR pair ~0.8-1.5 issue slots more than other VALU
+// at one wave a SIMD, on VCC a quarter of the rate in a chain of selects:
 // profiles/r06/valu_issue_1w/) in the walk's prologue, the halves' add and the
 // checkpoints: same box, c5 / c50k +2 %, c10k +1.7 % -- but c4 (3 passes)
 // -1.5 % with the halves' add and checkpoints masked, so those are 2-pass
